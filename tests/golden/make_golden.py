@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures by running the REFERENCE implementation (build container only).
+
+Run from the repo root:  python tests/golden/make_golden.py [--ref /root/reference]
+
+It imports the read-only reference (`/root/reference`) with the stub recipe of SURVEY.md §8(c)
+(off-path third-party deps replaced by empty modules, no bytecode written into the reference tree),
+fills every model with the seeded weights of `flamed-tts_amd/flamed/utils/seeded_init.py`
+(weights are NOT committed: they are regenerated bit-identically from (seed, key, shape)), runs the
+hot-path functions and stores inputs + outputs as small .npz files next to this script.
+The reference never leaves this container; only these data files are committed.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import yaml  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+
+
+def _stub(name, **attrs):
+    m = types.ModuleType(name)
+    m.__dict__.update(attrs)
+    sys.modules[name] = m
+    return m
+
+
+def install_stubs():
+    _stub("unidecode", unidecode=lambda s: s)
+    _stub("inflect", engine=lambda: None)
+    _stub("pyworld")
+    _stub("soundfile")
+    lib = _stub("librosa")
+    lib.filters = _stub("librosa.filters", mel=lambda **k: None)
+    ta = _stub("torchaudio")
+    ta.functional = _stub("torchaudio.functional", pitch_shift=None)
+    _stub("tgt")
+    _stub("wandb")
+    _stub("g2p_en", G2p=object)
+    _stub("transformers", get_cosine_schedule_with_warmup=None)
+    _stub("omegaconf", DictConfig=dict, OmegaConf=None)
+    _stub("lightning", LightningModule=torch.nn.Module, LightningDataModule=object)
+    _stub("pytorch_lightning")
+    _stub("pytorch_lightning.utilities", rank_zero_only=lambda f: f)
+
+
+def load_filler():
+    path = os.path.join(REPO, "flamed-tts_amd", "flamed", "utils", "seeded_init.py")
+    spec = importlib.util.spec_from_file_location("seeded_init", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_cfgs(ref):
+    with open(os.path.join(ref, "configs", "prior.yaml")) as f:
+        prior = yaml.safe_load(f)
+    with open(os.path.join(ref, "configs", "prob.yaml")) as f:
+        prob = yaml.safe_load(f)
+    prob["sigma_min"] = float(prob["sigma_min"])
+    prior["variance_adaptor"]["sigma_min"] = float(prior["variance_adaptor"]["sigma_min"])
+    prior["device"] = "cpu"
+    prob["device"] = "cpu"
+    return prior, prob
+
+
+def save(name, **arrays):
+    out = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        out[k] = np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(f"wrote {name}.npz  ({', '.join(f'{k}{tuple(v.shape)}' for k, v in out.items())})")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+    install_stubs()
+    sys.path.insert(0, args.ref)
+    filler = load_filler()
+    torch.set_num_threads(8)
+
+    from flamed.models.synthesizer.prob_generator import ProbGenerator, SimpleMLPAdaLN
+    from flamed.models.synthesizer.pva import PVA, LengthRegulator, ProbabilisticModule
+    from flamed.models.facodec import FACodecDecoder
+    from flamed.models.facodec.alias_free_torch import Activation1d
+    from flamed.models.facodec.facodec import SnakeBeta
+    from flamed.models import flamed as flamed_mod
+
+    prior_cfg, prob_cfg = load_cfgs(args.ref)
+    SEED = 20251205
+    manifest = {}
+
+    # ---------------- denoiser: tiny dims (weights regenerated from the filler) -----------------
+    with torch.inference_mode():
+        tiny = SimpleMLPAdaLN(in_channels=16, model_channels=64, out_channels=16, spk_dim=32,
+                              num_res_blocks=2, convnext_kernel=31, convnext_stride=1, convnext_padding=15,
+                              convnext_expand=1, convnext_groups=None).eval()
+        tiny.load_state_dict(filler.fill_state_dict(tiny.state_dict(), SEED))
+        manifest["den_tiny"] = {k: list(v.shape) for k, v in tiny.state_dict().items()}
+        g = torch.Generator().manual_seed(1)
+        x = torch.randn(2, 40, 16, generator=g)
+        c = torch.randn(2, 32, generator=g)
+        t1 = torch.tensor([[0.3]])
+        tB = torch.rand(2, 40, generator=g)
+        v1 = tiny(x, t1, c)
+        vB = tiny(x, tB, c)
+        # 4-step Euler trajectory
+        xt = x.clone()
+        traj = []
+        ts = torch.linspace(0, 1, 5)
+        for i in range(1, 5):
+            xt = xt + 0.25 * tiny(xt, ts[i - 1].unsqueeze(0).unsqueeze(1), c)
+            traj.append(xt.clone())
+        save("den_tiny", x=x, c=c, t1=t1, tB=tB, v1=v1, vB=vB, traj=torch.stack(traj), seed=SEED)
+
+    # ---------------- denoiser + ProbGenerator.sample: full dims ---------------------------------
+    with torch.inference_mode():
+        pg = ProbGenerator(prob_cfg).eval()
+        sd = {"prob_generator." + k: v for k, v in pg.state_dict().items()}
+        sd = filler.fill_state_dict(sd, SEED)
+        pg.load_state_dict({k[len("prob_generator."):]: v for k, v in sd.items()})
+        manifest["prob_generator"] = {k: list(v.shape) for k, v in sd.items()}
+        den = pg.denoiser
+        g = torch.Generator().manual_seed(2)
+        x = torch.randn(1, 64, 256, generator=g)
+        c = torch.randn(1, 256, generator=g)
+        t1 = torch.tensor([[0.25]])
+        v1 = den(x, t1, c)
+        xB = torch.randn(2, 48, 256, generator=g)
+        cB = torch.randn(2, 256, generator=g)
+        tB = torch.rand(2, 48, generator=g)
+        vB = den(xB, tB, cB)
+        t_mid = torch.tensor([[0.75]])
+        vB1 = den(xB, t_mid, cB)
+        save("den_full", x=x, c=c, t1=t1, v1=v1, xB=xB, cB=cB, tB=tB, vB=vB, t_mid=t_mid, vB1=vB1, seed=SEED)
+
+        # ProbGenerator.sample with cond fold, padded batch, global-RNG noise
+        cond = torch.randn(2, 6, 48, 384, generator=g)
+        spk = torch.randn(2, 256, generator=g)
+        lens = torch.tensor([48, 33])
+        mask = ~(torch.arange(48)[None, :] >= lens[:, None]).unsqueeze(-1)
+        torch.manual_seed(1234)
+        noise = torch.randn((2, 48, 256))
+        torch.manual_seed(1234)
+        lat = pg.sample(cond, spk, mask, nfe=4, temperature=0.3)
+        cf = pg.cond_downsampling(pg.quantizer_encoding(cond), mask)
+        save("prob_sample", cond=cond, spk=spk, lens=lens, noise=noise, latents=lat, cond_fold=cf,
+             nfe=4, temperature=0.3, rng_seed=1234, seed=SEED)
+
+    # ---------------- PVA: duration / silence generators + LR -----------------------------------
+    with torch.inference_mode():
+        pva = PVA(prior_cfg["variance_adaptor"]).eval()
+        sd = {"prior_generator.pva." + k: v for k, v in pva.state_dict().items()}
+        sd = filler.fill_state_dict(sd, SEED)
+        pva.load_state_dict({k[len("prior_generator.pva."):]: v for k, v in sd.items()})
+        manifest["pva"] = {k: list(v.shape) for k, v in sd.items()}
+        g = torch.Generator().manual_seed(3)
+        enc = torch.randn(2, 20, 192, generator=g)
+        src_len = torch.tensor([20, 13])
+        src_mask = torch.arange(20)[None, :] >= src_len[:, None]
+        # one ProbabilisticModule call
+        xt = torch.randn(2, 20, generator=g)
+        v_dur = pva.duration_generator(xt, enc, torch.tensor(0.5), src_mask)
+        v_sil = pva.sil_generator(xt, enc, torch.tensor(0.125), src_mask)
+        # full sample; capture final log-durations by replaying the loop with the reference modules
+        nfe, temp, rs = 8, 0.3, 77
+        torch.manual_seed(rs)
+        dn = torch.randn((2, 20))
+        sn = torch.randn((2, 20))
+        ts = torch.linspace(0, 1, nfe + 1)
+        d, s = dn * temp, sn * temp
+        for i in range(1, nfe + 1):
+            d = d + (1 / nfe) * pva.duration_generator(d, enc, ts[i - 1], src_mask)
+            s = s + (1 / nfe) * pva.sil_generator(s, enc, ts[i - 1], src_mask)
+        torch.manual_seed(rs)
+        x_lr, tgt_len = pva.sample(enc, src_len, src_mask, nfe=nfe, temperature=temp)
+        ed = torch.exp(d) - 1
+        es = torch.exp(s) - 1
+        margin = float(torch.min(torch.cat([(ed - ed.floor() - 0.5).abs().flatten(),
+                                            (es - es.floor() - 0.5).abs().flatten()])))
+        save("pva", enc=enc, src_len=src_len, xt=xt, v_dur=v_dur, v_sil=v_sil, noise_dur=dn, noise_sil=sn,
+             dur_final=d, sil_final=s, x_lr=x_lr, tgt_len=tgt_len, nfe=nfe, temperature=temp, rng_seed=rs,
+             round_margin=margin, seed=SEED)
+        print("pva rounding margin", margin)
+
+        # LengthRegulator integer cases (explicit durations, incl. zeros, padding, truncation)
+        lr = LengthRegulator()
+        cases = {}
+        rng = np.random.default_rng(5)
+        for ci, (B, L, H, max_len) in enumerate([(3, 7, 4, None), (2, 11, 3, 40), (2, 9, 2, 5), (1, 1, 5, None),
+                                                 (4, 16, 6, None)]):
+            xx = torch.from_numpy(rng.standard_normal((B, L, H)).astype(np.float32))
+            pd = torch.from_numpy(rng.integers(0, 6, (B, L)).astype(np.float32))
+            sdur = torch.from_numpy(rng.integers(0, 3, (B, L)).astype(np.float32))
+            sl = torch.from_numpy(rng.integers(1, L + 1, (B,)).astype(np.int64))
+            out, tl = lr(xx, pd, sdur, sl, max_len)
+            cases[f"c{ci}_x"] = xx
+            cases[f"c{ci}_pd"] = pd
+            cases[f"c{ci}_sd"] = sdur
+            cases[f"c{ci}_sl"] = sl
+            cases[f"c{ci}_max"] = np.int64(-1 if max_len is None else max_len)
+            cases[f"c{ci}_out"] = out
+            cases[f"c{ci}_tl"] = tl
+        save("lr_cases", n=np.int64(5), **cases)
+
+    # ---------------- FaCodec decoder ------------------------------------------------------------
+    with torch.inference_mode():
+        dec = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, ngf=32, up_ratios=[5, 5, 4, 2],
+                             vq_num_q_c=2, vq_num_q_p=1, vq_num_q_r=3, vq_dim=256, codebook_dim=8,
+                             codebook_size_prosody=10, codebook_size_content=10, codebook_size_residual=10,
+                             use_gr_x_timbre=True, use_gr_residual_f0=True, use_gr_residual_phone=True).eval()
+        sd = filler.fill_state_dict(dec.state_dict(), SEED)
+        dec.load_state_dict(sd)
+        manifest["facodec_decoder"] = {k: list(v.shape) for k, v in sd.items()}
+        filters = {k.replace(".", "_"): v for k, v in sd.items() if k.endswith(".filter")
+                   and k.startswith("model.1.block.0")}
+        g = torch.Generator().manual_seed(4)
+        lat1 = torch.randn(1, 256, 8, generator=g)
+        spk1 = torch.randn(1, 256, generator=g)
+        wav1 = dec.inference(lat1, spk1)
+        lat2 = torch.randn(2, 256, 5, generator=g)
+        spk2 = torch.randn(2, 256, generator=g)
+        wav2 = dec.inference(lat2, spk2)
+        save("facodec", lat1=lat1, spk1=spk1, wav1=wav1, lat2=lat2, spk2=spk2, wav2=wav2, seed=SEED, **filters)
+
+        # standalone Activation1d (SnakeBeta, log-scale) on an odd length
+        act = Activation1d(activation=SnakeBeta(16, alpha_logscale=True))
+        asd = filler.fill_state_dict(act.state_dict(), SEED)
+        act.load_state_dict(asd)
+        xa = torch.randn(2, 16, 37, generator=g)
+        ya = act(xa)
+        save("act1d", x=xa, y=ya, alpha=asd["act.alpha"], beta=asd["act.beta"],
+             up_filter=asd["upsample.filter"], down_filter=asd["downsample.lowpass.filter"])
+
+    # ---------------- CPU RNG stream (global generator, reference draw order) --------------------
+    torch.manual_seed(0)
+    r1 = torch.randn((2, 5))
+    r2 = torch.randn((2, 5))
+    r3 = torch.randn((2, 3, 4))
+    save("rng", r1=r1, r2=r2, r3=r3)
+
+    _ = flamed_mod  # imported to prove the top-level module graph imports with the stubs
+    with open(os.path.join(HERE, "state_dict_manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=0, sort_keys=True)
+    print("wrote state_dict_manifest.json")
+
+
+if __name__ == "__main__":
+    main()
