@@ -1,0 +1,110 @@
+// Common types, error plumbing and small device helpers for the Flamed MI355X (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+namespace fl {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- error reporting (thread-local last error, C-ABI flamed_last_error) ----
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+enum Status : int {
+  kOk = 0,
+  kBadArg = 1001,      // invalid dims / null pointers / unsupported config
+  kNoWorkspace = 1002, // workspace too small
+  kHip = 1003,         // HIP runtime failure (message has details)
+};
+
+#define FL_HIP(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      ::fl::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return ::fl::kHip;                                                                 \
+    }                                                                                    \
+  } while (0)
+
+#define FL_REQUIRE(cond, ...)        \
+  do {                               \
+    if (!(cond)) {                   \
+      ::fl::set_error(__VA_ARGS__);  \
+      return ::fl::kBadArg;          \
+    }                                \
+  } while (0)
+
+#define FL_LAUNCH_CHECK()                                                                  \
+  do {                                                                                     \
+    hipError_t e_ = hipGetLastError();                                                     \
+    if (e_ != hipSuccess) {                                                                \
+      ::fl::set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return ::fl::kHip;                                                                   \
+    }                                                                                      \
+  } while (0)
+
+// ---- device helpers ----
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float wave_sum16(float v) {  // sum over the 16 lanes sharing lane>>4
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Chan et al. parallel combine of (count, mean, M2) partials.
+__device__ __forceinline__ void chan_combine(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  float nn = n + nb;
+  if (nn <= 0.f) return;
+  float d = meanb - mean;
+  mean += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+template <typename DT> struct DTraits;
+template <> struct DTraits<bf16> {
+  static constexpr int EPC = 8;  // elements per 16-byte chunk
+  static constexpr int kCode = 1;
+};
+template <> struct DTraits<float> {
+  static constexpr int EPC = 4;
+  static constexpr int kCode = 0;
+};
+
+// 16-byte chunk of DT built from EPC floats.
+template <typename DT> __device__ __forceinline__ uint4 pack_chunk(const float* v);
+template <> __device__ __forceinline__ uint4 pack_chunk<float>(const float* v) {
+  uint4 r;
+  r.x = __float_as_uint(v[0]);
+  r.y = __float_as_uint(v[1]);
+  r.z = __float_as_uint(v[2]);
+  r.w = __float_as_uint(v[3]);
+  return r;
+}
+template <> __device__ __forceinline__ uint4 pack_chunk<bf16>(const float* v) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (bf16)v[j];
+  return *reinterpret_cast<uint4*>(&b);
+}
+
+template <typename DT> __device__ __forceinline__ void store_val(DT* p, float v) { *p = (DT)v; }
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+}  // namespace fl

@@ -1,0 +1,98 @@
+"""ctypes binding of the gfx950 C-ABI library (include/flamed_hip.h -> flamed/_native/libflamed_hip.so).
+
+The GPU path REQUIRES this library: every HIP entry point raises RuntimeError when it is missing or
+a call fails — there is no silent fallback to PyTorch ops.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FLAMED_HIP_LIB") or os.path.join(_HERE, "_native", "libflamed_hip.so")
+
+_lock = threading.Lock()
+_lib = None
+
+c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+P = c_void_p  # device pointers and opaque handles
+
+# name -> (restype, argtypes); mirrors include/flamed_hip.h
+SIGNATURES = {
+    "flamed_last_error": (ctypes.c_char_p, []),
+    "flamed_version": (c_int, []),
+    "flamed_den_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(P)]),
+    "flamed_den_destroy": (c_int, [P]),
+    "flamed_den_num_weights": (c_int, [P]),
+    "flamed_den_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_den_adaln_workspace_size": (c_size_t, [P, c_int, c_int]),
+    "flamed_den_adaln": (c_int, [P, P, c_int, P, c_int, P, P, c_int, P, P, c_size_t, P]),
+    "flamed_den_workspace_size": (c_size_t, [P, c_int, c_int]),
+    "flamed_den_velocity": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
+    "flamed_den_step": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, c_size_t, P]),
+    "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
+}
+
+FLAMED_F32, FLAMED_BF16 = 0, 1
+DTYPES = {"f32": FLAMED_F32, "fp32": FLAMED_F32, "float32": FLAMED_F32, "bf16": FLAMED_BF16, "bfloat16": FLAMED_BF16}
+
+
+def lib():
+    """Load (once) and return the C-ABI library; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"Flamed HIP extension not found at {LIB_PATH}. Build it with "
+                    "`make -C flamed-tts_amd/csrc` (or `python -c 'import __graft_entry__ as g; g.build()'`).")
+            so = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(so, name, None)
+                if fn is None:
+                    continue
+                fn.restype = res
+                fn.argtypes = args
+            _lib = so
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().flamed_last_error()
+        raise RuntimeError(f"{what} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def stream_ptr(device: torch.device | None = None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def dtype_code(name: str) -> int:
+    try:
+        return DTYPES[name]
+    except KeyError as e:
+        raise ValueError(f"unknown HIP compute dtype {name!r}; use one of {sorted(DTYPES)}") from e
+
+
+class Workspace:
+    """Grow-only device scratch buffer (stable pointer between calls of the same size)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        nbytes = max(int(nbytes), 256)
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != torch.device(device):
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        return self.buf

@@ -6,6 +6,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "flamed-tts_amd")
 GOLDEN = os.path.join(HERE, "golden")
 
 from flamed.utils.seeded_init import fill_state_dict  # noqa: E402
