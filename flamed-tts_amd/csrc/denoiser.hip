@@ -608,59 +608,64 @@ static DenWs carve(Den* d, void* ws, int B, int T) {
 // One velocity evaluation (+ Euler update when vout == nullptr).
 template <typename DT, int BM, int BN, int KCH>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
-                         const DenWs& w, hipStream_t st) {
+                         const DenWs& w, hipStream_t st, int only = -1) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const int NT = H / BN;
   DT* G = reinterpret_cast<DT*>(w.G);
   DT* U = reinterpret_cast<DT*>(w.U);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
-  TRY((launch_gemm<BM, BN, KCH, DT>(LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
-  for (int i = 0; i < d->NB; ++i) {
+#define K_(cls) if (only < 0 || only == (cls))
+  K_(0) TRY((launch_gemm<BM, BN, KCH, DT>(LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
+  for (int i = 0; i < (only < 0 ? d->NB : 1); ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div};
-    TRY((launch_dwconv_gn<DT, true, 31>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, G, B, T, st)));
-    TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{G, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
-    TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+    K_(1) TRY((launch_dwconv_gn<DT, true, 31>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, G, B, T, st)));
+    K_(2) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{G, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    K_(3) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
                                       EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
                                       M, H, H, st)));
-    TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
+    K_(4) TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
                                       EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
-    TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
+    K_(5) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
                                       EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
   ModRef mc{mf, mf + H, MS, mod_div};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div};
   const DenBlockW& F = d->fin;
+  if (only >= 0 && only != 6) return kOk;
+  if (only < 0) {
   TRY((launch_dwconv_gn<DT, false, 31>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, F.gnw, F.gnb, G, B, T, st)));
   TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{G, H}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                     EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
                                     M, H, H, st)));
+  }
   LoadConv3LN<DT> lo{w.X, H, w.S1, NT, BN, 1e-6f, mo, T};
   if (vout) {
     TRY((launch_gemm<BM, BN, KCH, DT>(lo, (const DT*)d->wout, 3 * H, EpiBiasAct<float, 0>{d->bout, vout, C}, M, C, 3 * H, st)));
   } else {
     TRY((launch_gemm<BM, BN, KCH, DT>(lo, (const DT*)d->wout, 3 * H, EpiEuler{d->bout, xt, C, dt}, M, C, 3 * H, st)));
   }
+#undef K_
 #undef TRY
   return kOk;
 }
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
-                    hipStream_t st) {
+                    hipStream_t st, int only = -1) {
   DenWs w = carve(d, ws, B, T);
   const int M = B * T;
   const bool big = M >= 4096;
   if (d->dt == FLAMED_BF16) {
-    return big ? den_step_impl<bf16, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st)
-               : den_step_impl<bf16, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
+    return big ? den_step_impl<bf16, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only)
+               : den_step_impl<bf16, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only);
   }
-  return big ? den_step_impl<float, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st)
-             : den_step_impl<float, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
+  return big ? den_step_impl<float, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only)
+             : den_step_impl<float, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only);
 }
 
 }  // namespace fl
@@ -728,6 +733,38 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   }
   FL_HIP(hipGraphLaunch(d->gexec, st));
   return kOk;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
+                                       size_t ws_bytes, int iters, float* ms_out, hipStream_t st) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && d->dev && xt && mods && ws && ms_out && iters > 0, "flamed_den_time_kernels: bad args");
+  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
+    set_error("flamed_den_time_kernels: workspace too small");
+    return kNoWorkspace;
+  }
+  hipEvent_t e0, e1;
+  FL_HIP(hipEventCreate(&e0));
+  FL_HIP(hipEventCreate(&e1));
+  int rc = kOk;
+  for (int cls = 0; cls < FLAMED_DEN_KERNEL_CLASSES && rc == kOk; ++cls) {
+    rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st, cls);  // warm
+    if (rc) break;
+    FL_HIP(hipEventRecord(e0, st));
+    for (int i = 0; i < iters && rc == kOk; ++i) rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st, cls);
+    FL_HIP(hipEventRecord(e1, st));
+    FL_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    FL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    ms_out[cls] = ms / iters;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
 }
 
 }  // extern "C"

@@ -34,6 +34,7 @@ SIGNATURES = {
     "flamed_den_velocity": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
     "flamed_den_step": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, c_size_t, P]),
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
+    "flamed_den_time_kernels": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
 }
 
 FLAMED_F32, FLAMED_BF16 = 0, 1

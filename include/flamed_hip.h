@@ -87,6 +87,14 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t stream);
 
+/* Diagnostic: average device time (ms, HIP events on `stream`) of each kernel class of one Euler
+ * step, each launched `iters` times in isolation: 0 proj_in GEMM, 1 dwconv+GroupNorm, 2 conv_2 GEMM
+ * +GELU, 3 conv_3 GEMM+gated residual, 4 LN/mod+mlp.0 GEMM+SiLU, 5 mlp.2 GEMM+gated residual,
+ * 6 conv_out k3 GEMM+Euler update.  Clobbers xt and the workspace (pass scratch copies). */
+enum { FLAMED_DEN_KERNEL_CLASSES = 7 };
+FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
+                                       size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
