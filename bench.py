@@ -31,8 +31,10 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 import yaml  # noqa: E402
 
-KERNEL_NAMES = ["proj_in_gemm", "dwconv_groupnorm", "conv2_gemm_gelu", "conv3_gemm_resid", "lnmod_mlp0_gemm_silu",
-                "mlp2_gemm_resid", "conv_out_k3_gemm_euler"]
+KERNEL_NAMES = ["proj_in_gemm", "lnmod_dwconv_gnpartials", "gn_finalize", "gnapply_conv2_gemm_gelu",
+                "conv3_gemm_gated_resid", "lnmod_mlp0_gemm_silu", "mlp2_gemm_gated_resid", "lnmod_conv_out_gemm",
+                "conv_out_combine_euler"]
+N_CLASSES = len(KERNEL_NAMES)
 HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md chip table (spec)
 MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}   # dense peaks
 
@@ -54,23 +56,29 @@ def parse():
 
 
 def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int):
-    """Algorithmic (bytes, flops) per launch of each kernel class, and launches per Euler step."""
+    """Algorithmic (bytes, flops) per launch of each kernel class, and launches per Euler step.
+    Bytes = every operand read once + every output written once."""
     M = B * T
     NT = H // 64
+    TS = (T + 63) // 64
     stats = M * NT * 8
     if cls == 0:
         return M * C * 4 + H * C * es + M * H * 4 + stats, 2 * M * H * C, 1
     if cls == 1:
-        return M * H * 4 + stats + M * H * es + 2 * B * H * 4, 2 * 31 * M * H, NB + 1
+        return M * H * 4 + stats + M * H * 4 + B * TS * H * 12, 2 * 31 * M * H, NB + 1
     if cls == 2:
-        return 2 * M * H * es + H * H * es, 2 * M * H * H, NB + 1
+        return B * TS * H * 12 + B * H * 8, 10 * B * TS * H, NB + 1
     if cls == 3:
-        return M * H * es + H * H * es + 2 * M * H * 4 + 2 * stats, 2 * M * H * H, NB + 1
+        return M * H * 4 + B * H * 8 + H * H * es + M * H * es, 2 * M * H * H, NB + 1
     if cls == 4:
-        return M * H * 4 + stats + H * H * es + M * H * es, 2 * M * H * H, NB
+        return M * H * es + H * H * es + 2 * M * H * 4 + 2 * stats, 2 * M * H * H, NB + 1
     if cls == 5:
+        return M * H * 4 + stats + H * H * es + M * H * es, 2 * M * H * H, NB
+    if cls == 6:
         return M * H * es + H * H * es + 2 * M * H * 4 + stats, 2 * M * H * H, NB
-    return M * H * 4 + stats + C * 3 * H * es + 2 * M * C * 4, 2 * M * C * 3 * H, 1
+    if cls == 7:
+        return M * H * 4 + stats + 3 * C * H * es + M * 3 * C * 4, 2 * M * 3 * C * H, 1
+    return M * 3 * C * 4 + 2 * M * C * 4, 4 * M * C, 1
 
 
 def main():
@@ -139,12 +147,12 @@ def main():
         mods = hip.adaln(ts[:1], spk, torch.zeros(B, dtype=torch.int32, device=dev), r.to(torch.int32))
         ws = nat.Workspace().get(L.flamed_den_workspace_size(hip.handle, B, T), dev)
         import ctypes
-        ms = (ctypes.c_float * 7)()
+        ms = (ctypes.c_float * N_CLASSES)()
         nat.check(L.flamed_den_time_kernels(hip.handle, nat.ptr(xs), nat.ptr(mods), B, T, nat.ptr(ws), ws.numel(),
                                             args.kernel_iters, ms, nat.stream_ptr(dev)), "flamed_den_time_kernels")
     es = 2 if args.dtype == "bf16" else 4
     kernels = []
-    for cls in range(7):
+    for cls in range(N_CLASSES):
         nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
         t = ms[cls] * 1e-3
         kernels.append({"name": KERNEL_NAMES[cls], "us": round(ms[cls] * 1e3, 2), "per_step": per_step,

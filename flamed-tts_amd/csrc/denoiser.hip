@@ -78,61 +78,6 @@ struct LoadLNMod {
   }
 };
 
-// FinalLayer conv_out: k=3, pad=1 over T of each utterance; source rows LN(no affine)+modulated.
-// K index = tap*H + c (weights re-ordered tap-major at load).
-template <typename DT>
-struct LoadConv3LN {
-  const float* __restrict__ x;
-  int H;
-  const float* __restrict__ S;
-  int NT, tw;
-  float eps;
-  ModRef mod;
-  int T;
-  static constexpr int EPC = DTraits<DT>::EPC;
-  struct Raw { float v[EPC], s[EPC], h[EPC]; int src; };
-  static constexpr int stat_rows(int BM) { return BM + 2; }
-  __device__ void prologue(int bm, int BM, int M, float* st) const {
-    for (int r = threadIdx.x; r < BM + 2; r += blockDim.x) {
-      int m = bm - 1 + r;
-      m = m < 0 ? 0 : (m < M ? m : M - 1);
-      row_stats_from_partials(S, m, NT, tw, eps, st[2 * r], st[2 * r + 1]);
-    }
-  }
-  __device__ Raw issue(int m, int k) const {
-    Raw r;
-    int tap = k / H, c = k - tap * H;
-    int t = m % T + tap - 1;
-    r.src = (t >= 0 && t < T) ? m + tap - 1 : -1;
-    if (r.src >= 0) {
-      const float* px = x + (size_t)r.src * H + c;
-      size_t mo = (size_t)(r.src / mod.div) * mod.ms + c;
-#pragma unroll
-      for (int j = 0; j < EPC; j += 4) {
-        float4 a = ld4(px + j), s = ld4(mod.sc + mo + j), h = ld4(mod.sh + mo + j);
-        r.v[j] = a.x; r.v[j + 1] = a.y; r.v[j + 2] = a.z; r.v[j + 3] = a.w;
-        r.s[j] = s.x; r.s[j + 1] = s.y; r.s[j + 2] = s.z; r.s[j + 3] = s.w;
-        r.h[j] = h.x; r.h[j + 1] = h.y; r.h[j + 2] = h.z; r.h[j + 3] = h.w;
-      }
-    }
-    return r;
-  }
-  template <typename D>
-  __device__ uint4 finish(const Raw& r, int, int, const float* st, int bm) const {
-    float o[EPC];
-    if (r.src < 0) {
-#pragma unroll
-      for (int j = 0; j < EPC; ++j) o[j] = 0.f;
-    } else {
-      int i = r.src - (bm - 1);
-      const float mean = st[2 * i], rstd = st[2 * i + 1];
-#pragma unroll
-      for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - mean) * rstd) * (1.0f + r.s[j]) + r.h[j];
-    }
-    return pack_chunk<D>(o);
-  }
-};
-
 // AdaLN input: A[r][k] = SiLU(TE[tidx[r]][k] + CE[sidx[r]][k])   (fp32 path)
 struct LoadAdaY {
   const float* __restrict__ te;
@@ -225,138 +170,177 @@ struct EpiEuler {  // xt = xt + dt * (acc + b)   (prob_generator.py:445)
   __device__ void store_stats(int, int, float, float) const {}
 };
 
-// ------------------------------ K2a: LN+mod -> depthwise conv -> GroupNorm(T) ------------------------------
-// grid (H/CG, B); one workgroup owns CG channels of one utterance for ALL T frames, so the GroupNorm
-// statistics over T (prob_generator.py:89, GroupNorm(H,H)) are exact in-workgroup reductions and the
-// conv output never leaves LDS.
-constexpr int kDwTC = 64;  // frames per staging chunk
+// ------------------------------ K2a: LN+mod -> depthwise conv (+ GroupNorm partials) ------------------------------
+// grid (H/64, ceil(T/64), B): one workgroup = 64 frames x 64 channels of one utterance.  It stages the
+// LN+AdaLN-modulated input rows (64 + 2*15 halo) in LDS, runs the depthwise k31 conv (reference
+// prob_generator.py:81-88, zero padding at the utterance edges), writes the raw conv output D (fp32)
+// and per-channel (count, mean, M2) partials of this frame chunk.  GroupNorm(H,H) statistics over the
+// whole T axis (:89) are finished by gn_finalize; the normalisation itself is applied in the conv_2
+// GEMM's A-operand loader (LoadGN).
+constexpr int kDwCG = 64, kDwTC = 64;
 
-template <int CG, int KS>
-struct DwSmem {
-  static constexpr int HALO = KS / 2;
-  static constexpr int RG = 256 / CG;
-  static size_t bytes(int T) {
-    return (size_t)T * CG * 4 + (size_t)(kDwTC + 2 * HALO) * CG * 4 + (kDwTC + 2 * HALO) * 8 + (size_t)RG * CG * 12 + CG * 8;
-  }
-};
-
-template <typename DT, bool AFF, int CG, int KS>
-__global__ __launch_bounds__(256) void dwconv_gn_kernel(const float* __restrict__ X, int H, const float* __restrict__ S,
-                                                        int NT, int tw, float eps_ln, ModRef mod,
-                                                        const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                        const float* __restrict__ dww, const float* __restrict__ dwb,
-                                                        const float* __restrict__ gnw, const float* __restrict__ gnb,
-                                                        float eps_gn, DT* __restrict__ G, int T) {
-  using SMD = DwSmem<CG, KS>;
-  constexpr int HALO = SMD::HALO, RG = SMD::RG, RPT = kDwTC / RG, SR = kDwTC + 2 * HALO;
-  static_assert(kDwTC % RG == 0, "chunk/rowgroup mismatch");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* dbuf = reinterpret_cast<float*>(smem);            // T x CG
-  float* hs = dbuf + (size_t)T * CG;                         // SR x CG
-  float* rs = hs + SR * CG;                                  // SR x 2
-  float* red = rs + SR * 2;                                  // RG x CG x 3
-  float* gnp = red + RG * CG * 3;                            // CG x 2
-
+template <bool AFF, int KS>
+__global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restrict__ X, int H, const float* __restrict__ S,
+                                                           int NT, int tw, float eps_ln, ModRef mod,
+                                                           const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                           const float* __restrict__ dww, const float* __restrict__ dwb,
+                                                           float* __restrict__ D, float* __restrict__ GP, int T, int TS) {
+  constexpr int HALO = KS / 2, SR = kDwTC + 2 * HALO, RG = 256 / kDwCG, RPT = kDwTC / RG, WIN = RPT + KS - 1;
+  __shared__ float hs[SR * kDwCG];
+  __shared__ float rs[SR * 2];
+  __shared__ float red[RG * kDwCG * 3];
   const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * CG;
-  const int b = blockIdx.y;
-  const int cl = tid % CG, rg = tid / CG;
-  const int c = c0 + cl;
-
+  const int c0 = blockIdx.x * kDwCG, ts = blockIdx.y, b = blockIdx.z;
+  const int t0 = ts * kDwTC;
+  if (tid < SR) {
+    int t = t0 - HALO + tid;
+    if (t >= 0 && t < T) row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rs[2 * tid], rs[2 * tid + 1]);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < SR * kDwCG; idx += 256) {
+    int r = idx / kDwCG, cc = idx - r * kDwCG;
+    int t = t0 - HALO + r;
+    float v = 0.f;
+    if (t >= 0 && t < T) {
+      size_t m = (size_t)b * T + t;
+      float xh = (X[m * H + c0 + cc] - rs[2 * r]) * rs[2 * r + 1];
+      if constexpr (AFF) xh = xh * lnw[c0 + cc] + lnb[c0 + cc];
+      size_t mo = (m / mod.div) * mod.ms + c0 + cc;
+      v = xh * (1.0f + mod.sc[mo]) + mod.sh[mo];
+    }
+    hs[idx] = v;
+  }
+  __syncthreads();
+  const int cl = tid % kDwCG, rg = tid / kDwCG, c = c0 + cl;
   float w[KS];
 #pragma unroll
   for (int j = 0; j < KS; ++j) w[j] = dww[(size_t)c * KS + j];
+  float win[WIN];
+#pragma unroll
+  for (int j = 0; j < WIN; ++j) win[j] = hs[(rg * RPT + j) * kDwCG + cl];
   const float bias = dwb[c];
-
-  float n_run = 0.f, mean_run = 0.f, m2_run = 0.f;
-  for (int t0 = 0; t0 < T; t0 += kDwTC) {
-    for (int r = tid; r < SR; r += 256) {
-      int t = t0 - HALO + r;
-      if (t >= 0 && t < T) row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rs[2 * r], rs[2 * r + 1]);
-    }
-    __syncthreads();
-    for (int idx = tid; idx < SR * CG; idx += 256) {
-      int r = idx / CG, cc = idx - r * CG;
-      int t = t0 - HALO + r;
-      float v = 0.f;
-      if (t >= 0 && t < T) {
-        size_t m = (size_t)b * T + t;
-        float xh = (X[m * H + c0 + cc] - rs[2 * r]) * rs[2 * r + 1];
-        size_t mo = (m / mod.div) * mod.ms + c0 + cc;
-        if constexpr (AFF) xh = xh * lnw[c0 + cc] + lnb[c0 + cc];
-        v = xh * (1.0f + mod.sc[mo]) + mod.sh[mo];
-      }
-      hs[idx] = v;
-    }
-    __syncthreads();
-    float vals[RPT];
-    float cn = 0.f, cs = 0.f;
+  float vals[RPT];
+  float cn = 0.f, cs = 0.f;
 #pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      int tl = rg * RPT + q;
-      float a = bias;
+  for (int q = 0; q < RPT; ++q) {
+    float a = bias;
 #pragma unroll
-      for (int j = 0; j < KS; ++j) a += w[j] * hs[(tl + j) * CG + cl];
-      vals[q] = a;
-      if (t0 + tl < T) {
-        dbuf[(size_t)(t0 + tl) * CG + cl] = a;
-        cn += 1.f;
-        cs += a;
-      }
+    for (int j = 0; j < KS; ++j) a += w[j] * win[q + j];
+    vals[q] = a;
+    int t = t0 + rg * RPT + q;
+    if (t < T) {
+      D[((size_t)b * T + t) * H + c] = a;
+      cn += 1.f;
+      cs += a;
     }
-    if (cn > 0.f) {
-      float cm = cs / cn, c2 = 0.f;
-#pragma unroll
-      for (int q = 0; q < RPT; ++q)
-        if (t0 + rg * RPT + q < T) {
-          float d = vals[q] - cm;
-          c2 += d * d;
-        }
-      chan_combine(n_run, mean_run, m2_run, cn, cm, c2);
-    }
-    __syncthreads();
   }
-  red[(rg * CG + cl) * 3 + 0] = n_run;
-  red[(rg * CG + cl) * 3 + 1] = mean_run;
-  red[(rg * CG + cl) * 3 + 2] = m2_run;
+  float cm = cn > 0.f ? cs / cn : 0.f, c2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q)
+    if (t0 + rg * RPT + q < T) {
+      float d = vals[q] - cm;
+      c2 += d * d;
+    }
+  red[(rg * kDwCG + cl) * 3 + 0] = cn;
+  red[(rg * kDwCG + cl) * 3 + 1] = cm;
+  red[(rg * kDwCG + cl) * 3 + 2] = c2;
   __syncthreads();
-  if (tid < CG) {
+  if (tid < kDwCG) {
     float n = 0.f, mu = 0.f, m2 = 0.f;
-    for (int g = 0; g < RG; ++g) chan_combine(n, mu, m2, red[(g * CG + tid) * 3], red[(g * CG + tid) * 3 + 1], red[(g * CG + tid) * 3 + 2]);
-    gnp[2 * tid] = mu;
-    gnp[2 * tid + 1] = 1.0f / sqrtf(m2 / (float)T + eps_gn);
-  }
-  __syncthreads();
-  for (int idx = tid; idx < T * CG; idx += 256) {
-    int t = idx / CG, cc = idx - t * CG;
-    float g = ((dbuf[idx] - gnp[2 * cc]) * gnp[2 * cc + 1]) * gnw[c0 + cc] + gnb[c0 + cc];
-    store_val<DT>(G + ((size_t)b * T + t) * H + c0 + cc, g);
+#pragma unroll
+    for (int g = 0; g < RG; ++g) chan_combine(n, mu, m2, red[(g * kDwCG + tid) * 3], red[(g * kDwCG + tid) * 3 + 1], red[(g * kDwCG + tid) * 3 + 2]);
+    float* o = GP + (((size_t)b * TS + ts) * H + c0 + tid) * 3;
+    o[0] = n; o[1] = mu; o[2] = m2;
   }
 }
 
-template <typename DT, bool AFF, int KS>
-static int launch_dwconv_gn(const float* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw,
-                            const float* lnb, const float* dww, const float* dwb, const float* gnw, const float* gnb,
-                            DT* G, int B, int T, hipStream_t st) {
-  const size_t budget = 150 * 1024;
-  auto go = [&](auto cgc) -> int {
-    constexpr int CG = decltype(cgc)::value;
-    size_t bytes = DwSmem<CG, KS>::bytes(T);
-    auto kern = dwconv_gn_kernel<DT, AFF, CG, KS>;
-    static bool attr = false;
-    if (!attr) {
-      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
-    hipLaunchKernelGGL(kern, dim3(H / CG, B), dim3(256), bytes, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, 1e-5f, G, T);
+// GroupNorm(H,H) statistics over all T frames of each (utterance, channel): GNS[b][c] = (mean, rstd).
+__global__ void gn_finalize_kernel(const float* __restrict__ GP, float* __restrict__ GNS, int H, int T, int TS, float eps) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  int b = blockIdx.y;
+  if (c >= H) return;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int ts = 0; ts < TS; ++ts) {
+    const float* p = GP + (((size_t)b * TS + ts) * H + c) * 3;
+    chan_combine(n, mu, m2, p[0], p[1], p[2]);
+  }
+  GNS[((size_t)b * H + c) * 2] = mu;
+  GNS[((size_t)b * H + c) * 2 + 1] = 1.0f / sqrtf(m2 / (float)T + eps);
+}
+
+template <bool AFF>
+static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw,
+                               const float* lnb, const float* dww, const float* dwb, float* D, float* GP, float* GNS,
+                               int B, int T, hipStream_t st, int part) {
+  FL_REQUIRE(H % kDwCG == 0 && H % 256 == 0, "dwconv: H=%d must be a multiple of 256", H);
+  const int TS = (T + kDwTC - 1) / kDwTC;
+  if (part != 2) {
+    hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
+                       mod, lnw, lnb, dww, dwb, D, GP, T, TS);
     FL_LAUNCH_CHECK();
-    return kOk;
-  };
-  FL_REQUIRE(H % 32 == 0, "dwconv_gn: H=%d must be a multiple of 32", H);
-  if (DwSmem<32, KS>::bytes(T) <= budget && B * (H / 32) >= 128) return go(std::integral_constant<int, 32>());
-  if (DwSmem<16, KS>::bytes(T) <= budget) return go(std::integral_constant<int, 16>());
-  if (DwSmem<8, KS>::bytes(T) <= budget) return go(std::integral_constant<int, 8>());
-  FL_REQUIRE(false, "dwconv_gn: T=%d frames too long for the LDS-resident GroupNorm (max ~4500)", T);
+  }
+  if (part != 1) {
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(H / 256, B), dim3(256), 0, st, GP, GNS, H, T, TS, 1e-5f);
+    FL_LAUNCH_CHECK();
+  }
+  return kOk;
+}
+
+// conv_2 A operand: GroupNorm applied on the fly, A = ((D - mean) * rstd) * gn_w + gn_b.
+template <typename DT>
+struct LoadGN {
+  const float* __restrict__ D;
+  int H;
+  const float* __restrict__ gns;
+  const float* __restrict__ gnw;
+  const float* __restrict__ gnb;
+  int T;
+  static constexpr int EPC = DTraits<DT>::EPC;
+  struct Raw { float v[EPC], mu[EPC], rs[EPC], w[EPC], b[EPC]; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    Raw r;
+    const float* pd = D + (size_t)m * H + k;
+    const float* pg = gns + ((size_t)(m / T) * H + k) * 2;
+#pragma unroll
+    for (int j = 0; j < EPC; j += 4) {
+      float4 a = ld4(pd + j), w = ld4(gnw + k + j), bb = ld4(gnb + k + j);
+      float4 g0 = ld4(pg + 2 * j), g1 = ld4(pg + 2 * j + 4);
+      r.v[j] = a.x; r.v[j + 1] = a.y; r.v[j + 2] = a.z; r.v[j + 3] = a.w;
+      r.w[j] = w.x; r.w[j + 1] = w.y; r.w[j + 2] = w.z; r.w[j + 3] = w.w;
+      r.b[j] = bb.x; r.b[j + 1] = bb.y; r.b[j + 2] = bb.z; r.b[j + 3] = bb.w;
+      r.mu[j] = g0.x; r.rs[j] = g0.y; r.mu[j + 1] = g0.z; r.rs[j + 1] = g0.w;
+      r.mu[j + 2] = g1.x; r.rs[j + 2] = g1.y; r.mu[j + 3] = g1.z; r.rs[j + 3] = g1.w;
+    }
+    return r;
+  }
+  template <typename Dt>
+  __device__ uint4 finish(const Raw& r, int, int, const float*, int) const {
+    float o[EPC];
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - r.mu[j]) * r.rs[j]) * r.w[j] + r.b[j];
+    return pack_chunk<Dt>(o);
+  }
+};
+
+// FinalLayer conv_out (k=3, pad=1) from the tap-stacked GEMM Y[m] = [W_0; W_1; W_2] x_mod[m]:
+// v[t] = b + Y0[t-1] + Y1[t] + Y2[t+1] within each utterance; then xt += dt*v (or v_out = v).
+__global__ void conv3_combine_kernel(const float* __restrict__ Y, const float* __restrict__ bias, float* xt,
+                                     float* __restrict__ vout, int M, int T, int C, float dt) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)M * C) return;
+  int m = idx / C, n = idx - (size_t)m * C;
+  int t = m % T;
+  const size_t ld = 3 * (size_t)C;
+  float v = bias[n] + Y[m * ld + C + n];
+  if (t > 0) v += Y[(m - 1) * ld + n];
+  if (t < T - 1) v += Y[(m + 1) * ld + 2 * C + n];
+  if (vout) {
+    vout[idx] = v;
+  } else {
+    xt[idx] = __fadd_rn(xt[idx], __fmul_rn(dt, v));
+  }
 }
 
 // ------------------------------ AdaLN helpers ------------------------------
@@ -382,9 +366,9 @@ __global__ void copy_kernel_f32(const float* __restrict__ src, float* __restrict
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = src[i];
 }
-// conv weight (N, Cin, KT) -> (N, KT, Cin) in DT
+// conv weight (N, Cin, KT) -> tap-stacked rows (KT, N, Cin) in DT
 template <typename DT>
-__global__ void reorder_taps_kernel(const float* __restrict__ src, DT* __restrict__ dst, int N, int Cin, int KT) {
+__global__ void stack_taps_kernel(const float* __restrict__ src, DT* __restrict__ dst, int N, int Cin, int KT) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t total = (size_t)N * Cin * KT;
   if (i >= total) return;
@@ -392,7 +376,7 @@ __global__ void reorder_taps_kernel(const float* __restrict__ src, DT* __restric
   size_t t = i / KT;
   int c = t % Cin;
   int n = t / Cin;
-  store_val<DT>(dst + ((size_t)n * KT + k) * Cin + c, src[i]);
+  store_val<DT>(dst + ((size_t)k * N + n) * Cin + c, src[i]);
 }
 
 // ------------------------------ handle ------------------------------
@@ -422,6 +406,38 @@ struct Den {
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct DenWs {
+  float* X;    // residual stream, M x H
+  float* S0;   // LN partials, M x (H/64) x 2
+  float* S1;
+  float* D;    // depthwise conv output, M x H fp32
+  void* U;     // GEMM intermediate, M x H (DT)
+  float* GP;   // GroupNorm chunk partials, B x TS x H x 3
+  float* GNS;  // GroupNorm (mean, rstd), B x H x 2
+  float* Y;    // conv_out tap-stacked GEMM output, M x 3C
+};
+
+static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
+  size_t M = (size_t)B * T;
+  size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
+  size_t NTmax = d->H / 64;
+  size_t TS = (T + 63) / 64;
+  size_t sizes[8] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
+                     8 * (size_t)B * d->H, 12 * M * d->C};
+  size_t off = 0;
+  void* ptrs[8];
+  for (int i = 0; i < 8; ++i) {
+    ptrs[i] = base ? (char*)base + off : nullptr;
+    off += align256(sizes[i]);
+  }
+  if (w) {
+    w->X = (float*)ptrs[0]; w->S0 = (float*)ptrs[1]; w->S1 = (float*)ptrs[2]; w->D = (float*)ptrs[3];
+    w->U = ptrs[4]; w->GP = (float*)ptrs[5]; w->GNS = (float*)ptrs[6]; w->Y = (float*)ptrs[7];
+  }
+  return off;
+}
+static size_t den_ws_bytes(const Den* d, int B, int T) { return den_ws_layout(d, B, T, nullptr, nullptr); }
 
 }  // namespace fl
 
@@ -526,9 +542,9 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     F.w2 = base + o_fin; F.w3 = base + o_fin + es * H * H;
     size_t n = (size_t)C * H * 3;
     if (d->dt == FLAMED_BF16)
-      hipLaunchKernelGGL(reorder_taps_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, st, fw[10], reinterpret_cast<bf16*>(base + o_out), C, H, 3);
+      hipLaunchKernelGGL(stack_taps_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, st, fw[10], reinterpret_cast<bf16*>(base + o_out), C, H, 3);
     else
-      hipLaunchKernelGGL(reorder_taps_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, st, fw[10], reinterpret_cast<float*>(base + o_out), C, H, 3);
+      hipLaunchKernelGGL(stack_taps_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, st, fw[10], reinterpret_cast<float*>(base + o_out), C, H, 3);
     FL_LAUNCH_CHECK();
     d->wout = base + o_out; d->bout = fw[11];
   }
@@ -573,82 +589,60 @@ FLAMED_API int flamed_den_adaln(flamed_den_t h, const float* t_vals, int n_t, co
 FLAMED_API size_t flamed_den_workspace_size(flamed_den_t h, int B, int T) {
   Den* d = reinterpret_cast<Den*>(h);
   if (!d) return 0;
-  size_t M = (size_t)B * T;
-  size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
-  size_t NTmax = d->H / 64;
-  return align256(4 * M * d->H) + 2 * align256(8 * M * NTmax) + 2 * align256(es * M * d->H);
+  return den_ws_bytes(d, B, T);
 }
 
 }  // extern "C"
 
 namespace fl {
 
-struct DenWs {
-  float* X;
-  float* S0;
-  float* S1;
-  void* G;
-  void* U;
-};
-
-static DenWs carve(Den* d, void* ws, int B, int T) {
-  size_t M = (size_t)B * T;
-  size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
-  size_t NTmax = d->H / 64;
-  char* p = (char*)ws;
-  DenWs w;
-  w.X = (float*)p; p += align256(4 * M * d->H);
-  w.S0 = (float*)p; p += align256(8 * M * NTmax);
-  w.S1 = (float*)p; p += align256(8 * M * NTmax);
-  w.G = p; p += align256(es * M * d->H);
-  w.U = p;
-  return w;
-}
-
-// One velocity evaluation (+ Euler update when vout == nullptr).
+// One velocity evaluation (+ Euler update when vout == nullptr).  `only` >= 0 launches only the
+// kernel class `only` (diagnostic timing, see flamed_den_time_kernels).
 template <typename DT, int BM, int BN, int KCH>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
                          const DenWs& w, hipStream_t st, int only = -1) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const int NT = H / BN;
-  DT* G = reinterpret_cast<DT*>(w.G);
   DT* U = reinterpret_cast<DT*>(w.U);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls) if (only < 0 || only == (cls))
   K_(0) TRY((launch_gemm<BM, BN, KCH, DT>(LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
-  for (int i = 0; i < (only < 0 ? d->NB : 1); ++i) {
+  const int nb = only < 0 ? d->NB : 1;
+  for (int i = 0; i < nb; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div};
-    K_(1) TRY((launch_dwconv_gn<DT, true, 31>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, G, B, T, st)));
-    K_(2) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{G, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
-    K_(3) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
-                                      EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
-                                      M, H, H, st)));
-    K_(4) TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
-                                      EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
-    K_(5) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
-                                      EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
+    K_(1) TRY((launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
+    K_(2) TRY((launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
+    K_(3) TRY((launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
+                                            EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    K_(4) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+                                            EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
+                                            M, H, H, st)));
+    K_(5) TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
+                                            EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
+    K_(6) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
+                                            EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
   ModRef mc{mf, mf + H, MS, mod_div};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div};
   const DenBlockW& F = d->fin;
-  if (only >= 0 && only != 6) return kOk;
   if (only < 0) {
-  TRY((launch_dwconv_gn<DT, false, 31>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, F.gnw, F.gnb, G, B, T, st)));
-  TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{G, H}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
-  TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
-                                    EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
-                                    M, H, H, st)));
+    TRY((launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 0)));
+    TRY((launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+    TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
+                                      EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
+                                      M, H, H, st)));
   }
-  LoadConv3LN<DT> lo{w.X, H, w.S1, NT, BN, 1e-6f, mo, T};
-  if (vout) {
-    TRY((launch_gemm<BM, BN, KCH, DT>(lo, (const DT*)d->wout, 3 * H, EpiBiasAct<float, 0>{d->bout, vout, C}, M, C, 3 * H, st)));
-  } else {
-    TRY((launch_gemm<BM, BN, KCH, DT>(lo, (const DT*)d->wout, 3 * H, EpiEuler{d->bout, xt, C, dt}, M, C, 3 * H, st)));
+  K_(7) TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr}, (const DT*)d->wout, H,
+                                          EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
+  K_(8) {
+    size_t n = (size_t)M * C;
+    hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt);
+    FL_LAUNCH_CHECK();
   }
 #undef K_
 #undef TRY
@@ -657,7 +651,8 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
                     hipStream_t st, int only = -1) {
-  DenWs w = carve(d, ws, B, T);
+  DenWs w;
+  den_ws_layout(d, B, T, ws, &w);
   const int M = B * T;
   const bool big = M >= 4096;
   if (d->dt == FLAMED_BF16) {

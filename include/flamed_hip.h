@@ -88,10 +88,12 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
                                 size_t ws_bytes, int use_graph, hipStream_t stream);
 
 /* Diagnostic: average device time (ms, HIP events on `stream`) of each kernel class of one Euler
- * step, each launched `iters` times in isolation: 0 proj_in GEMM, 1 dwconv+GroupNorm, 2 conv_2 GEMM
- * +GELU, 3 conv_3 GEMM+gated residual, 4 LN/mod+mlp.0 GEMM+SiLU, 5 mlp.2 GEMM+gated residual,
- * 6 conv_out k3 GEMM+Euler update.  Clobbers xt and the workspace (pass scratch copies). */
-enum { FLAMED_DEN_KERNEL_CLASSES = 7 };
+ * step, each launched `iters` times in isolation: 0 proj_in GEMM, 1 LN/mod+depthwise conv (+GN
+ * partials), 2 GroupNorm finalize, 3 GN-apply+conv_2 GEMM+GELU, 4 conv_3 GEMM+gated residual,
+ * 5 LN/mod+mlp.0 GEMM+SiLU, 6 mlp.2 GEMM+gated residual, 7 LN/mod+conv_out tap-stacked GEMM,
+ * 8 conv_out tap combine + Euler update.  ms_out must hold FLAMED_DEN_KERNEL_CLASSES floats.
+ * Clobbers xt and the workspace (pass scratch copies). */
+enum { FLAMED_DEN_KERNEL_CLASSES = 9 };
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                        size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);
 
