@@ -1,0 +1,379 @@
+// PVA duration / silence flow-matching generators + integer length regulator on gfx950.
+// Reference: flamed/models/synthesizer/pva.py:9-41 (SinusoidalPosEmb, TimeEmbedding), :88-116
+// (PVA.sample Euler loop), :125-166 (LengthRegulator.LR), :173-238 (ProbabilisticModule),
+// :241-284 (Conv); flamed/utils/tools.py:91-99 (get_mask_from_lengths), :299-317 (pad).
+//
+// Per Euler step and per net (dur, sil), M = B*L phoneme rows, all exact fp32 (f32 MFMA = fp32 FMA
+// chains) so the rounded integer durations match the reference:
+//   conv1 GEMM  A[m][tap*192+c] = P[src][c] + w0[c]*xt[src] + temb_s[c]  (proj + time embedding
+//               folded in the loader; P = enc.W[:,1:]^T + b precomputed once)  -> +b, ReLU, LN partials
+//   conv2 GEMM  A[m][tap*384+c] = LN1(R1[src])[c]                           -> +b, ReLU
+//   head        LN2 + Linear(384->1) + masked_fill + Euler update, one wave per row
+// The length regulator turns the final log-durations into frame counts (clamp(round(exp(d)-1),0),
+// pva.py:111-112), builds the interleaved phone/silence repeat prefix sums, and gathers the frames.
+#include "flamed_hip.h"
+#include "gemm.hpp"
+
+#include <vector>
+
+namespace fl {
+
+// SinusoidalPosEmb (pva.py:9-22), scale 1000, [sin, cos], frequency denominator (half-1).
+__global__ void pos_emb_kernel(const float* __restrict__ t, int R, int dim, float* __restrict__ F) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= R * dim) return;
+  int half = dim / 2;
+  int r = idx / dim, j = idx - r * dim;
+  int jj = j < half ? j : j - half;
+  const float negemb = (float)(-9.210340371976184 / (double)(half - 1));
+  float f = expf((float)jj * negemb);
+  float a = (1000.0f * t[r]) * f;
+  F[idx] = j < half ? sinf(a) : cosf(a);
+}
+
+// conv weight (N, Cin, KT) -> (N, KT, Cin) fp32 (K index = tap*Cin + c)
+__global__ void taps_major_kernel(const float* __restrict__ src, float* __restrict__ dst, int N, int Cin, int KT) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t total = (size_t)N * Cin * KT;
+  if (i >= total) return;
+  int k = i % KT;
+  size_t t = i / KT;
+  int c = t % Cin;
+  int n = t / Cin;
+  dst[((size_t)n * KT + k) * Cin + c] = src[i];
+}
+
+// proj weight (D, D+1): column 0 -> w0[D], columns 1.. -> We[D][D]
+__global__ void split_proj_kernel(const float* __restrict__ src, float* __restrict__ w0, float* __restrict__ we, int D) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= D * (D + 1)) return;
+  int r = i / (D + 1), c = i - r * (D + 1);
+  if (c == 0) w0[r] = src[i];
+  else we[(size_t)r * D + c - 1] = src[i];
+}
+
+// conv1 A operand: out0[src] = P[src] + w0 * xt[src] + temb (zero outside the utterance)
+struct LoadDurIn {
+  const float* __restrict__ P;
+  const float* __restrict__ w0;
+  const float* __restrict__ xt;
+  const float* __restrict__ temb;
+  int Cin;
+  int L;
+  struct Raw { float v[4]; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    Raw r;
+    int tap = k / Cin, c = k - tap * Cin;
+    int l = m % L + tap - 1;
+    if (l < 0 || l >= L) {
+      r.v[0] = r.v[1] = r.v[2] = r.v[3] = 0.f;
+      return r;
+    }
+    int src = m + tap - 1;
+    float4 p = ld4(P + (size_t)src * Cin + c), w = ld4(w0 + c), te = ld4(temb + c);
+    float x = xt[src];
+    r.v[0] = (p.x + w.x * x) + te.x;
+    r.v[1] = (p.y + w.y * x) + te.y;
+    r.v[2] = (p.z + w.z * x) + te.z;
+    r.v[3] = (p.w + w.w * x) + te.w;
+    return r;
+  }
+  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
+};
+
+// LN2 + Linear(F->1) + masked_fill(mask, 0) + Euler update; one wave per row.
+template <int F>
+__global__ __launch_bounds__(256) void dur_head_kernel(const float* __restrict__ R2, const float* __restrict__ g,
+                                                       const float* __restrict__ b, const float* __restrict__ wl,
+                                                       const float* __restrict__ bl, const uint8_t* __restrict__ mask,
+                                                       float* xt, int M, float dt) {
+  constexpr int PER = F / 64;
+  int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (m >= M) return;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = R2[(size_t)m * F + lane + 64 * j];
+    s += v[j];
+  }
+  float mean = wave_sum64(s) / (float)F;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    float d = v[j] - mean;
+    q += d * d;
+  }
+  float rstd = 1.0f / sqrtf(wave_sum64(q) / (float)F + 1e-5f);
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    int c = lane + 64 * j;
+    float y = ((v[j] - mean) * rstd) * g[c] + b[c];
+    dot += y * wl[c];
+  }
+  dot = wave_sum64(dot);
+  if (lane == 0) {
+    float vel = mask[m] ? 0.f : dot + bl[0];
+    xt[m] = __fadd_rn(xt[m], __fmul_rn(dt, vel));
+  }
+}
+
+struct DurNet {
+  int D, F, KT;
+  char* dev = nullptr;
+  float *w0, *we, *c1w, *c2w;  // packed
+  const float *pb, *t1w, *t1b, *t2w, *t2b, *c1b, *g1, *b1, *c2b, *g2, *b2, *lw, *lb;
+};
+
+struct PvaGraph {
+  hipGraphExec_t exec = nullptr;
+  hipStream_t cap = nullptr;
+  std::vector<const void*> key;
+};
+static PvaGraph g_pva;  // one cached graph per process (durgen is tiny; recaptured on any change)
+
+static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct PvaWs {
+  float *Fd, *TH, *TEMBd, *TEMBs, *Pd, *Ps, *R1, *S1, *R2;
+};
+static size_t pva_ws_layout(const DurNet* n, int B, int L, int nfe, void* base, PvaWs* w) {
+  size_t M = (size_t)B * L;
+  size_t sizes[9] = {4ull * nfe * n->D, 4ull * nfe * 4 * n->D, 4ull * nfe * n->D, 4ull * nfe * n->D, 4 * M * n->D,
+                     4 * M * n->D, 4 * M * n->F, 8 * M * (n->F / 64), 4 * M * n->F};
+  size_t off = 0;
+  float* p[9];
+  for (int i = 0; i < 9; ++i) {
+    p[i] = base ? (float*)((char*)base + off) : nullptr;
+    off += a256(sizes[i]);
+  }
+  if (w) *w = PvaWs{p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8]};
+  return off;
+}
+
+static int net_prepare(DurNet* n, const float* enc, int M, const float* ts, int nfe, float* F, float* TH, float* TEMB,
+                       float* P, hipStream_t st) {
+  const int D = n->D;
+  hipLaunchKernelGGL(pos_emb_kernel, dim3((nfe * D + 255) / 256), dim3(256), 0, st, ts, nfe, D, F);
+  FL_LAUNCH_CHECK();
+  int rc;
+  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{F, D}, n->t1w, D, EpiBiasAct<float, 2>{n->t1b, TH, 4 * D}, nfe, 4 * D, D, st))) return rc;
+  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{TH, 4 * D}, n->t2w, 4 * D, EpiBiasAct<float, 0>{n->t2b, TEMB, D}, nfe, D, 4 * D, st))) return rc;
+  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{enc, D}, n->we, D, EpiBiasAct<float, 0>{n->pb, P, D}, M, D, D, st))) return rc;
+  return kOk;
+}
+
+static int net_step(DurNet* n, const float* P, const float* temb, float* xt, const uint8_t* mask, int B, int L, float dt,
+                    const PvaWs& w, hipStream_t st) {
+  const int M = B * L, D = n->D, F = n->F;
+  const int NT = F / 64;
+  int rc;
+  if ((rc = launch_gemm<64, 64, 4, float>(LoadDurIn{P, n->w0, xt, temb, D, L}, n->c1w, 3 * D,
+                                          EpiBiasStatsT<true>{n->c1b, w.R1, F, w.S1, NT}, M, F, 3 * D, st)))
+    return rc;
+  if ((rc = launch_gemm<64, 64, 4, float>(LoadConvRows<float, true>{w.R1, F, L, 3, w.S1, NT, 64, 1e-5f, n->g1, n->b1}, n->c2w,
+                                          3 * F, EpiBiasAct<float, 3>{n->c2b, w.R2, F}, M, F, 3 * F, st)))
+    return rc;
+  hipLaunchKernelGGL(dur_head_kernel<384>, dim3((M + 3) / 4), dim3(256), 0, st, w.R2, n->g2, n->b2, n->lw, n->lb, mask, xt, M, dt);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+// -------- length regulator --------
+// One workgroup per utterance: repeats (interleaved phone/silence), exclusive prefix sum, total.
+__global__ __launch_bounds__(256) void lr_lengths_kernel(const float* __restrict__ pd, const float* __restrict__ sd,
+                                                         const int64_t* __restrict__ src_lens, int L, int log_domain,
+                                                         int64_t* __restrict__ cum, int64_t* __restrict__ tgt_len) {
+  __shared__ int64_t part[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int n2 = 2 * L;
+  const int per = (n2 + 255) / 256;
+  const int64_t sl = src_lens[b];
+  auto rep = [&](int j) -> int64_t {
+    int l = j >> 1;
+    float v = (j & 1) ? sd[(size_t)b * L + l] : pd[(size_t)b * L + l];
+    if (log_domain) v = fmaxf(rintf(expf(v) - 1.0f), 0.0f);   // pva.py:111-112
+    bool valid = l < sl;
+    if (!(j & 1)) {
+      int64_t r = valid ? (int64_t)rintf(v) : 0;              // pva.py:136-137 (round, clamp >= 1)
+      return r < 1 ? 1 : r;
+    }
+    int64_t r = valid ? (int64_t)rintf(v) : 0;                // pva.py:139-140 (round, clamp >= 0)
+    return r < 0 ? 0 : r;
+  };
+  int64_t s = 0;
+  for (int q = 0; q < per; ++q) {
+    int j = tid * per + q;
+    if (j < n2) s += rep(j);
+  }
+  part[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan of the thread totals
+    int64_t v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int64_t run = tid ? part[tid - 1] : 0;
+  int64_t* c = cum + (size_t)b * (n2 + 1);
+  for (int q = 0; q < per; ++q) {
+    int j = tid * per + q;
+    if (j < n2) {
+      c[j] = run;
+      run += rep(j);
+    }
+  }
+  if (tid == 255) {
+    c[n2] = part[255];
+    tgt_len[b] = part[255];
+  }
+}
+
+// out[b][f] = x[b][src(f)] for f < tgt_len[b] (src = segment j's phoneme, silence -> phoneme 0), else 0.
+__global__ __launch_bounds__(256) void lr_expand_kernel(const float* __restrict__ x, const int64_t* __restrict__ cum,
+                                                        int L, int H, int T_out, float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.y;
+  if (row >= T_out) return;
+  const int n2 = 2 * L;
+  const int64_t* c = cum + (size_t)b * (n2 + 1);
+  float* o = out + ((size_t)b * T_out + row) * H;
+  if ((int64_t)row >= c[n2]) {
+    for (int h = lane; h < H; h += 64) o[h] = 0.f;
+    return;
+  }
+  int lo = 0, hi = n2 - 1;  // last j with c[j] <= row and a non-empty segment
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (c[mid] <= (int64_t)row) lo = mid;
+    else hi = mid - 1;
+  }
+  int src = (lo & 1) ? 0 : (lo >> 1);
+  const float* xs = x + ((size_t)b * L + src) * H;
+  for (int h = lane; h < H; h += 64) o[h] = xs[h];
+}
+
+}  // namespace fl
+
+using namespace fl;
+
+extern "C" {
+
+FLAMED_API int flamed_dur_create(int input_size, int filter_size, int kernel, flamed_dur_t* out) {
+  FL_REQUIRE(out, "flamed_dur_create: null out");
+  FL_REQUIRE(kernel == 3, "flamed_dur_create: only kernel_size=3 is specialised (got %d)", kernel);
+  FL_REQUIRE(input_size % 64 == 0 && filter_size == 384, "flamed_dur_create: unsupported dims input=%d filter=%d", input_size, filter_size);
+  DurNet* n = new DurNet();
+  n->D = input_size; n->F = filter_size; n->KT = kernel;
+  *out = reinterpret_cast<flamed_dur_t>(n);
+  return kOk;
+}
+
+FLAMED_API int flamed_dur_destroy(flamed_dur_t h) {
+  DurNet* n = reinterpret_cast<DurNet*>(h);
+  if (!n) return kOk;
+  if (n->dev) (void)hipFree(n->dev);
+  delete n;
+  return kOk;
+}
+
+FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* w, int nw, hipStream_t st) {
+  DurNet* n = reinterpret_cast<DurNet*>(h);
+  FL_REQUIRE(n && w && nw == FLAMED_DUR_W, "flamed_dur_load: expected %d weights", FLAMED_DUR_W);
+  for (int i = 0; i < nw; ++i) FL_REQUIRE(w[i], "flamed_dur_load: weight %d is null", i);
+  const int D = n->D, F = n->F;
+  size_t o_w0 = 0, o_we = a256(4ull * D), o_c1 = o_we + a256(4ull * D * D), o_c2 = o_c1 + a256(4ull * F * 3 * D);
+  size_t total = o_c2 + a256(4ull * F * 3 * F);
+  if (n->dev) { FL_HIP(hipFree(n->dev)); n->dev = nullptr; }
+  FL_HIP(hipMalloc(&n->dev, total));
+  n->w0 = (float*)(n->dev + o_w0); n->we = (float*)(n->dev + o_we);
+  n->c1w = (float*)(n->dev + o_c1); n->c2w = (float*)(n->dev + o_c2);
+  hipLaunchKernelGGL(split_proj_kernel, dim3((D * (D + 1) + 255) / 256), dim3(256), 0, st, w[0], n->w0, n->we, D);
+  FL_LAUNCH_CHECK();
+  size_t t1 = (size_t)F * D * 3, t2 = (size_t)F * F * 3;
+  hipLaunchKernelGGL(taps_major_kernel, dim3((t1 + 255) / 256), dim3(256), 0, st, w[6], n->c1w, F, D, 3);
+  FL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(taps_major_kernel, dim3((t2 + 255) / 256), dim3(256), 0, st, w[10], n->c2w, F, F, 3);
+  FL_LAUNCH_CHECK();
+  n->pb = w[1]; n->t1w = w[2]; n->t1b = w[3]; n->t2w = w[4]; n->t2b = w[5]; n->c1b = w[7]; n->g1 = w[8]; n->b1 = w[9];
+  n->c2b = w[11]; n->g2 = w[12]; n->b2 = w[13]; n->lw = w[14]; n->lb = w[15];
+  return kOk;
+}
+
+FLAMED_API size_t flamed_pva_workspace_size(flamed_dur_t h, int B, int L, int nfe) {
+  DurNet* n = reinterpret_cast<DurNet*>(h);
+  return n ? pva_ws_layout(n, B, L, nfe, nullptr, nullptr) : 0;
+}
+
+FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* enc, const uint8_t* mask, float* dur_t,
+                               float* sil_t, const float* ts, int nfe, int B, int L, void* ws, size_t ws_bytes,
+                               int use_graph, hipStream_t st) {
+  DurNet* nd = reinterpret_cast<DurNet*>(dur);
+  DurNet* ns = reinterpret_cast<DurNet*>(sil);
+  FL_REQUIRE(nd && ns && nd->dev && ns->dev, "flamed_pva_flow: handles not loaded");
+  FL_REQUIRE(nd->D == ns->D && nd->F == ns->F, "flamed_pva_flow: dur/sil nets differ in dims");
+  FL_REQUIRE(enc && mask && dur_t && sil_t && ts && ws && nfe > 0 && B > 0 && L > 0, "flamed_pva_flow: bad args");
+  if (ws_bytes < pva_ws_layout(nd, B, L, nfe, nullptr, nullptr)) {
+    set_error("flamed_pva_flow: workspace too small");
+    return kNoWorkspace;
+  }
+  PvaWs w;
+  pva_ws_layout(nd, B, L, nfe, ws, &w);
+  const int M = B * L, D = nd->D;
+  // delta_t = 1 / nfe as a python float, applied in fp32 (pva.py:99,106,109)
+  const float dt = (float)(1.0 / (double)nfe);
+  int rc;
+  if ((rc = net_prepare(nd, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBd, w.Pd, st))) return rc;
+  if ((rc = net_prepare(ns, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBs, w.Ps, st))) return rc;
+  auto body = [&](hipStream_t s) -> int {
+    int r;
+    for (int i = 0; i < nfe; ++i) {  // dur then sil on every step (pva.py:104-109)
+      if ((r = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, w, s))) return r;
+      if ((r = net_step(ns, w.Ps, w.TEMBs + (size_t)i * D, sil_t, mask, B, L, dt, w, s))) return r;
+    }
+    return kOk;
+  };
+  if (!use_graph) return body(st);
+  std::vector<const void*> key = {nd, ns, enc, mask, dur_t, sil_t, ts, ws, (const void*)(intptr_t)nfe,
+                                  (const void*)(intptr_t)B, (const void*)(intptr_t)L, nd->dev, ns->dev};
+  if (!g_pva.exec || g_pva.key != key) {
+    if (g_pva.exec) { FL_HIP(hipGraphExecDestroy(g_pva.exec)); g_pva.exec = nullptr; }
+    if (!g_pva.cap) FL_HIP(hipStreamCreateWithFlags(&g_pva.cap, hipStreamNonBlocking));
+    FL_HIP(hipStreamBeginCapture(g_pva.cap, hipStreamCaptureModeRelaxed));
+    int r = body(g_pva.cap);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(g_pva.cap, &g);
+    if (r) { if (g) (void)hipGraphDestroy(g); return r; }
+    FL_HIP(e);
+    hipError_t ie = hipGraphInstantiate(&g_pva.exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    FL_HIP(ie);
+    g_pva.key = key;
+  }
+  FL_HIP(hipGraphLaunch(g_pva.exec, st));
+  return kOk;
+}
+
+FLAMED_API int flamed_lr_lengths(const float* phone, const float* sil, const int64_t* src_lens, int B, int L,
+                                 int log_domain, int64_t* cum, int64_t* tgt_len, hipStream_t st) {
+  FL_REQUIRE(phone && sil && src_lens && cum && tgt_len && B > 0 && L > 0, "flamed_lr_lengths: bad args");
+  hipLaunchKernelGGL(lr_lengths_kernel, dim3(B), dim3(256), 0, st, phone, sil, src_lens, L, log_domain, cum, tgt_len);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+FLAMED_API int flamed_lr_expand(const float* x, const int64_t* cum, int B, int L, int H, int T_out, float* out,
+                                hipStream_t st) {
+  FL_REQUIRE(x && cum && out && B > 0 && L > 0 && H > 0 && T_out >= 0, "flamed_lr_expand: bad args");
+  if (T_out == 0) return kOk;
+  hipLaunchKernelGGL(lr_expand_kernel, dim3((T_out + 3) / 4, B), dim3(256), 0, st, x, cum, L, H, T_out, out);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+}  // extern "C"

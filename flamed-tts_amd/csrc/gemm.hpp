@@ -287,8 +287,10 @@ struct EpiBiasAct {
   __device__ void store_stats(int, int, float, float) const {}
 };
 
-// fp32 output + per-(row, N-tile) LayerNorm partials (mean, M2) for the consumer's LayerNorm.
-struct EpiBiasStats {
+// fp32 output (+ optional ReLU) + per-(row, N-tile) LayerNorm partials (mean, M2) for the
+// consumer's LayerNorm.
+template <bool RELU = false>
+struct EpiBiasStatsT {
   const float* __restrict__ bias;
   float* __restrict__ out;
   int ldo;
@@ -297,10 +299,79 @@ struct EpiBiasStats {
   static constexpr bool kRowStats = true;
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
-  __device__ float value(int, int n, float acc, const float*, int) const { return acc + bias[n]; }
+  __device__ float value(int, int n, float acc, const float*, int) const {
+    float v = acc + bias[n];
+    return RELU ? fmaxf(v, 0.f) : v;
+  }
   __device__ void store(int m, int n, float v) const { out[(size_t)m * ldo + n] = v; }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(S)[(size_t)m * NT + nt] = make_float2(mean, m2);
+  }
+};
+using EpiBiasStats = EpiBiasStatsT<false>;
+
+// Conv1d (kernel KT, pad KT/2, zero padding at each sequence edge) as a GEMM over K = tap*Cin + c,
+// source rows optionally LayerNorm'ed (affine) from producer partials.  Row m = b*L + l.
+template <typename DT, bool LN>
+struct LoadConvRows {
+  const float* __restrict__ x;
+  int Cin;
+  int L;
+  int KT;
+  const float* __restrict__ S;  // LN partials of x rows (LN only)
+  int NT, tw;
+  float eps;
+  const float* __restrict__ g;
+  const float* __restrict__ bb;
+  static constexpr int EPC = DTraits<DT>::EPC;
+  struct Raw { float v[EPC], w[LN ? EPC : 1], b[LN ? EPC : 1]; int src; };
+  static constexpr int stat_rows(int BM) { return LN ? BM + 8 : 0; }
+  __device__ void prologue(int bm, int BM, int M, float* st) const {
+    if constexpr (LN) {
+      const int h = KT / 2;
+      for (int r = threadIdx.x; r < BM + 2 * h; r += blockDim.x) {
+        int m = bm - h + r;
+        m = m < 0 ? 0 : (m < M ? m : M - 1);
+        row_stats_from_partials(S, m, NT, tw, eps, st[2 * r], st[2 * r + 1]);
+      }
+    }
+  }
+  __device__ Raw issue(int m, int k) const {
+    Raw r;
+    int tap = k / Cin, c = k - tap * Cin;
+    int l = m % L + tap - KT / 2;
+    r.src = (l >= 0 && l < L) ? m + tap - KT / 2 : -1;
+    if (r.src >= 0) {
+      const float* px = x + (size_t)r.src * Cin + c;
+#pragma unroll
+      for (int j = 0; j < EPC; j += 4) {
+        float4 a = ld4(px + j);
+        r.v[j] = a.x; r.v[j + 1] = a.y; r.v[j + 2] = a.z; r.v[j + 3] = a.w;
+        if constexpr (LN) {
+          float4 w = ld4(g + c + j), b = ld4(bb + c + j);
+          r.w[j] = w.x; r.w[j + 1] = w.y; r.w[j + 2] = w.z; r.w[j + 3] = w.w;
+          r.b[j] = b.x; r.b[j + 1] = b.y; r.b[j + 2] = b.z; r.b[j + 3] = b.w;
+        }
+      }
+    }
+    return r;
+  }
+  template <typename D>
+  __device__ uint4 finish(const Raw& r, int, int, const float* st, int bm) const {
+    float o[EPC];
+    if (r.src < 0) {
+#pragma unroll
+      for (int j = 0; j < EPC; ++j) o[j] = 0.f;
+    } else if constexpr (LN) {
+      int i = r.src - (bm - KT / 2);
+      const float mean = st[2 * i], rstd = st[2 * i + 1];
+#pragma unroll
+      for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - mean) * rstd) * r.w[j] + r.b[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < EPC; ++j) o[j] = r.v[j];
+    }
+    return pack_chunk<D>(o);
   }
 };
 

@@ -35,6 +35,13 @@ SIGNATURES = {
     "flamed_den_step": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, c_size_t, P]),
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_den_time_kernels": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
+    "flamed_dur_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(P)]),
+    "flamed_dur_destroy": (c_int, [P]),
+    "flamed_dur_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_pva_workspace_size": (c_size_t, [P, c_int, c_int, c_int]),
+    "flamed_pva_flow": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
+    "flamed_lr_lengths": (c_int, [P, P, P, c_int, c_int, c_int, P, P, P]),
+    "flamed_lr_expand": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
 }
 
 FLAMED_F32, FLAMED_BF16 = 0, 1

@@ -97,6 +97,37 @@ enum { FLAMED_DEN_KERNEL_CLASSES = 9 };
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                        size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);
 
+/* ==================== PVA duration / silence generators + length regulator ====================
+ * Replaces ProbabilisticModule.forward (pva.py:221-238) inside the Euler loop of PVA.sample
+ * (pva.py:97-109) and LengthRegulator.LR (pva.py:125-166, with tools.pad :299-317).
+ * Weight order for flamed_dur_load (fp32 device tensors, prefix prior_generator.pva.{duration,sil}_generator.):
+ *   proj.{weight,bias}, time_emb.time_emb.1.{weight,bias}, time_emb.time_emb.3.{weight,bias},
+ *   conv_layer.conv1d_1.conv.{weight,bias}, conv_layer.layer_norm_1.{weight,bias},
+ *   conv_layer.conv1d_2.conv.{weight,bias}, conv_layer.layer_norm_2.{weight,bias}, linear_layer.{weight,bias}
+ * Vectors are referenced in place (keep them alive); the proj split and conv taps are packed. */
+enum { FLAMED_DUR_W = 16 };
+typedef struct flamed_dur_s* flamed_dur_t;
+FLAMED_API int flamed_dur_create(int input_size, int filter_size, int kernel, flamed_dur_t* out);
+FLAMED_API int flamed_dur_destroy(flamed_dur_t h);
+FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* weights, int n_weights, hipStream_t stream);
+FLAMED_API size_t flamed_pva_workspace_size(flamed_dur_t h, int B, int L, int nfe);
+/* Whole nfe-step flow of both generators, in place on dur_t / sil_t (B*L, the initial noise *
+ * temperature).  enc: (B*L) x input_size encoder output; mask: uint8 B*L, 1 = padding (src_mask);
+ * ts: nfe+1 fp32 time grid (torch.linspace(0, 1, nfe+1)).  use_graph != 0 replays a cached hipGraph. */
+FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* enc, const uint8_t* mask, float* dur_t,
+                               float* sil_t, const float* ts, int nfe, int B, int L, void* ws, size_t ws_bytes,
+                               int use_graph, hipStream_t stream);
+/* Length regulator, phase 1: per-utterance interleaved [phone_l, silence_l] repeat counts
+ * (padding phonemes -> 1 frame, 0 silence), exclusive prefix sums cum (int64 B x (2L+1)) and
+ * tgt_len (int64 B).  phone/sil are frame counts, or final log-durations when log_domain != 0
+ * (then clamp(round(exp(d) - 1), 0) is applied first, pva.py:111-112).  src_lens: int64 B. */
+FLAMED_API int flamed_lr_lengths(const float* phone, const float* sil, const int64_t* src_lens, int B, int L,
+                                 int log_domain, int64_t* cum, int64_t* tgt_len, hipStream_t stream);
+/* Phase 2 (after the host has read max(tgt_len), as the reference's .tolist() does): gather frames
+ * out[b][f] = x[b][src] (silence frames copy phoneme 0), zero beyond tgt_len[b], truncated at T_out. */
+FLAMED_API int flamed_lr_expand(const float* x, const int64_t* cum, int B, int L, int H, int T_out, float* out,
+                                hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,124 @@
+"""GPU parity: PVA duration / silence flow (HIP, exact-fp32 MFMA) and the HIP length regulator.
+
+Tolerances: final log-durations rel-L2 <= 1e-5 vs the reference (fp32, summation order only);
+frame counts / tgt_len / regulated frames BIT-EXACT (integer work); for random weights at larger
+sizes any duration within 1e-4 of a .5 rounding boundary is excluded and counted as a possible flip.
+"""
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from _common import golden, seeded, t32, rel_l2, orc, PKG
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def pva():
+    import os
+    from flamed.models.synthesizer.pva import PVA
+    cfg = yaml.safe_load(open(os.path.join(PKG, "configs", "prior.yaml")))["variance_adaptor"]
+    m = PVA(cfg).eval()
+    sd = seeded("pva")
+    m.load_state_dict({k[len("prior_generator.pva."):]: v for k, v in sd.items()})
+    return m.to(DEV), sd
+
+
+def test_pva_flow_and_sample_golden(pva):
+    m, _ = pva
+    g = golden("pva")
+    src_len = t32(g["src_len"])
+    L = g["enc"].shape[1]
+    mask = torch.arange(L)[None, :] >= src_len[:, None]
+    enc = t32(g["enc"]).to(DEV)
+    with torch.inference_mode():
+        torch.manual_seed(int(g["rng_seed"]))
+        d, s = m.flow(enc, mask.to(DEV), int(g["nfe"]), float(g["temperature"]))
+        assert rel_l2(d.cpu(), g["dur_final"]) < 1e-5 and rel_l2(s.cpu(), g["sil_final"]) < 1e-5
+        torch.manual_seed(int(g["rng_seed"]))
+        x_lr, tgt = m.sample(enc, src_len.to(DEV), mask.to(DEV), nfe=int(g["nfe"]), temperature=float(g["temperature"]))
+    assert np.array_equal(tgt.cpu().numpy(), g["tgt_len"])
+    assert x_lr.shape == g["x_lr"].shape and np.array_equal(x_lr.cpu().numpy(), g["x_lr"])
+
+
+def test_pva_graph_equals_eager(pva):
+    m, _ = pva
+    gen = torch.Generator().manual_seed(3)
+    B, L = 3, 41
+    enc = torch.randn(B, L, 192, generator=gen).to(DEV)
+    mask = (torch.arange(L)[None, :] >= torch.tensor([41, 30, 7])[:, None]).to(DEV)
+    outs = []
+    with torch.inference_mode():
+        for graph in (True, True, False):
+            m.hip_graph = graph
+            torch.manual_seed(5)
+            outs.append(m.flow(enc, mask, 6, 0.3))
+    m.hip_graph = True
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+
+
+def test_pva_flow_vs_oracle_larger(pva):
+    m, sd = pva
+    gen = torch.Generator().manual_seed(11)
+    B, L, nfe = 6, 97, 16
+    enc = torch.randn(B, L, 192, generator=gen)
+    lens = torch.tensor([97, 80, 64, 33, 12, 1])
+    mask = torch.arange(L)[None, :] >= lens[:, None]
+    torch.manual_seed(21)
+    dn, sn = torch.randn((B, L)), torch.randn((B, L))
+    with torch.inference_mode():
+        torch.manual_seed(21)
+        d, s = m.flow(enc.to(DEV), mask.to(DEV), nfe, 0.3)
+    rd, rs = orc.pva_flow(sd, enc, mask, nfe, 0.3, noise=(dn, sn))
+    assert rel_l2(d.cpu(), rd) < 1e-5 and rel_l2(s.cpu(), rs) < 1e-5
+    for got, ref in ((d.cpu(), rd), (s.cpu(), rs)):
+        e = torch.exp(ref) - 1
+        safe = (e - e.floor() - 0.5).abs() > 1e-4
+        gf, rf = orc.log_to_frames(got), orc.log_to_frames(ref)
+        assert torch.equal(gf[safe], rf[safe])
+
+
+def test_length_regulator_golden_cases_bit_exact():
+    from flamed.models.synthesizer.pva import hip_length_regulate
+    g = golden("lr_cases")
+    for ci in range(int(g["n"])):
+        mx = int(g[f"c{ci}_max"])
+        out, tl = hip_length_regulate(t32(g[f"c{ci}_x"]).to(DEV), t32(g[f"c{ci}_pd"]).to(DEV),
+                                      t32(g[f"c{ci}_sd"]).to(DEV), t32(g[f"c{ci}_sl"]).to(DEV),
+                                      None if mx < 0 else mx)
+        assert np.array_equal(tl.cpu().numpy(), g[f"c{ci}_tl"]), ci
+        assert np.array_equal(out.cpu().numpy(), g[f"c{ci}_out"]), ci
+
+
+@pytest.mark.parametrize("B,L,H,max_len", [(5, 37, 192, None), (2, 300, 64, 50), (7, 3, 8, None), (1, 1, 192, 3),
+                                           (4, 513, 32, None)])
+def test_length_regulator_random_bit_exact(B, L, H, max_len):
+    from flamed.models.synthesizer.pva import hip_length_regulate
+    rng = np.random.default_rng(B * 7919 + L)
+    x = rng.standard_normal((B, L, H)).astype(np.float32)
+    pd = rng.integers(0, 9, (B, L)).astype(np.float32)
+    sdur = rng.integers(0, 4, (B, L)).astype(np.float32)
+    sl = rng.integers(1, L + 1, (B,)).astype(np.int64)
+    ref, rtl = orc.length_regulate(x, pd, sdur, sl, max_len)
+    out, tl = hip_length_regulate(t32(x).to(DEV), t32(pd).to(DEV), t32(sdur).to(DEV), t32(sl).to(DEV), max_len)
+    assert np.array_equal(tl.cpu().numpy(), rtl)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_length_regulator_log_domain():
+    from flamed.models.synthesizer.pva import hip_length_regulate
+    rng = np.random.default_rng(3)
+    B, L, H = 3, 50, 16
+    x = rng.standard_normal((B, L, H)).astype(np.float32)
+    d = rng.uniform(-1, 3, (B, L)).astype(np.float32)
+    s = rng.uniform(-1, 1.5, (B, L)).astype(np.float32)
+    sl = np.array([50, 20, 1], dtype=np.int64)
+    pdf = orc.log_to_frames(t32(d)).numpy()
+    sdf = orc.log_to_frames(t32(s)).numpy()
+    ref, rtl = orc.length_regulate(x, pdf, sdf, sl)
+    out, tl = hip_length_regulate(t32(x).to(DEV), t32(d).to(DEV), t32(s).to(DEV), t32(sl).to(DEV), None,
+                                  log_domain=True)
+    assert np.array_equal(tl.cpu().numpy(), rtl) and np.array_equal(out.cpu().numpy(), ref)
