@@ -175,7 +175,7 @@ static int net_step(DurNet* n, const float* P, const float* temb, float* xt, con
   if ((rc = launch_gemm<64, 64, 4, float>(LoadDurIn{P, n->w0, xt, temb, D, L}, n->c1w, 3 * D,
                                           EpiBiasStatsT<true>{n->c1b, w.R1, F, w.S1, NT}, M, F, 3 * D, st)))
     return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadConvRows<float, true>{w.R1, F, L, 3, w.S1, NT, 64, 1e-5f, n->g1, n->b1}, n->c2w,
+  if ((rc = launch_gemm<64, 64, 4, float>(LoadConvRows<float, true>{w.R1, F, L, 3, 1, w.S1, NT, 64, 1e-5f, n->g1, n->b1}, n->c2w,
                                           3 * F, EpiBiasAct<float, 3>{n->c2b, w.R2, F}, M, F, 3 * F, st)))
     return rc;
   hipLaunchKernelGGL(dur_head_kernel<384>, dim3((M + 3) / 4), dim3(256), 0, st, w.R2, n->g2, n->b2, n->lw, n->lb, mask, xt, M, dt);

@@ -1,0 +1,497 @@
+// FaCodec decoder (inference) on gfx950.  Reference: flamed/models/facodec/facodec.py:27-32
+// (WNConv1d / WNConvTranspose1d), :57-118 (SnakeBeta), :121-133 (ResidualUnit), :246-265
+// (DecoderBlock), :398-415 (model stack), :630-638 (FACodecDecoder.inference);
+// alias_free_torch/act.py:7-29, resample.py:9-57, filter.py:27-96 (Activation1d).
+//
+// Layout: channels-last rows (B*n, C) fp32 residual stream; every conv is an implicit GEMM on the
+// MFMA template (K = tap*Cin + c), weight norm folded at load.  ConvTranspose(k=2s, stride s) is
+// s polyphase GEMMs with 2 taps each: output o = q*s + r - p takes W[:,:,r] x[q] + W[:,:,r+s] x[q-1].
+// Activation1d (replicate-pad, 12-tap kaiser-sinc x2 upsample, SnakeBeta, 12-tap lowpass /2) is one
+// LDS-tiled stencil kernel: fp32 in, GEMM-operand dtype out.
+#include "flamed_hip.h"
+#include "gemm.hpp"
+
+#include <vector>
+
+namespace fl {
+
+// ------------------------------ weight packing ------------------------------
+
+// weight_norm(dim=0): w[i] = g[i] * v[i] / ||v[i]||  (one workgroup per dim-0 slice of `inner` values)
+__global__ __launch_bounds__(256) void wn_fold_kernel(const float* __restrict__ g, const float* __restrict__ v, int inner,
+                                                      float* __restrict__ w) {
+  __shared__ float red[4];
+  const int i = blockIdx.x;
+  const float* vi = v + (size_t)i * inner;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < inner; k += 256) s += vi[k] * vi[k];
+  s = wave_sum64(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float nrm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+  const float sc = g[i] / nrm;
+  for (int k = threadIdx.x; k < inner; k += 256) w[(size_t)i * inner + k] = vi[k] * sc;
+}
+
+// conv (N, Cin, KT) -> (N, KT, Cin) in DT
+template <typename DT>
+__global__ void pack_conv_kernel(const float* __restrict__ src, DT* __restrict__ dst, int N, int Cin, int KT) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)N * Cin * KT) return;
+  int k = i % KT;
+  size_t t = i / KT;
+  int c = t % Cin;
+  int n = t / Cin;
+  store_val<DT>(dst + ((size_t)n * KT + k) * Cin + c, src[i]);
+}
+
+// convT (Cin, Cout, 2s) -> per phase r: (Cout, 2, Cin) with tap 0 = kernel index r, tap 1 = r + s
+template <typename DT>
+__global__ void pack_convt_kernel(const float* __restrict__ src, DT* __restrict__ dst, int Cin, int Cout, int s) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KT = 2 * s;
+  if (i >= (size_t)Cin * Cout * KT) return;
+  int k = i % KT;
+  size_t t = i / KT;
+  int oc = t % Cout;
+  int ic = t / Cout;
+  int r = k % s, tap = k / s;
+  store_val<DT>(dst + (size_t)r * Cout * 2 * Cin + ((size_t)oc * 2 + tap) * Cin + ic, src[i]);
+}
+
+// ------------------------------ fused Activation1d ------------------------------
+constexpr int kActA = 64;  // output samples per workgroup
+constexpr int kActCG = 64; // channels per workgroup
+
+template <typename OT>
+__global__ __launch_bounds__(256) void act1d_kernel(const float* __restrict__ x, int C, int n,
+                                                    const float* __restrict__ alpha, const float* __restrict__ beta,
+                                                    const float* __restrict__ fu, const float* __restrict__ fd,
+                                                    OT* __restrict__ out) {
+  constexpr int XR = kActA + 13;      // x rows a0-6 .. a0+A+6
+  constexpr int SR = 2 * kActA + 12;  // snake samples j = 2a0-5 .. 2a0+2A+6
+  __shared__ float xs[XR * kActCG];
+  __shared__ float ss[SR * kActCG];
+  __shared__ float filt[24];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * kActCG, a0 = blockIdx.y * kActA, b = blockIdx.z;
+  if (tid < 12) filt[tid] = fu[tid];
+  else if (tid < 24) filt[tid] = fd[tid - 12];
+  const float* xb = x + (size_t)b * n * C;
+  for (int idx = tid; idx < XR * kActCG; idx += 256) {
+    int r = idx / kActCG, cc = idx - r * kActCG;
+    int a = a0 - 6 + r;
+    a = a < 0 ? 0 : (a >= n ? n - 1 : a);
+    xs[idx] = xb[(size_t)a * C + c0 + cc];
+  }
+  __syncthreads();
+  const int cc = tid & 63, rg = tid >> 6;
+  const float ea = expf(alpha[c0 + cc]);
+  const float ib = 1.0f / (expf(beta[c0 + cc]) + 1e-9f);
+  const int n2 = 2 * n;
+  for (int jj = rg; jj < SR; jj += 4) {
+    int j = 2 * a0 - 5 + jj;
+    j = j < 0 ? 0 : (j >= n2 ? n2 - 1 : j);
+    const int ap = j >> 1;
+    const int base = ap - (a0 - 6);  // xs row of x[ap]
+    float u = 0.f;
+    if (j & 1) {
+#pragma unroll
+      for (int m = -2; m <= 3; ++m) u += filt[6 - 2 * m] * xs[(base + m) * kActCG + cc];
+    } else {
+#pragma unroll
+      for (int m = -3; m <= 2; ++m) u += filt[5 - 2 * m] * xs[(base + m) * kActCG + cc];
+    }
+    u = 2.0f * u;
+    float sn = sinf(u * ea);
+    ss[jj * kActCG + cc] = u + ib * (sn * sn);
+  }
+  __syncthreads();
+  OT* ob = out + (size_t)b * n * C;
+  for (int q = rg; q < kActA; q += 4) {
+    int a = a0 + q;
+    if (a >= n) break;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc += filt[12 + k] * ss[(2 * q + k) * kActCG + cc];
+    store_val<OT>(ob + (size_t)a * C + c0 + cc, acc);
+  }
+}
+
+// ------------------------------ prep: LayerNorm over C + timbre affine + transpose ------------------------------
+// lat (B, C, T) channels-first -> h0 (B*T, C): LN(eps 1e-5, no affine) then x*gamma + beta (facodec.py:631-636)
+__global__ __launch_bounds__(256) void fac_prep_kernel(const float* __restrict__ lat, const float* __restrict__ style,
+                                                       int C, int T, float* __restrict__ h0) {
+  extern __shared__ float tile[];  // C x 33
+  const int b = blockIdx.y, t0 = blockIdx.x * 32, tid = threadIdx.x;
+  for (int idx = tid; idx < C * 32; idx += 256) {
+    int c = idx >> 5, t = idx & 31;
+    tile[c * 33 + t] = (t0 + t < T) ? lat[((size_t)b * C + c) * T + t0 + t] : 0.f;
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  const int per = C / 64;
+  for (int t = wave; t < 32; t += 4) {
+    if (t0 + t >= T) break;
+    float v[8];
+    float s = 0.f;
+    for (int j = 0; j < per; ++j) {
+      v[j] = tile[(lane + 64 * j) * 33 + t];
+      s += v[j];
+    }
+    float mean = wave_sum64(s) / (float)C;
+    float q = 0.f;
+    for (int j = 0; j < per; ++j) {
+      float d = v[j] - mean;
+      q += d * d;
+    }
+    float rstd = 1.0f / sqrtf(wave_sum64(q) / (float)C + 1e-5f);
+    for (int j = 0; j < per; ++j) {
+      int c = lane + 64 * j;
+      float y = (v[j] - mean) * rstd;
+      h0[((size_t)b * T + t0 + t) * C + c] = y * style[(size_t)b * 2 * C + c] + style[(size_t)b * 2 * C + C + c];
+    }
+  }
+}
+
+// ------------------------------ final Conv1d(64 -> 1, k7, pad 3) + tanh ------------------------------
+template <typename IT>
+__global__ __launch_bounds__(128) void fac_out_kernel(const IT* __restrict__ act, int C, int n, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, float* __restrict__ wav) {
+  constexpr int TS = 128, HALO = 3;
+  extern __shared__ float sm[];
+  float* rows = sm;                      // (TS + 6) x (C + 1)
+  float* ws = sm + (TS + 2 * HALO) * (C + 1);  // C x 7
+  const int b = blockIdx.y, t0 = blockIdx.x * TS, tid = threadIdx.x;
+  for (int i = tid; i < C * 7; i += TS) ws[i] = w[i];
+  const IT* ab = act + (size_t)b * n * C;
+  for (int idx = tid; idx < (TS + 2 * HALO) * C; idx += TS) {
+    int r = idx / C, c = idx - r * C;
+    int t = t0 - HALO + r;
+    rows[r * (C + 1) + c] = (t >= 0 && t < n) ? (float)ab[(size_t)t * C + c] : 0.f;
+  }
+  __syncthreads();
+  const int t = t0 + tid;
+  if (t >= n) return;
+  float acc = bias[0];
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) acc += ws[c * 7 + k] * rows[(tid + k) * (C + 1) + c];
+  wav[(size_t)b * n + t] = tanhf(acc);
+}
+
+// ------------------------------ GEMM loaders / epilogues ------------------------------
+
+// ConvTranspose phase GEMM A operand: row m -> (b, q), q in [0, n]; tap 0 = x[q], tap 1 = x[q-1].
+template <typename DT>
+struct LoadConvT {
+  const DT* __restrict__ x;
+  int Cin;
+  int n;
+  struct Raw { uint4 v; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    int b = m / (n + 1), q = m - b * (n + 1);
+    int tap = k / Cin, c = k - tap * Cin;
+    int i = q - tap;
+    if (i < 0 || i >= n) return Raw{make_uint4(0u, 0u, 0u, 0u)};
+    return Raw{*reinterpret_cast<const uint4*>(x + ((size_t)b * n + i) * Cin + c)};
+  }
+  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
+};
+
+struct EpiConvTStore {
+  const float* __restrict__ bias;
+  float* __restrict__ out;
+  int Cout, n, s, r, p;
+  static constexpr bool kRowStats = false;
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ float value(int, int col, float acc, const float*, int) const { return acc + bias[col]; }
+  __device__ void store(int m, int col, float v) const {
+    int b = m / (n + 1), q = m - b * (n + 1);
+    int o = q * s + r - p;
+    if (o >= 0 && o < s * n) out[((size_t)b * s * n + o) * Cout + col] = v;
+  }
+  __device__ void store_stats(int, int, float, float) const {}
+};
+
+struct EpiResAdd {  // X += acc + bias  (ResidualUnit skip, facodec.py:132-133)
+  const float* __restrict__ bias;
+  float* X;
+  int ld;
+  static constexpr bool kRowStats = false;
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ float value(int m, int col, float acc, const float*, int) const { return X[(size_t)m * ld + col] + (acc + bias[col]); }
+  __device__ void store(int m, int col, float v) const { X[(size_t)m * ld + col] = v; }
+  __device__ void store_stats(int, int, float, float) const {}
+};
+
+template <typename DT, class AL, class EP>
+static int gemm_auto(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  if (M >= 4096 && N % 128 == 0) return launch_gemm<128, 128, 4, DT>(al, W, ldw, ep, M, N, K, st);
+  if (M >= 4096) return launch_gemm<128, 64, 4, DT>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm<64, 64, 4, DT>(al, W, ldw, ep, M, N, K, st);
+}
+
+// ------------------------------ handle ------------------------------
+struct FacAct { const float *alpha, *beta, *fu, *fd; };
+struct FacRU { FacAct a1, a2; void* w7; const float* b7; void* w1; const float* b1; int dil; };
+struct FacBlk { FacAct a; void* wt; const float* bt; int s, cin, cout; FacRU ru[3]; };
+
+struct Fac {
+  int C0, CI, NUP, dt;
+  int ups[8];
+  const float *tlw, *tlb;
+  void* win; const float* bin;
+  FacBlk blk[8];
+  FacAct afin;
+  float* wout; const float* bout;
+  int cfin;
+  char* dev = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  hipStream_t cap = nullptr;
+  std::vector<const void*> gkey;
+};
+
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct FacWs { float* style; float* h0; float* X; float* Z; void* A; };
+static size_t fac_ws_layout(const Fac* f, int B, int T, void* base, FacWs* w) {
+  size_t maxcn = (size_t)f->CI * T;
+  size_t n = T;
+  int c = f->CI;
+  for (int i = 0; i < f->NUP; ++i) {
+    n *= f->ups[i];
+    c /= 2;
+    maxcn = maxcn > (size_t)c * n ? maxcn : (size_t)c * n;
+  }
+  size_t es = f->dt == FLAMED_BF16 ? 2 : 4;
+  size_t sizes[5] = {4ull * B * 2 * f->C0, 4ull * B * T * f->C0, 4 * B * maxcn, 4 * B * maxcn, es * B * maxcn};
+  size_t off = 0;
+  char* p[5];
+  for (int i = 0; i < 5; ++i) {
+    p[i] = base ? (char*)base + off : nullptr;
+    off += al256(sizes[i]);
+  }
+  if (w) *w = FacWs{(float*)p[0], (float*)p[1], (float*)p[2], (float*)p[3], p[4]};
+  return off;
+}
+
+template <typename DT>
+static int launch_act(const FacAct& a, const float* x, int C, int n, int B, DT* out, hipStream_t st) {
+  FL_REQUIRE(C % kActCG == 0, "act1d: C=%d must be a multiple of 64", C);
+  hipLaunchKernelGGL(act1d_kernel<DT>, dim3(C / kActCG, (n + kActA - 1) / kActA, B), dim3(256), 0, st, x, C, n, a.alpha,
+                     a.beta, a.fu, a.fd, out);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+template <typename DT>
+static int fac_decode_impl(Fac* f, const float* lat, const float* spk, int B, int T, float* wav, const FacWs& w,
+                           hipStream_t st) {
+  int rc;
+#define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
+  const int C0 = f->C0;
+  DT* A = reinterpret_cast<DT*>(w.A);
+  TRY((launch_gemm<64, 64, 4, float>(LoadF32<float>{spk, C0}, f->tlw, C0, EpiBiasAct<float, 0>{f->tlb, w.style, 2 * C0}, B, 2 * C0, C0, st)));
+  hipLaunchKernelGGL(fac_prep_kernel, dim3((T + 31) / 32, B), dim3(256), (size_t)C0 * 33 * 4, st, lat, w.style, C0, T, w.h0);
+  FL_LAUNCH_CHECK();
+  TRY((gemm_auto<DT>(LoadConvRows<DT, false>{w.h0, C0, T, 7, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, (const DT*)f->win, 7 * C0,
+                     EpiBiasAct<float, 0>{f->bin, w.X, f->CI}, B * T, f->CI, 7 * C0, st)));
+  int n = T;
+  for (int i = 0; i < f->NUP; ++i) {
+    const FacBlk& bk = f->blk[i];
+    const int s = bk.s, Cin = bk.cin, Cout = bk.cout, p = s / 2 + s % 2;
+    TRY(launch_act<DT>(bk.a, w.X, Cin, n, B, A, st));
+    for (int r = 0; r < s; ++r) {
+      const DT* Wr = (const DT*)bk.wt + (size_t)r * Cout * 2 * Cin;
+      TRY((gemm_auto<DT>(LoadConvT<DT>{A, Cin, n}, Wr, 2 * Cin, EpiConvTStore{bk.bt, w.X, Cout, n, s, r, p}, B * (n + 1), Cout,
+                         2 * Cin, st)));
+    }
+    n *= s;
+    for (int j = 0; j < 3; ++j) {
+      const FacRU& ru = bk.ru[j];
+      TRY(launch_act<DT>(ru.a1, w.X, Cout, n, B, A, st));
+      TRY((gemm_auto<DT>(LoadConvPlain<DT>{A, Cout, n, 7, ru.dil}, (const DT*)ru.w7, 7 * Cout,
+                         EpiBiasAct<float, 0>{ru.b7, w.Z, Cout}, B * n, Cout, 7 * Cout, st)));
+      TRY(launch_act<DT>(ru.a2, w.Z, Cout, n, B, A, st));
+      TRY((gemm_auto<DT>(LoadPlain<DT>{A, Cout}, (const DT*)ru.w1, Cout, EpiResAdd{ru.b1, w.X, Cout}, B * n, Cout, Cout, st)));
+    }
+  }
+  const int cf = f->cfin;
+  TRY(launch_act<DT>(f->afin, w.X, cf, n, B, A, st));
+  size_t smem = ((128 + 6) * (cf + 1) + cf * 7) * 4;
+  hipLaunchKernelGGL(fac_out_kernel<DT>, dim3((n + 127) / 128, B), dim3(128), smem, st, A, cf, n, f->wout, f->bout, wav);
+  FL_LAUNCH_CHECK();
+#undef TRY
+  return kOk;
+}
+
+}  // namespace fl
+
+using namespace fl;
+
+extern "C" {
+
+FLAMED_API int flamed_fac_create(int in_channels, int upsample_initial_channel, int n_up, const int* up_ratios, int dtype,
+                                 flamed_fac_t* out) {
+  FL_REQUIRE(out && up_ratios, "flamed_fac_create: null args");
+  FL_REQUIRE(n_up >= 1 && n_up <= 8, "flamed_fac_create: n_up=%d unsupported", n_up);
+  FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16, "flamed_fac_create: bad dtype");
+  FL_REQUIRE(in_channels % 64 == 0 && in_channels <= 512, "flamed_fac_create: in_channels=%d unsupported", in_channels);
+  FL_REQUIRE((upsample_initial_channel >> n_up) >= 64 && (upsample_initial_channel >> n_up) % 64 == 0,
+             "flamed_fac_create: unsupported dims (channels %d over %d stages)", upsample_initial_channel, n_up);
+  Fac* f = new Fac();
+  f->C0 = in_channels; f->CI = upsample_initial_channel; f->NUP = n_up; f->dt = dtype;
+  for (int i = 0; i < n_up; ++i) {
+    FL_REQUIRE(up_ratios[i] >= 1 && up_ratios[i] <= 8, "flamed_fac_create: up ratio %d unsupported", up_ratios[i]);
+    f->ups[i] = up_ratios[i];
+  }
+  *out = reinterpret_cast<flamed_fac_t>(f);
+  return kOk;
+}
+
+FLAMED_API int flamed_fac_destroy(flamed_fac_t h) {
+  Fac* f = reinterpret_cast<Fac*>(h);
+  if (!f) return kOk;
+  if (f->gexec) (void)hipGraphExecDestroy(f->gexec);
+  if (f->cap) (void)hipStreamDestroy(f->cap);
+  if (f->dev) (void)hipFree(f->dev);
+  delete f;
+  return kOk;
+}
+
+FLAMED_API int flamed_fac_num_weights(flamed_fac_t h) {
+  Fac* f = reinterpret_cast<Fac*>(h);
+  return f ? 5 + FLAMED_FAC_BLOCK_W * f->NUP + 7 : -1;
+}
+
+FLAMED_API int flamed_fac_load(flamed_fac_t h, const float* const* w, int nw, hipStream_t st) {
+  Fac* f = reinterpret_cast<Fac*>(h);
+  FL_REQUIRE(f && w, "flamed_fac_load: null args");
+  FL_REQUIRE(nw == flamed_fac_num_weights(h), "flamed_fac_load: expected %d weights, got %d", flamed_fac_num_weights(h), nw);
+  for (int i = 0; i < nw; ++i) FL_REQUIRE(w[i], "flamed_fac_load: weight %d is null", i);
+  const size_t es = f->dt == FLAMED_BF16 ? 2 : 4;
+  // ---- arena layout
+  struct Conv { const float *g, *v, *b; int dim0, inner, kind, N, Cin, KT, s; size_t off; };  // kind 0 conv, 1 convT
+  std::vector<Conv> convs;
+  size_t off = 0, maxfold = 0;
+  auto add = [&](const float* g, const float* v, const float* b, int kind, int N, int Cin, int KT, int s) -> int {
+    Conv c{g, v, b, kind == 0 ? N : Cin, kind == 0 ? Cin * KT : N * KT, kind, N, Cin, KT, s, off};
+    off = al256(off + es * (size_t)N * Cin * KT);
+    maxfold = maxfold > (size_t)N * Cin * KT ? maxfold : (size_t)N * Cin * KT;
+    convs.push_back(c);
+    return (int)convs.size() - 1;
+  };
+  f->tlw = w[0]; f->tlb = w[1];
+  int ci = add(w[2], w[3], w[4], 0, f->CI, f->C0, 7, 0);
+  f->bin = w[4];
+  std::vector<int> idx_t(f->NUP), idx7(f->NUP * 3), idx1(f->NUP * 3);
+  int c = f->CI;
+  for (int i = 0; i < f->NUP; ++i) {
+    const float* const* bw = w + 5 + FLAMED_FAC_BLOCK_W * i;
+    FacBlk& bk = f->blk[i];
+    bk.s = f->ups[i]; bk.cin = c; bk.cout = c / 2;
+    bk.a = FacAct{bw[0], bw[1], bw[2], bw[3]};
+    idx_t[i] = add(bw[4], bw[5], bw[6], 1, bk.cout, bk.cin, 2 * bk.s, bk.s);
+    bk.bt = bw[6];
+    const int dils[3] = {1, 3, 9};
+    for (int j = 0; j < 3; ++j) {
+      const float* const* rw = bw + 7 + 14 * j;
+      FacRU& ru = bk.ru[j];
+      ru.dil = dils[j];
+      ru.a1 = FacAct{rw[0], rw[1], rw[2], rw[3]};
+      idx7[i * 3 + j] = add(rw[4], rw[5], rw[6], 0, bk.cout, bk.cout, 7, 0);
+      ru.b7 = rw[6];
+      ru.a2 = FacAct{rw[7], rw[8], rw[9], rw[10]};
+      idx1[i * 3 + j] = add(rw[11], rw[12], rw[13], 0, bk.cout, bk.cout, 1, 0);
+      ru.b1 = rw[13];
+    }
+    c /= 2;
+  }
+  f->cfin = c;
+  const float* const* fw = w + 5 + FLAMED_FAC_BLOCK_W * f->NUP;
+  f->afin = FacAct{fw[0], fw[1], fw[2], fw[3]};
+  f->bout = fw[6];
+  size_t o_out = off;
+  off = al256(off + 4ull * c * 7);
+  size_t o_tmp = off;
+  off = al256(off + 4 * maxfold);
+  if (f->dev) { FL_HIP(hipFree(f->dev)); f->dev = nullptr; }
+  FL_HIP(hipMalloc(&f->dev, off));
+  float* tmp = reinterpret_cast<float*>(f->dev + o_tmp);
+  for (const Conv& cv : convs) {
+    hipLaunchKernelGGL(wn_fold_kernel, dim3(cv.dim0), dim3(256), 0, st, cv.g, cv.v, cv.inner, tmp);
+    FL_LAUNCH_CHECK();
+    size_t total = (size_t)cv.N * cv.Cin * cv.KT;
+    dim3 grid((total + 255) / 256);
+    if (cv.kind == 0) {
+      if (f->dt == FLAMED_BF16) hipLaunchKernelGGL(pack_conv_kernel<bf16>, grid, dim3(256), 0, st, tmp, (bf16*)(f->dev + cv.off), cv.N, cv.Cin, cv.KT);
+      else hipLaunchKernelGGL(pack_conv_kernel<float>, grid, dim3(256), 0, st, tmp, (float*)(f->dev + cv.off), cv.N, cv.Cin, cv.KT);
+    } else {
+      if (f->dt == FLAMED_BF16) hipLaunchKernelGGL(pack_convt_kernel<bf16>, grid, dim3(256), 0, st, tmp, (bf16*)(f->dev + cv.off), cv.Cin, cv.N, cv.s);
+      else hipLaunchKernelGGL(pack_convt_kernel<float>, grid, dim3(256), 0, st, tmp, (float*)(f->dev + cv.off), cv.Cin, cv.N, cv.s);
+    }
+    FL_LAUNCH_CHECK();
+  }
+  // final conv (1, c, 7): folded fp32, kept as (c, 7)
+  hipLaunchKernelGGL(wn_fold_kernel, dim3(1), dim3(256), 0, st, fw[4], fw[5], c * 7, reinterpret_cast<float*>(f->dev + o_out));
+  FL_LAUNCH_CHECK();
+  f->wout = reinterpret_cast<float*>(f->dev + o_out);
+  f->win = f->dev + convs[ci].off;
+  for (int i = 0; i < f->NUP; ++i) {
+    f->blk[i].wt = f->dev + convs[idx_t[i]].off;
+    for (int j = 0; j < 3; ++j) {
+      f->blk[i].ru[j].w7 = f->dev + convs[idx7[i * 3 + j]].off;
+      f->blk[i].ru[j].w1 = f->dev + convs[idx1[i * 3 + j]].off;
+    }
+  }
+  FL_HIP(hipStreamSynchronize(st));  // the fold scratch is reused per conv on the same stream; drain before returning
+  if (f->gexec) { (void)hipGraphExecDestroy(f->gexec); f->gexec = nullptr; }
+  return kOk;
+}
+
+FLAMED_API size_t flamed_fac_workspace_size(flamed_fac_t h, int B, int T) {
+  Fac* f = reinterpret_cast<Fac*>(h);
+  return f ? fac_ws_layout(f, B, T, nullptr, nullptr) : 0;
+}
+
+FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const float* spk, int B, int T, float* wav,
+                                 void* ws, size_t ws_bytes, int use_graph, hipStream_t st) {
+  Fac* f = reinterpret_cast<Fac*>(h);
+  FL_REQUIRE(f && f->dev, "flamed_fac_decode: handle not loaded");
+  FL_REQUIRE(latents && spk && wav && ws && B > 0 && T > 0, "flamed_fac_decode: bad args");
+  if (ws_bytes < fac_ws_layout(f, B, T, nullptr, nullptr)) {
+    set_error("flamed_fac_decode: workspace too small");
+    return kNoWorkspace;
+  }
+  FacWs w;
+  fac_ws_layout(f, B, T, ws, &w);
+  auto run = [&](hipStream_t s) -> int {
+    return f->dt == FLAMED_BF16 ? fac_decode_impl<bf16>(f, latents, spk, B, T, wav, w, s)
+                                : fac_decode_impl<float>(f, latents, spk, B, T, wav, w, s);
+  };
+  if (!use_graph) return run(st);
+  std::vector<const void*> key = {latents, spk, wav, ws, (const void*)(intptr_t)B, (const void*)(intptr_t)T, f->dev};
+  if (!f->gexec || f->gkey != key) {
+    if (f->gexec) { FL_HIP(hipGraphExecDestroy(f->gexec)); f->gexec = nullptr; }
+    if (!f->cap) FL_HIP(hipStreamCreateWithFlags(&f->cap, hipStreamNonBlocking));
+    FL_HIP(hipStreamBeginCapture(f->cap, hipStreamCaptureModeRelaxed));
+    int r = run(f->cap);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(f->cap, &g);
+    if (r) { if (g) (void)hipGraphDestroy(g); return r; }
+    FL_HIP(e);
+    hipError_t ie = hipGraphInstantiate(&f->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    FL_HIP(ie);
+    f->gkey = key;
+  }
+  FL_HIP(hipGraphLaunch(f->gexec, st));
+  return kOk;
+}
+
+}  // extern "C"

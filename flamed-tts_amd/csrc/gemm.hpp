@@ -318,6 +318,7 @@ struct LoadConvRows {
   int Cin;
   int L;
   int KT;
+  int dil;
   const float* __restrict__ S;  // LN partials of x rows (LN only)
   int NT, tw;
   float eps;
@@ -339,8 +340,9 @@ struct LoadConvRows {
   __device__ Raw issue(int m, int k) const {
     Raw r;
     int tap = k / Cin, c = k - tap * Cin;
-    int l = m % L + tap - KT / 2;
-    r.src = (l >= 0 && l < L) ? m + tap - KT / 2 : -1;
+    int off = (tap - KT / 2) * dil;
+    int l = m % L + off;
+    r.src = (l >= 0 && l < L) ? m + off : -1;
     if (r.src >= 0) {
       const float* px = x + (size_t)r.src * Cin + c;
 #pragma unroll
@@ -373,6 +375,27 @@ struct LoadConvRows {
     }
     return pack_chunk<D>(o);
   }
+};
+
+// Dilated conv gather over a DT activation (no transform): K index = tap*Cin + c.
+template <typename DT>
+struct LoadConvPlain {
+  const DT* __restrict__ x;
+  int Cin;
+  int L;
+  int KT;
+  int dil;
+  struct Raw { uint4 v; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    int tap = k / Cin, c = k - tap * Cin;
+    int off = (tap - KT / 2) * dil;
+    int l = m % L + off;
+    if (l < 0 || l >= L) return Raw{make_uint4(0u, 0u, 0u, 0u)};
+    return Raw{*reinterpret_cast<const uint4*>(x + (size_t)(m + off) * Cin + c)};
+  }
+  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
 };
 
 // Host-side launcher.

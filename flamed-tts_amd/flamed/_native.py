@@ -42,6 +42,12 @@ SIGNATURES = {
     "flamed_pva_flow": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_lr_lengths": (c_int, [P, P, P, c_int, c_int, c_int, P, P, P]),
     "flamed_lr_expand": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
+    "flamed_fac_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), c_int, ctypes.POINTER(P)]),
+    "flamed_fac_destroy": (c_int, [P]),
+    "flamed_fac_num_weights": (c_int, [P]),
+    "flamed_fac_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_fac_workspace_size": (c_size_t, [P, c_int, c_int]),
+    "flamed_fac_decode": (c_int, [P, P, P, c_int, c_int, P, P, c_size_t, c_int, P]),
 }
 
 FLAMED_F32, FLAMED_BF16 = 0, 1

@@ -1,0 +1,244 @@
+"""FaCodec decoder — inference path (drop-in for reference flamed/models/facodec/facodec.py).
+
+Implemented here: the waveform decoder used by Flamed.sample_batch (`FACodecDecoder.inference`,
+reference :630-638) with the same module tree and state-dict keys (`model.*` with weight-norm
+`weight_g`/`weight_v`, alias-free filter buffers, `timbre_linear.*`).  On a CUDA (ROCm) device the
+whole decoder runs in the gfx950 HIP library (weight norm folded at load, implicit-GEMM convs on MFMA,
+polyphase ConvTranspose, fused Activation1d, graph-captured); the library is mandatory there.
+
+Not implemented in this round (prompt encoding): the quantizers, timbre encoder
+and the training-only predictor heads.  Their checkpoint entries are accepted by `load_state_dict`
+and kept in `self.unused_state` so the released decoder checkpoint loads for decoding.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn.utils import weight_norm
+
+from flamed import _native as nat
+from .alias_free_torch import Activation1d
+
+
+def WNConv1d(*args, **kwargs):
+    return weight_norm(nn.Conv1d(*args, **kwargs))
+
+
+def WNConvTranspose1d(*args, **kwargs):
+    return weight_norm(nn.ConvTranspose1d(*args, **kwargs))
+
+
+class SnakeBeta(nn.Module):
+    """x + 1/(beta + 1e-9) * sin(alpha * x)^2 with per-channel (optionally log-scale) alpha, beta
+    (reference :57-118)."""
+
+    def __init__(self, in_features, alpha=1.0, alpha_trainable=True, alpha_logscale=False):
+        super().__init__()
+        self.in_features = in_features
+        self.alpha_logscale = alpha_logscale
+        init = torch.zeros(in_features) if alpha_logscale else torch.ones(in_features)
+        self.alpha = nn.Parameter(init * alpha)
+        self.beta = nn.Parameter(init.clone() * alpha)
+        self.alpha.requires_grad = alpha_trainable
+        self.beta.requires_grad = alpha_trainable
+        self.no_div_by_zero = 0.000000001
+
+    def forward(self, x):
+        a = self.alpha.unsqueeze(0).unsqueeze(-1)
+        b = self.beta.unsqueeze(0).unsqueeze(-1)
+        if self.alpha_logscale:
+            a, b = torch.exp(a), torch.exp(b)
+        return x + (1.0 / (b + self.no_div_by_zero)) * torch.pow(torch.sin(x * a), 2)
+
+
+def _act(dim):
+    return Activation1d(activation=SnakeBeta(dim, alpha_logscale=True))
+
+
+class ResidualUnit(nn.Module):
+    """x + conv1x1(act(conv7_dilated(act(x)))) (reference :121-133)."""
+
+    def __init__(self, dim: int = 16, dilation: int = 1):
+        super().__init__()
+        self.block = nn.Sequential(_act(dim), WNConv1d(dim, dim, kernel_size=7, dilation=dilation,
+                                                       padding=((7 - 1) * dilation) // 2),
+                                   _act(dim), WNConv1d(dim, dim, kernel_size=1))
+
+    def forward(self, x):
+        return x + self.block(x)
+
+
+class DecoderBlock(nn.Module):
+    """act -> ConvTranspose(k=2s, stride s) -> 3 residual units (dilation 1, 3, 9) (reference :246-265)."""
+
+    def __init__(self, input_dim: int = 16, output_dim: int = 8, stride: int = 1):
+        super().__init__()
+        self.block = nn.Sequential(
+            _act(input_dim),
+            WNConvTranspose1d(input_dim, output_dim, kernel_size=2 * stride, stride=stride,
+                              padding=stride // 2 + stride % 2, output_padding=stride % 2),
+            ResidualUnit(output_dim, dilation=1), ResidualUnit(output_dim, dilation=3),
+            ResidualUnit(output_dim, dilation=9))
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class FACodecDecoder(nn.Module):
+    """FaCodec waveform decoder (reference :268-660, inference subset)."""
+
+    default_ckpt = os.path.join(os.path.dirname(__file__), "checkpoints", "ns3_facodec_decoder.bin")
+
+    @classmethod
+    def from_pretrained(cls, cfg, ckpt_path=None):
+        dec = cls(in_channels=cfg["in_channels"], upsample_initial_channel=cfg["upsample_initial_channel"],
+                  ngf=cfg["ngf"], up_ratios=cfg["up_ratios"], vq_num_q_c=cfg["vq_num_q_c"],
+                  vq_num_q_p=cfg["vq_num_q_p"], vq_num_q_r=cfg["vq_num_q_r"], vq_dim=cfg["vq_dim"],
+                  codebook_dim=cfg["codebook_dim"], codebook_size_prosody=cfg["codebook_size_prosody"],
+                  codebook_size_content=cfg["codebook_size_content"],
+                  codebook_size_residual=cfg["codebook_size_residual"], use_gr_x_timbre=cfg["use_gr_x_timbre"],
+                  use_gr_residual_f0=cfg["use_gr_residual_f0"], use_gr_residual_phone=cfg["use_gr_residual_phone"])
+        sd = torch.load(ckpt_path or cls.default_ckpt, map_location=cfg.get("device", "cpu"), weights_only=True)
+        dec.load_state_dict(sd)
+        return dec.eval()
+
+    def __init__(self, in_channels=256, upsample_initial_channel=1536, ngf=32, up_ratios=(5, 5, 4, 2),
+                 vq_num_q_c=2, vq_num_q_p=1, vq_num_q_r=3, vq_dim=1024, vq_commit_weight=0.005,
+                 vq_weight_init=False, vq_full_commit_loss=False, codebook_dim=8, codebook_size_prosody=10,
+                 codebook_size_content=10, codebook_size_residual=10, quantizer_dropout=0.0, dropout_type="linear",
+                 use_gr_content_f0=False, use_gr_prosody_phone=False, use_gr_residual_f0=False,
+                 use_gr_residual_phone=False, use_gr_x_timbre=False, use_random_mask_residual=True,
+                 prob_random_mask_residual=0.75):
+        super().__init__()
+        self.in_channels = in_channels
+        self.upsample_initial_channel = upsample_initial_channel
+        self.hop_length = int(np.prod(up_ratios))
+        self.ngf = ngf
+        self.up_ratios = list(up_ratios)
+        ch = upsample_initial_channel
+        layers: List[nn.Module] = [WNConv1d(in_channels, ch, kernel_size=7, padding=3)]
+        out_dim = ch
+        for i, stride in enumerate(self.up_ratios):
+            layers.append(DecoderBlock(ch // 2 ** i, ch // 2 ** (i + 1), stride))
+            out_dim = ch // 2 ** (i + 1)
+        layers += [_act(out_dim), WNConv1d(out_dim, 1, kernel_size=7, padding=3), nn.Tanh()]
+        self.model = nn.Sequential(*layers)
+        self.timbre_linear = nn.Linear(in_channels, in_channels * 2)
+        with torch.no_grad():
+            self.timbre_linear.bias[:in_channels] = 1
+            self.timbre_linear.bias[in_channels:] = 0
+        self.timbre_norm = nn.LayerNorm(in_channels, elementwise_affine=False)
+        self.unused_state: Dict[str, torch.Tensor] = {}
+        self.hip_dtype = "bf16"
+        self.hip_graph = True
+        self._hip = None
+        for m in self.modules():
+            if isinstance(m, nn.Conv1d):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.constant_(m.bias, 0)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        own = set(self.state_dict().keys())
+        extra = {k: v for k, v in state_dict.items() if k not in own}
+        self.unused_state = extra
+        return super().load_state_dict({k: v for k, v in state_dict.items() if k in own}, strict=strict, assign=assign)
+
+    def _use_hip(self, x):
+        return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+
+    def inference(self, x, speaker_embedding):
+        """latents (B, in_channels, T), speaker (B, in_channels) -> wav (B, 1, hop*T)."""
+        if self._use_hip(x):
+            if self._hip is None or self._hip.dtype_name != self.hip_dtype:
+                self._hip = FacDecoderHIP(self, self.hip_dtype)
+            return self._hip.decode(x, speaker_embedding)
+        gamma, beta = self.timbre_linear(speaker_embedding).unsqueeze(2).chunk(2, 1)
+        h = self.timbre_norm(x.transpose(1, 2)).transpose(1, 2)
+        return self.model(h * gamma + beta)
+
+
+def fac_weight_list(dec: FACodecDecoder) -> List[torch.Tensor]:
+    """Weights in the order flamed_fac_load expects (include/flamed_hip.h)."""
+
+    def act(a):
+        return [a.act.alpha, a.act.beta, a.upsample.filter, a.downsample.lowpass.filter]
+
+    def wn(c):
+        return [c.weight_g, c.weight_v, c.bias]
+
+    m = dec.model
+    w = [dec.timbre_linear.weight, dec.timbre_linear.bias] + wn(m[0])
+    nup = len(dec.up_ratios)
+    for i in range(nup):
+        blk = m[1 + i].block
+        w += act(blk[0]) + wn(blk[1])
+        for j in range(2, 5):
+            ru = blk[j].block
+            w += act(ru[0]) + wn(ru[1]) + act(ru[2]) + wn(ru[3])
+    w += act(m[1 + nup]) + wn(m[2 + nup])
+    return w
+
+
+class FacDecoderHIP:
+    """Owns one flamed_fac_t handle."""
+
+    def __init__(self, dec: FACodecDecoder, dtype_name: str):
+        self.dec = dec
+        self.dtype_name = dtype_name
+        self.handle = None
+        self._sig = None
+        self._keep = []
+        self.ws = nat.Workspace()
+        self._bufs = {}
+
+    def __del__(self):
+        try:
+            if self.handle is not None:
+                nat.lib().flamed_fac_destroy(self.handle)
+        except Exception:
+            pass
+
+    def _ensure(self, dev):
+        params = fac_weight_list(self.dec)
+        sig = tuple((p.data_ptr(), p._version) for p in params) + (str(dev),)
+        if sig == self._sig:
+            return
+        L = nat.lib()
+        if self.handle is None:
+            h = ctypes.c_void_p()
+            ups = (ctypes.c_int * len(self.dec.up_ratios))(*self.dec.up_ratios)
+            nat.check(L.flamed_fac_create(self.dec.in_channels, self.dec.upsample_initial_channel,
+                                          len(self.dec.up_ratios), ups, nat.dtype_code(self.dtype_name),
+                                          ctypes.byref(h)), "flamed_fac_create")
+            self.handle = h
+        keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
+        arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
+        nat.check(L.flamed_fac_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_fac_load")
+        self._keep = keep
+        self._sig = sig
+        self._bufs = {}
+
+    def decode(self, x, spk):
+        dev = x.device
+        self._ensure(dev)
+        B, C, T = x.shape
+        key = (B, T)
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            bufs = {"x": torch.empty((B, C, T), dtype=torch.float32, device=dev),
+                    "s": torch.empty((B, C), dtype=torch.float32, device=dev),
+                    "wav": torch.empty((B, 1, self.dec.hop_length * T), dtype=torch.float32, device=dev)}
+            self._bufs = {key: bufs}
+        bufs["x"].copy_(x)
+        bufs["s"].copy_(spk)
+        L = nat.lib()
+        ws = self.ws.get(L.flamed_fac_workspace_size(self.handle, B, T), dev)
+        nat.check(L.flamed_fac_decode(self.handle, nat.ptr(bufs["x"]), nat.ptr(bufs["s"]), B, T, nat.ptr(bufs["wav"]),
+                                      nat.ptr(ws), ws.numel(), int(bool(self.dec.hip_graph)), nat.stream_ptr(dev)),
+                  "flamed_fac_decode")
+        return bufs["wav"].clone()

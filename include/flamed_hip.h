@@ -128,6 +128,31 @@ FLAMED_API int flamed_lr_lengths(const float* phone, const float* sil, const int
 FLAMED_API int flamed_lr_expand(const float* x, const int64_t* cum, int B, int L, int H, int T_out, float* out,
                                 hipStream_t stream);
 
+/* ================================ FaCodec decoder (inference) ================================
+ * Replaces FACodecDecoder.inference (facodec.py:630-638) and its model stack (:398-415).
+ * Weight order for flamed_fac_load (fp32 device tensors as in the decoder state dict):
+ *   timbre_linear.{weight,bias}, model.0.{weight_g,weight_v,bias},
+ *   per DecoderBlock model.{1..n_up}.block (FLAMED_FAC_BLOCK_W = 49 each):
+ *     0.act.{alpha,beta}, 0.upsample.filter, 0.downsample.lowpass.filter, 1.{weight_g,weight_v,bias},
+ *     then for each ResidualUnit j in 2,3,4: j.block.0.act.{alpha,beta}, j.block.0.upsample.filter,
+ *     j.block.0.downsample.lowpass.filter, j.block.1.{weight_g,weight_v,bias}, j.block.2.act.{alpha,beta},
+ *     j.block.2.upsample.filter, j.block.2.downsample.lowpass.filter, j.block.3.{weight_g,weight_v,bias}
+ *   final: model.{n_up+1}.act.{alpha,beta}, .upsample.filter, .downsample.lowpass.filter,
+ *          model.{n_up+2}.{weight_g,weight_v,bias}
+ * Weight norm is folded and conv weights packed at load; vectors are referenced in place. */
+enum { FLAMED_FAC_BLOCK_W = 49 };
+typedef struct flamed_fac_s* flamed_fac_t;
+FLAMED_API int flamed_fac_create(int in_channels, int upsample_initial_channel, int n_up, const int* up_ratios, int dtype,
+                                 flamed_fac_t* out);
+FLAMED_API int flamed_fac_destroy(flamed_fac_t h);
+FLAMED_API int flamed_fac_num_weights(flamed_fac_t h);
+FLAMED_API int flamed_fac_load(flamed_fac_t h, const float* const* weights, int n_weights, hipStream_t stream);
+FLAMED_API size_t flamed_fac_workspace_size(flamed_fac_t h, int B, int T);
+/* latents: (B, in_channels, T) channels-first as the reference passes them; spk: (B, in_channels);
+ * wav: (B, hop*T) with hop = prod(up_ratios).  use_graph != 0 replays a cached hipGraph. */
+FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const float* spk, int B, int T, float* wav,
+                                 void* ws, size_t ws_bytes, int use_graph, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
