@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--kernel-iters", type=int, default=10, help="eager steps timed in-context per kernel class")
     return ap.parse_args()
 
 
@@ -150,6 +150,7 @@ def main():
         ms = (ctypes.c_float * N_CLASSES)()
         nat.check(L.flamed_den_time_kernels(hip.handle, nat.ptr(xs), nat.ptr(mods), B, T, nat.ptr(ws), ws.numel(),
                                             args.kernel_iters, ms, nat.stream_ptr(dev)), "flamed_den_time_kernels")
+        torch.cuda.synchronize()
     es = 2 if args.dtype == "bf16" else 4
     kernels = []
     for cls in range(N_CLASSES):
@@ -167,7 +168,15 @@ def main():
     else:
         roof = {"bound": "mfma", "achieved": dom["TFLOPs"], "peak": MFMA_PEAK_TFS[args.dtype], "unit": "TFLOP/s",
                 "frac": round(dom["TFLOPs"] / MFMA_PEAK_TFS[args.dtype], 4)}
-    roof.update({"kernel": dom["name"], "launch_us": dom["us"], "traffic": None,
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "latest_traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if (tj.get("batch"), tj.get("frames"), tj.get("dtype")) == (B, T, args.dtype):
+            traffic = tj.get("bytes_per_launch", {}).get(dom["name"])
+    roof.update({"kernel": dom["name"], "launch_us": dom["us"], "traffic": traffic,
+                 "traffic_source": "rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, profiles/latest_traffic.json"
+                 if traffic is not None else None,
                  "algorithmic_bytes": dom["bytes"], "algorithmic_flops": dom["flops"]})
 
     # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only), bounded sample

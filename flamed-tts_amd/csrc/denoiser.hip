@@ -596,53 +596,68 @@ FLAMED_API size_t flamed_den_workspace_size(flamed_den_t h, int B, int T) {
 
 namespace fl {
 
-// One velocity evaluation (+ Euler update when vout == nullptr).  `only` >= 0 launches only the
-// kernel class `only` (diagnostic timing, see flamed_den_time_kernels).
+// In-context kernel timer (diagnostic): when set, an event is recorded after every launch of a
+// full step, tagged with the kernel class, so per-kernel device time is measured inside the real
+// sequence (flamed_den_time_kernels).
+struct KTimer {
+  static constexpr int kMax = 128;
+  hipEvent_t ev[kMax];
+  int cls[kMax];
+  int n = 0;
+};
+static thread_local KTimer* g_kt = nullptr;
+static inline void kt_mark(int c, hipStream_t st) {
+  if (g_kt && g_kt->n < KTimer::kMax) {
+    (void)hipEventRecord(g_kt->ev[g_kt->n], st);
+    g_kt->cls[g_kt->n++] = c;
+  }
+}
+
+// One velocity evaluation (+ Euler update when vout == nullptr).
 template <typename DT, int BM, int BN, int KCH>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
-                         const DenWs& w, hipStream_t st, int only = -1) {
+                         const DenWs& w, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
-#define K_(cls) if (only < 0 || only == (cls))
-  K_(0) TRY((launch_gemm<BM, BN, KCH, DT>(LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
-  const int nb = only < 0 ? d->NB : 1;
-  for (int i = 0; i < nb; ++i) {
+#define K_(cls, x) do { TRY(x); kt_mark(cls, st); } while (0)
+  K_(0, (launch_gemm<BM, BN, KCH, DT>(LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
+  for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div};
-    K_(1) TRY((launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
-    K_(2) TRY((launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
-    K_(3) TRY((launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
-                                            EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
-    K_(4) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
-                                            EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
-                                            M, H, H, st)));
-    K_(5) TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
-                                            EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
-    K_(6) TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
-                                            EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
+    K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
+    K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
+    K_(3, (launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
+                                        EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    K_(4, (launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+                                        EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
+                                        M, H, H, st)));
+    K_(5, (launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
+                                        EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
+    K_(6, (launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
+                                        EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
   ModRef mc{mf, mf + H, MS, mod_div};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div};
   const DenBlockW& F = d->fin;
-  if (only < 0) {
-    TRY((launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 0)));
-    TRY((launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
-    TRY((launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
+  K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
+  K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
+  K_(3, (launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  K_(4, (launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                       EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
                                       M, H, H, st)));
-  }
-  K_(7) TRY((launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr}, (const DT*)d->wout, H,
-                                          EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
-  K_(8) {
+  K_(7, (launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr}, (const DT*)d->wout, H,
+                                      EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
+  {
     size_t n = (size_t)M * C;
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt);
     FL_LAUNCH_CHECK();
+    kt_mark(8, st);
   }
 #undef K_
 #undef TRY
@@ -650,17 +665,17 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
 }
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
-                    hipStream_t st, int only = -1) {
+                    hipStream_t st) {
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   const int M = B * T;
   const bool big = M >= 4096;
   if (d->dt == FLAMED_BF16) {
-    return big ? den_step_impl<bf16, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only)
-               : den_step_impl<bf16, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only);
+    return big ? den_step_impl<bf16, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st)
+               : den_step_impl<bf16, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
   }
-  return big ? den_step_impl<float, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only)
-             : den_step_impl<float, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st, only);
+  return big ? den_step_impl<float, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st)
+             : den_step_impl<float, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
 }
 
 }  // namespace fl
@@ -742,23 +757,30 @@ FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* m
     set_error("flamed_den_time_kernels: workspace too small");
     return kNoWorkspace;
   }
-  hipEvent_t e0, e1;
-  FL_HIP(hipEventCreate(&e0));
-  FL_HIP(hipEventCreate(&e1));
-  int rc = kOk;
-  for (int cls = 0; cls < FLAMED_DEN_KERNEL_CLASSES && rc == kOk; ++cls) {
-    rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st, cls);  // warm
+  KTimer kt;
+  for (int i = 0; i < KTimer::kMax; ++i) FL_HIP(hipEventCreate(&kt.ev[i]));
+  double sum[FLAMED_DEN_KERNEL_CLASSES] = {0};
+  int cnt[FLAMED_DEN_KERNEL_CLASSES] = {0};
+  int rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st);  // warm
+  for (int it = 0; it < iters && rc == kOk; ++it) {
+    kt.n = 0;
+    (void)hipEventRecord(kt.ev[0], st);
+    kt.cls[0] = -1;
+    kt.n = 1;
+    g_kt = &kt;
+    rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st);
+    g_kt = nullptr;
     if (rc) break;
-    FL_HIP(hipEventRecord(e0, st));
-    for (int i = 0; i < iters && rc == kOk; ++i) rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st, cls);
-    FL_HIP(hipEventRecord(e1, st));
-    FL_HIP(hipEventSynchronize(e1));
-    float ms = 0.f;
-    FL_HIP(hipEventElapsedTime(&ms, e0, e1));
-    ms_out[cls] = ms / iters;
+    FL_HIP(hipEventSynchronize(kt.ev[kt.n - 1]));
+    for (int i = 1; i < kt.n; ++i) {
+      float ms = 0.f;
+      FL_HIP(hipEventElapsedTime(&ms, kt.ev[i - 1], kt.ev[i]));
+      sum[kt.cls[i]] += ms;
+      cnt[kt.cls[i]] += 1;
+    }
   }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  for (int c = 0; c < FLAMED_DEN_KERNEL_CLASSES; ++c) ms_out[c] = cnt[c] ? (float)(sum[c] / cnt[c]) : 0.f;
+  for (int i = 0; i < KTimer::kMax; ++i) (void)hipEventDestroy(kt.ev[i]);
   return rc;
 }
 

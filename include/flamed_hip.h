@@ -87,12 +87,14 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t stream);
 
-/* Diagnostic: average device time (ms, HIP events on `stream`) of each kernel class of one Euler
- * step, each launched `iters` times in isolation: 0 proj_in GEMM, 1 LN/mod+depthwise conv (+GN
+/* Diagnostic: average device time per launch (ms) of each kernel class of an Euler step, measured
+ * IN CONTEXT: `iters` full steps run eagerly with a HIP event recorded on `stream` after every
+ * launch (the interval before a launch's end event = that kernel, incl. its dispatch gap).
+ * Classes: 0 proj_in GEMM, 1 LN/mod+depthwise conv (+GN
  * partials), 2 GroupNorm finalize, 3 GN-apply+conv_2 GEMM+GELU, 4 conv_3 GEMM+gated residual,
  * 5 LN/mod+mlp.0 GEMM+SiLU, 6 mlp.2 GEMM+gated residual, 7 LN/mod+conv_out tap-stacked GEMM,
- * 8 conv_out tap combine + Euler update.  ms_out must hold FLAMED_DEN_KERNEL_CLASSES floats.
- * Clobbers xt and the workspace (pass scratch copies). */
+ * 8 conv_out tap combine.  ms_out must hold FLAMED_DEN_KERNEL_CLASSES floats.  Runs dt = 0 steps
+ * (xt unchanged); clobbers the workspace. */
 enum { FLAMED_DEN_KERNEL_CLASSES = 9 };
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                        size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);

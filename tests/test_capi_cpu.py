@@ -1,0 +1,62 @@
+"""C-ABI library: loads without a GPU, exports every symbol include/flamed_hip.h declares, and its
+host-side argument validation reports errors through flamed_last_error (no GPU work involved)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from _common import PKG
+
+HDR = os.path.join(os.path.dirname(PKG), "include", "flamed_hip.h")
+
+
+def declared():
+    src = open(HDR).read()
+    return re.findall(r"FLAMED_API\s+[\w\s\*]+?\b(flamed_\w+)\s*\(", src)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from flamed import _native
+    return _native.lib()
+
+
+def test_header_declares_entry_points():
+    names = declared()
+    assert len(names) >= 25
+    for n in ("flamed_den_solve", "flamed_pva_flow", "flamed_lr_lengths", "flamed_lr_expand", "flamed_fac_decode"):
+        assert n in names
+
+
+def test_every_declared_symbol_is_exported(lib):
+    missing = [n for n in declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_bindings_cover_header():
+    from flamed import _native
+    assert set(declared()) == set(_native.SIGNATURES)
+
+
+def test_host_side_validation_errors(lib):
+    from flamed import _native
+    h = ctypes.c_void_p()
+    assert lib.flamed_den_create(256, 100, 4, 31, 256, 1, ctypes.byref(h)) == 1001
+    assert b"unsupported dims" in lib.flamed_last_error()
+    assert lib.flamed_den_create(256, 1024, 4, 7, 256, 1, ctypes.byref(h)) == 1001
+    assert b"kernel_size=31" in lib.flamed_last_error()
+    assert lib.flamed_den_create(256, 1024, 4, 31, 256, 1, ctypes.byref(h)) == 0
+    assert lib.flamed_den_num_weights(h) == 8 + 18 * 4 + 12
+    assert lib.flamed_den_destroy(h) == 0
+    d = ctypes.c_void_p()
+    assert lib.flamed_dur_create(192, 384, 5, ctypes.byref(d)) == 1001
+    assert lib.flamed_dur_create(192, 384, 3, ctypes.byref(d)) == 0
+    assert lib.flamed_dur_destroy(d) == 0
+    f = ctypes.c_void_p()
+    ups = (ctypes.c_int * 4)(5, 5, 4, 2)
+    assert lib.flamed_fac_create(256, 1024, 4, ups, 1, ctypes.byref(f)) == 0
+    assert lib.flamed_fac_num_weights(f) == 208
+    assert lib.flamed_fac_destroy(f) == 0
+    with pytest.raises(RuntimeError, match="status 1001"):
+        _native.check(lib.flamed_den_create(256, 1024, 4, 31, 256, 9, ctypes.byref(h)), "create")

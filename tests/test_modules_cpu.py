@@ -1,0 +1,95 @@
+"""The drop-in modules (flamed-tts_amd/flamed) on CPU — the `--device cpu` plumbing path — against
+the reference golden vectors; state-dict schema; HIP weight-list ordering."""
+import os
+
+import numpy as np
+import torch
+import yaml
+
+from _common import golden, seeded, manifest, t32, rel_l2, PKG
+
+TOL = 2e-5
+
+
+def _pg():
+    from flamed.models.synthesizer.prob_generator import ProbGenerator
+    cfg = yaml.safe_load(open(os.path.join(PKG, "configs", "prob.yaml")))
+    pg = ProbGenerator(cfg).eval()
+    pg.load_state_dict({k[len("prob_generator."):]: v for k, v in seeded("prob_generator").items()})
+    return pg
+
+
+def _pva():
+    from flamed.models.synthesizer.pva import PVA
+    cfg = yaml.safe_load(open(os.path.join(PKG, "configs", "prior.yaml")))["variance_adaptor"]
+    m = PVA(cfg).eval()
+    m.load_state_dict({k[len("prior_generator.pva."):]: v for k, v in seeded("pva").items()})
+    return m
+
+
+def test_state_dict_schemas_match_reference():
+    from flamed.models.facodec import FACodecDecoder
+    pg = _pg()
+    assert {"prob_generator." + k: list(v.shape) for k, v in pg.state_dict().items()} == manifest("prob_generator")
+    m = _pva()
+    assert {"prior_generator.pva." + k: list(v.shape) for k, v in m.state_dict().items()} == manifest("pva")
+    d = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256)
+    ref = manifest("facodec_decoder")
+    assert all(ref[k] == list(v.shape) for k, v in d.state_dict().items())
+    assert set(ref) - set(d.state_dict()) == {k for k in ref if not k.startswith(("model.", "timbre_linear."))}
+
+
+def test_hip_weight_lists():
+    from flamed.models.synthesizer.prob_generator import denoiser_weight_list
+    from flamed.models.facodec import FACodecDecoder
+    from flamed.models.facodec.facodec import fac_weight_list
+    pg = _pg()
+    w = denoiser_weight_list(pg.denoiser)
+    assert len(w) == 8 + 18 * 4 + 12
+    assert w[8] is pg.denoiser.res_blocks[0].adaLN_modulation[1].weight
+    assert w[-2] is pg.denoiser.final_layer.conv_out.weight
+    d = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256)
+    assert len(fac_weight_list(d)) == 208
+    assert len(_pva().duration_generator.hip_weights()) == 16
+
+
+def test_denoiser_and_sample_cpu_path():
+    pg = _pg()
+    g = golden("den_full")
+    with torch.inference_mode():
+        assert rel_l2(pg.denoiser(t32(g["x"]), t32(g["t1"]), t32(g["c"])), g["v1"]) < TOL
+        assert rel_l2(pg.denoiser(t32(g["xB"]), t32(g["tB"]), t32(g["cB"])), g["vB"]) < TOL
+        s = golden("prob_sample")
+        lens = t32(s["lens"])
+        T = s["cond"].shape[2]
+        mask = ~(torch.arange(T)[None, :] >= lens[:, None]).unsqueeze(-1)
+        torch.manual_seed(int(s["rng_seed"]))
+        lat = pg.sample(t32(s["cond"]), t32(s["spk"]), mask, nfe=int(s["nfe"]), temperature=float(s["temperature"]))
+    assert rel_l2(lat, s["latents"]) < TOL
+
+
+def test_pva_cpu_path():
+    m = _pva()
+    g = golden("pva")
+    src_len = t32(g["src_len"])
+    mask = torch.arange(g["enc"].shape[1])[None, :] >= src_len[:, None]
+    with torch.inference_mode():
+        torch.manual_seed(int(g["rng_seed"]))
+        x_lr, tl = m.sample(t32(g["enc"]), src_len, mask, nfe=int(g["nfe"]), temperature=float(g["temperature"]))
+    assert np.array_equal(tl.numpy(), g["tgt_len"]) and np.array_equal(x_lr.numpy(), g["x_lr"])
+    lr = golden("lr_cases")
+    for ci in range(int(lr["n"])):
+        mx = int(lr[f"c{ci}_max"])
+        out, t = m.length_regulator(t32(lr[f"c{ci}_x"]), t32(lr[f"c{ci}_pd"]), t32(lr[f"c{ci}_sd"]),
+                                    t32(lr[f"c{ci}_sl"]), None if mx < 0 else mx)
+        assert np.array_equal(t.numpy(), lr[f"c{ci}_tl"]) and np.array_equal(out.numpy(), lr[f"c{ci}_out"])
+
+
+def test_facodec_cpu_path():
+    from flamed.models.facodec import FACodecDecoder
+    d = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256).eval()
+    d.load_state_dict(seeded("facodec_decoder"))
+    g = golden("facodec")
+    with torch.inference_mode():
+        w = d.inference(t32(g["lat1"]), t32(g["spk1"]))
+    assert rel_l2(w, g["wav1"]) < 1e-4
