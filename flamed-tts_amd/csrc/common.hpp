@@ -10,6 +10,7 @@ namespace fl {
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // SROA-friendly (HIP uint4 is a union struct)
 
 // ---- error reporting (thread-local last error, C-ABI flamed_last_error) ----
 void set_error(const char* fmt, ...);
@@ -87,20 +88,15 @@ template <> struct DTraits<float> {
 };
 
 // 16-byte chunk of DT built from EPC floats.
-template <typename DT> __device__ __forceinline__ uint4 pack_chunk(const float* v);
-template <> __device__ __forceinline__ uint4 pack_chunk<float>(const float* v) {
-  uint4 r;
-  r.x = __float_as_uint(v[0]);
-  r.y = __float_as_uint(v[1]);
-  r.z = __float_as_uint(v[2]);
-  r.w = __float_as_uint(v[3]);
-  return r;
+template <typename DT> __device__ __forceinline__ u32x4 pack_chunk(const float* v);
+template <> __device__ __forceinline__ u32x4 pack_chunk<float>(const float* v) {
+  return u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
 }
-template <> __device__ __forceinline__ uint4 pack_chunk<bf16>(const float* v) {
+template <> __device__ __forceinline__ u32x4 pack_chunk<bf16>(const float* v) {
   bf16x8 b;
 #pragma unroll
   for (int j = 0; j < 8; ++j) b[j] = (bf16)v[j];
-  return *reinterpret_cast<uint4*>(&b);
+  return __builtin_bit_cast(u32x4, b);
 }
 
 template <typename DT> __device__ __forceinline__ void store_val(DT* p, float v) { *p = (DT)v; }

@@ -26,6 +26,11 @@ struct ModRef {  // AdaLN modulation vectors: row = m / div, stride `ms` floats
   int div;
 };
 
+// LayerNorm (+ optional affine) + AdaLN modulate of fp32 rows, converted to DT (A-operand loader).
+// Row stats come from the producer's partials; the per-column modulation vectors
+// alpha = w (1 + scale), beta = b (1 + scale) + shift are staged once per workgroup in LDS for the
+// (at most two) modulation rows the tile touches; otherwise (per-frame t, or T < tile) each chunk
+// is transformed straight from global memory.
 template <typename DT, bool AFF>
 struct LoadLNMod {
   const float* __restrict__ x;
@@ -36,43 +41,58 @@ struct LoadLNMod {
   ModRef mod;
   const float* __restrict__ lnw;
   const float* __restrict__ lnb;
+  int kdim;  // K: columns staged per vector
   static constexpr int EPC = DTraits<DT>::EPC;
-  struct Raw { float v[EPC], s[EPC], h[EPC], w[AFF ? EPC : 1], b[AFF ? EPC : 1]; };
+  static constexpr int kVec = 4;  // 2 slots x (alpha, beta)
+  struct Raw { float v[EPC]; };
   static constexpr int stat_rows(int BM) { return BM; }
-  __device__ void prologue(int bm, int BM, int M, float* st) const {
+  __device__ bool prologue_v(int bm, int BM, int M, int K, float* st, float* vec) const {
     for (int r = threadIdx.x; r < BM; r += blockDim.x) {
       int m = bm + r;
       m = m < M ? m : M - 1;
       row_stats_from_partials(S, m, NT, tw, eps, st[2 * r], st[2 * r + 1]);
     }
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int r0 = bm / mod.div, r1 = last / mod.div;
+    if (r1 - r0 > 1) return false;
+    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * K; idx += blockDim.x) {
+      int slot = idx / K, k = idx - slot * K;
+      size_t mo = (size_t)(r0 + slot) * mod.ms + k;
+      float sc1 = 1.0f + mod.sc[mo];
+      float w = AFF ? lnw[k] : 1.0f, b = AFF ? lnb[k] : 0.0f;
+      vec[(2 * slot) * K + k] = w * sc1;
+      vec[(2 * slot + 1) * K + k] = b * sc1 + mod.sh[mo];
+    }
+    return true;
   }
-  __device__ Raw issue(int m, int k) const {
+  __device__ Raw issue_v(int m, int k, bool) const {
     Raw r;
     const float* px = x + (size_t)m * ld + k;
-    size_t mo = (size_t)(m / mod.div) * mod.ms + k;
 #pragma unroll
     for (int j = 0; j < EPC; j += 4) {
-      float4 a = ld4(px + j), s = ld4(mod.sc + mo + j), h = ld4(mod.sh + mo + j);
+      float4 a = ld4(px + j);
       r.v[j] = a.x; r.v[j + 1] = a.y; r.v[j + 2] = a.z; r.v[j + 3] = a.w;
-      r.s[j] = s.x; r.s[j + 1] = s.y; r.s[j + 2] = s.z; r.s[j + 3] = s.w;
-      r.h[j] = h.x; r.h[j + 1] = h.y; r.h[j + 2] = h.z; r.h[j + 3] = h.w;
-      if constexpr (AFF) {
-        float4 w = ld4(lnw + k + j), b = ld4(lnb + k + j);
-        r.w[j] = w.x; r.w[j + 1] = w.y; r.w[j + 2] = w.z; r.w[j + 3] = w.w;
-        r.b[j] = b.x; r.b[j + 1] = b.y; r.b[j + 2] = b.z; r.b[j + 3] = b.w;
-      }
     }
     return r;
   }
   template <typename D>
-  __device__ uint4 finish(const Raw& r, int m, int, const float* st, int bm) const {
+  __device__ u32x4 finish_v(const Raw& r, int m, int k, const float* st, const float* vec, bool use, int bm) const {
     const float mean = st[2 * (m - bm)], rstd = st[2 * (m - bm) + 1];
     float o[EPC];
+    if (use) {
+      const int slot = m / mod.div - bm / mod.div;
+      const float* va = vec + (size_t)(2 * slot) * kdim + k;
+      const float* vb = vec + (size_t)(2 * slot + 1) * kdim + k;
 #pragma unroll
-    for (int j = 0; j < EPC; ++j) {
-      float xh = (r.v[j] - mean) * rstd;
-      if constexpr (AFF) xh = xh * r.w[j] + r.b[j];
-      o[j] = xh * (1.0f + r.s[j]) + r.h[j];
+      for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - mean) * rstd) * va[j] + vb[j];
+    } else {  // rare path (per-frame t or tiles spanning > 2 modulation rows): vectors from global
+      size_t mo = (size_t)(m / mod.div) * mod.ms + k;
+#pragma unroll
+      for (int j = 0; j < EPC; ++j) {
+        float sc1 = 1.0f + mod.sc[mo + j];
+        float w = AFF ? lnw[k + j] : 1.0f, b = AFF ? lnb[k + j] : 0.0f;
+        o[j] = ((r.v[j] - mean) * rstd) * (w * sc1) + (b * sc1 + mod.sh[mo + j]);
+      }
     }
     return pack_chunk<D>(o);
   }
@@ -92,11 +112,12 @@ struct LoadAdaY {
     float4 a = ld4(te + (size_t)tidx[m] * H + k), b = ld4(ce + (size_t)sidx[m] * H + k);
     return Raw{{silu(a.x + b.x), silu(a.y + b.y), silu(a.z + b.z), silu(a.w + b.w)}};
   }
-  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
 };
 
 // X = X + gate * (h + acc + b3), h = LN(X)(+affine) * (1 + sc) + sh recomputed from the same
-// stats the dwconv_gn prologue used; emits LN partials of the new X.
+// stats the dwconv prologue used; emits LN partials of the new X.  Per-column vectors
+// [alpha, beta, gate] x 2 modulation rows + b3 are staged in LDS (kEVec = 8 floats per column).
 template <bool AFF>
 struct EpiConvNeXtResid {
   const float* __restrict__ b3;
@@ -112,20 +133,41 @@ struct EpiConvNeXtResid {
   float* __restrict__ Sout;
   int NTout;
   static constexpr bool kRowStats = true;
+  static constexpr int kEVec = 8;
   static constexpr int stat_rows(int BM) { return BM; }
-  __device__ void prologue(int bm, int BM, int M, float* st) const {
+  __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
     for (int r = threadIdx.x; r < BM; r += blockDim.x) {
       int m = bm + r;
       m = m < M ? m : M - 1;
       row_stats_from_partials(Sin, m, NTin, twin, eps, st[2 * r], st[2 * r + 1]);
     }
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int r0 = bm / mod.div, r1 = last / mod.div;
+    if (r1 - r0 > 1) return false;
+    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {
+      int slot = idx / BN, c = idx - slot * BN, n = bn + c;
+      size_t mo = (size_t)(r0 + slot) * mod.ms + n;
+      float sc1 = 1.0f + mod.sc[mo];
+      float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
+      vec[c * 8 + slot * 3 + 0] = w * sc1;
+      vec[c * 8 + slot * 3 + 1] = b * sc1 + mod.sh[mo];
+      vec[c * 8 + slot * 3 + 2] = gate[mo];
+      if (slot == 0) vec[c * 8 + 6] = b3[n];
+    }
+    return true;
   }
-  __device__ float value(int m, int n, float acc, const float* st, int bm) const {
+  __device__ float value_v(int m, int n, float acc, const float* st, const float* vec, bool use, int bm, int bn) const {
     float x = X[(size_t)m * ld + n];
-    size_t mo = (size_t)(m / mod.div) * mod.ms + n;
     float xh = (x - st[2 * (m - bm)]) * st[2 * (m - bm) + 1];
-    if constexpr (AFF) xh = xh * lnw[n] + lnb[n];
-    float h = xh * (1.0f + mod.sc[mo]) + mod.sh[mo];
+    if (use) {
+      const float* v = vec + (n - bn) * 8 + (m / mod.div - bm / mod.div) * 3;
+      float h = xh * v[0] + v[1];
+      return x + v[2] * (h + (acc + vec[(n - bn) * 8 + 6]));
+    }
+    size_t mo = (size_t)(m / mod.div) * mod.ms + n;
+    float sc1 = 1.0f + mod.sc[mo];
+    float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
+    float h = xh * (w * sc1) + (b * sc1 + mod.sh[mo]);
     return x + gate[mo] * (h + (acc + b3[n]));
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
@@ -134,7 +176,7 @@ struct EpiConvNeXtResid {
   }
 };
 
-struct EpiGatedResid {  // X = X + gate * (acc + b)
+struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged per column
   const float* __restrict__ b;
   float* X;
   int ld;
@@ -143,10 +185,26 @@ struct EpiGatedResid {  // X = X + gate * (acc + b)
   float* __restrict__ Sout;
   int NTout;
   static constexpr bool kRowStats = true;
+  static constexpr int kEVec = 4;
   static constexpr int stat_rows(int) { return 0; }
-  __device__ void prologue(int, int, int, float*) const {}
-  __device__ float value(int m, int n, float acc, const float*, int) const {
-    return X[(size_t)m * ld + n] + gate[(size_t)(m / div) * ms + n] * (acc + b[n]);
+  __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float*, float* vec) const {
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int r0 = bm / div, r1 = last / div;
+    if (r1 - r0 > 1) return false;
+    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {
+      int slot = idx / BN, c = idx - slot * BN, n = bn + c;
+      vec[c * 4 + slot] = gate[(size_t)(r0 + slot) * ms + n];
+      if (slot == 0) vec[c * 4 + 2] = b[n];
+    }
+    return true;
+  }
+  __device__ float value_v(int m, int n, float acc, const float*, const float* vec, bool use, int bm, int bn) const {
+    float x = X[(size_t)m * ld + n];
+    if (use) {
+      const float* v = vec + (n - bn) * 4;
+      return x + v[m / div - bm / div] * (acc + v[2]);
+    }
+    return x + gate[(size_t)(m / div) * ms + n] * (acc + b[n]);
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
@@ -286,40 +344,58 @@ static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, in
   return kOk;
 }
 
-// conv_2 A operand: GroupNorm applied on the fly, A = ((D - mean) * rstd) * gn_w + gn_b.
+// conv_2 A operand: GroupNorm applied on the fly, A = (D - mean) * (rstd * gn_w) + gn_b, with
+// [mean, rstd*gn_w] per (utterance, channel) staged in LDS for the <= 2 utterances of the tile.
 template <typename DT>
 struct LoadGN {
   const float* __restrict__ D;
   int H;
-  const float* __restrict__ gns;
+  const float* __restrict__ gns;  // (B, H, 2) = (mean, rstd)
   const float* __restrict__ gnw;
   const float* __restrict__ gnb;
   int T;
   static constexpr int EPC = DTraits<DT>::EPC;
-  struct Raw { float v[EPC], mu[EPC], rs[EPC], w[EPC], b[EPC]; };
+  static constexpr int kVec = 5;  // 2 slots x (mean, scale) + bias
+  struct Raw { float v[EPC]; };
   static constexpr int stat_rows(int) { return 0; }
-  __device__ void prologue(int, int, int, float*) const {}
-  __device__ Raw issue(int m, int k) const {
+  __device__ bool prologue_v(int bm, int BM, int M, int K, float*, float* vec) const {
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int b0 = bm / T, b1 = last / T;
+    if (b1 - b0 > 1) return false;
+    for (int idx = threadIdx.x; idx < (b1 - b0 + 1) * K; idx += blockDim.x) {
+      int slot = idx / K, k = idx - slot * K;
+      const float* g = gns + ((size_t)(b0 + slot) * H + k) * 2;
+      vec[(2 * slot) * K + k] = g[0];
+      vec[(2 * slot + 1) * K + k] = g[1] * gnw[k];
+      if (slot == 0) vec[4 * K + k] = gnb[k];
+    }
+    return true;
+  }
+  __device__ Raw issue_v(int m, int k, bool) const {
     Raw r;
     const float* pd = D + (size_t)m * H + k;
-    const float* pg = gns + ((size_t)(m / T) * H + k) * 2;
 #pragma unroll
     for (int j = 0; j < EPC; j += 4) {
-      float4 a = ld4(pd + j), w = ld4(gnw + k + j), bb = ld4(gnb + k + j);
-      float4 g0 = ld4(pg + 2 * j), g1 = ld4(pg + 2 * j + 4);
+      float4 a = ld4(pd + j);
       r.v[j] = a.x; r.v[j + 1] = a.y; r.v[j + 2] = a.z; r.v[j + 3] = a.w;
-      r.w[j] = w.x; r.w[j + 1] = w.y; r.w[j + 2] = w.z; r.w[j + 3] = w.w;
-      r.b[j] = bb.x; r.b[j + 1] = bb.y; r.b[j + 2] = bb.z; r.b[j + 3] = bb.w;
-      r.mu[j] = g0.x; r.rs[j] = g0.y; r.mu[j + 1] = g0.z; r.rs[j + 1] = g0.w;
-      r.mu[j + 2] = g1.x; r.rs[j + 2] = g1.y; r.mu[j + 3] = g1.z; r.rs[j + 3] = g1.w;
     }
     return r;
   }
   template <typename Dt>
-  __device__ uint4 finish(const Raw& r, int, int, const float*, int) const {
+  __device__ u32x4 finish_v(const Raw& r, int m, int k, const float*, const float* vec, bool use, int bm) const {
     float o[EPC];
+    if (use) {
+      const int slot = m / T - bm / T;
+      const float* mu = vec + (size_t)(2 * slot) * H + k;
+      const float* sc = vec + (size_t)(2 * slot + 1) * H + k;
+      const float* bb = vec + (size_t)4 * H + k;
 #pragma unroll
-    for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - r.mu[j]) * r.rs[j]) * r.w[j] + r.b[j];
+      for (int j = 0; j < EPC; ++j) o[j] = (r.v[j] - mu[j]) * sc[j] + bb[j];
+    } else {
+      const float* g = gns + ((size_t)(m / T) * H + k) * 2;
+#pragma unroll
+      for (int j = 0; j < EPC; ++j) o[j] = (r.v[j] - g[2 * j]) * (g[2 * j + 1] * gnw[k + j]) + gnb[k + j];
+    }
     return pack_chunk<Dt>(o);
   }
 };
@@ -579,10 +655,10 @@ FLAMED_API int flamed_den_adaln(flamed_den_t h, const float* t_vals, int n_t, co
   hipLaunchKernelGGL(tfreq_kernel, dim3((n_t * 256 + 255) / 256), dim3(256), 0, st, t_vals, n_t, 256, F);
   FL_LAUNCH_CHECK();
   int rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{F, 256}, d->t0w, 256, EpiBiasAct<float, 2>{d->t0b, T1, H}, n_t, H, 256, st))) return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{T1, H}, d->t2w, H, EpiBiasAct<float, 0>{d->t2b, TE, H}, n_t, H, H, st))) return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{spk, d->S}, d->cw, d->S, EpiBiasAct<float, 0>{d->cb, CE, H}, n_spk, H, d->S, st))) return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadAdaY{TE, CE, tidx, sidx, H}, d->adaw, H, EpiBiasAct<float, 0>{d->adab, mods, d->MS}, R, d->MS, H, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadF32<float>{F, 256}, d->t0w, 256, EpiBiasAct<float, 2>{d->t0b, T1, H}, n_t, H, 256, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadF32<float>{T1, H}, d->t2w, H, EpiBiasAct<float, 0>{d->t2b, TE, H}, n_t, H, H, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadF32<float>{spk, d->S}, d->cw, d->S, EpiBiasAct<float, 0>{d->cb, CE, H}, n_spk, H, d->S, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadAdaY{TE, CE, tidx, sidx, H}, d->adaw, H, EpiBiasAct<float, 0>{d->adab, mods, d->MS}, R, d->MS, H, st))) return rc;
   return kOk;
 }
 
@@ -614,16 +690,18 @@ static inline void kt_mark(int c, hipStream_t st) {
 }
 
 // One velocity evaluation (+ Euler update when vout == nullptr).
-template <typename DT, int BM, int BN, int KCH>
+template <typename DT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
                          const DenWs& w, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
+  const GemmCfg cfg = pick_cfg(M);
+  const int BN = cfg_bn(cfg);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { TRY(x); kt_mark(cls, st); } while (0)
-  K_(0, (launch_gemm<BM, BN, KCH, DT>(LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
+  K_(0, (launch_gemm_auto<DT>(cfg, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
@@ -631,14 +709,14 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div};
     K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
     K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
-    K_(3, (launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
+    K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
                                         EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
-    K_(4, (launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+    K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
                                         EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
                                         M, H, H, st)));
-    K_(5, (launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb}, (const DT*)Bw.m0, H,
+    K_(5, (launch_gemm_auto<DT>(cfg, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
                                         EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
-    K_(6, (launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
+    K_(6, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
                                         EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
@@ -647,11 +725,11 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   const DenBlockW& F = d->fin;
   K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
   K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
-  K_(3, (launch_gemm<BM, BN, KCH, DT>(LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
-  K_(4, (launch_gemm<BM, BN, KCH, DT>(LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
+  K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                       EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
                                       M, H, H, st)));
-  K_(7, (launch_gemm<BM, BN, KCH, DT>(LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr}, (const DT*)d->wout, H,
+  K_(7, (launch_gemm_auto<DT>(cfg, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
                                       EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
   {
     size_t n = (size_t)M * C;
@@ -668,14 +746,8 @@ static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, in
                     hipStream_t st) {
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
-  const int M = B * T;
-  const bool big = M >= 4096;
-  if (d->dt == FLAMED_BF16) {
-    return big ? den_step_impl<bf16, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st)
-               : den_step_impl<bf16, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
-  }
-  return big ? den_step_impl<float, 128, 128, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st)
-             : den_step_impl<float, 64, 64, 4>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
+  if (d->dt == FLAMED_BF16) return den_step_impl<bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
+  return den_step_impl<float>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
 }
 
 }  // namespace fl

@@ -80,7 +80,7 @@ struct LoadDurIn {
     r.v[3] = (p.w + w.w * x) + te.w;
     return r;
   }
-  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
 };
 
 // LN2 + Linear(F->1) + masked_fill(mask, 0) + Euler update; one wave per row.
@@ -161,9 +161,9 @@ static int net_prepare(DurNet* n, const float* enc, int M, const float* ts, int 
   hipLaunchKernelGGL(pos_emb_kernel, dim3((nfe * D + 255) / 256), dim3(256), 0, st, ts, nfe, D, F);
   FL_LAUNCH_CHECK();
   int rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{F, D}, n->t1w, D, EpiBiasAct<float, 2>{n->t1b, TH, 4 * D}, nfe, 4 * D, D, st))) return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{TH, 4 * D}, n->t2w, 4 * D, EpiBiasAct<float, 0>{n->t2b, TEMB, D}, nfe, D, 4 * D, st))) return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadF32<float>{enc, D}, n->we, D, EpiBiasAct<float, 0>{n->pb, P, D}, M, D, D, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadF32<float>{F, D}, n->t1w, D, EpiBiasAct<float, 2>{n->t1b, TH, 4 * D}, nfe, 4 * D, D, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadF32<float>{TH, 4 * D}, n->t2w, 4 * D, EpiBiasAct<float, 0>{n->t2b, TEMB, D}, nfe, D, 4 * D, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadF32<float>{enc, D}, n->we, D, EpiBiasAct<float, 0>{n->pb, P, D}, M, D, D, st))) return rc;
   return kOk;
 }
 
@@ -172,10 +172,10 @@ static int net_step(DurNet* n, const float* P, const float* temb, float* xt, con
   const int M = B * L, D = n->D, F = n->F;
   const int NT = F / 64;
   int rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadDurIn{P, n->w0, xt, temb, D, L}, n->c1w, 3 * D,
+  if ((rc = launch_gemm_auto<float>(pick_cfg(M) == kCfgSmall ? kCfgSmall : kCfgMid, LoadDurIn{P, n->w0, xt, temb, D, L}, n->c1w, 3 * D,
                                           EpiBiasStatsT<true>{n->c1b, w.R1, F, w.S1, NT}, M, F, 3 * D, st)))
     return rc;
-  if ((rc = launch_gemm<64, 64, 4, float>(LoadConvRows<float, true>{w.R1, F, L, 3, 1, w.S1, NT, 64, 1e-5f, n->g1, n->b1}, n->c2w,
+  if ((rc = launch_gemm<float>(LoadConvRows<float, true>{w.R1, F, L, 3, 1, w.S1, NT, 64, 1e-5f, n->g1, n->b1}, n->c2w,
                                           3 * F, EpiBiasAct<float, 3>{n->c2b, w.R2, F}, M, F, 3 * F, st)))
     return rc;
   hipLaunchKernelGGL(dur_head_kernel<384>, dim3((M + 3) / 4), dim3(256), 0, st, w.R2, n->g2, n->b2, n->lw, n->lb, mask, xt, M, dt);

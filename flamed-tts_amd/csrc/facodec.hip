@@ -188,17 +188,17 @@ struct LoadConvT {
   const DT* __restrict__ x;
   int Cin;
   int n;
-  struct Raw { uint4 v; };
+  struct Raw { u32x4 v; };
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
   __device__ Raw issue(int m, int k) const {
     int b = m / (n + 1), q = m - b * (n + 1);
     int tap = k / Cin, c = k - tap * Cin;
     int i = q - tap;
-    if (i < 0 || i >= n) return Raw{make_uint4(0u, 0u, 0u, 0u)};
-    return Raw{*reinterpret_cast<const uint4*>(x + ((size_t)b * n + i) * Cin + c)};
+    if (i < 0 || i >= n) return Raw{u32x4{0u, 0u, 0u, 0u}};
+    return Raw{*reinterpret_cast<const u32x4*>(x + ((size_t)b * n + i) * Cin + c)};
   }
-  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
 };
 
 struct EpiConvTStore {
@@ -231,9 +231,7 @@ struct EpiResAdd {  // X += acc + bias  (ResidualUnit skip, facodec.py:132-133)
 
 template <typename DT, class AL, class EP>
 static int gemm_auto(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
-  if (M >= 4096 && N % 128 == 0) return launch_gemm<128, 128, 4, DT>(al, W, ldw, ep, M, N, K, st);
-  if (M >= 4096) return launch_gemm<128, 64, 4, DT>(al, W, ldw, ep, M, N, K, st);
-  return launch_gemm<64, 64, 4, DT>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm<DT>(al, W, ldw, ep, M, N, K, st);
 }
 
 // ------------------------------ handle ------------------------------
@@ -296,7 +294,7 @@ static int fac_decode_impl(Fac* f, const float* lat, const float* spk, int B, in
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
   const int C0 = f->C0;
   DT* A = reinterpret_cast<DT*>(w.A);
-  TRY((launch_gemm<64, 64, 4, float>(LoadF32<float>{spk, C0}, f->tlw, C0, EpiBiasAct<float, 0>{f->tlb, w.style, 2 * C0}, B, 2 * C0, C0, st)));
+  TRY((launch_gemm<float>(LoadF32<float>{spk, C0}, f->tlw, C0, EpiBiasAct<float, 0>{f->tlb, w.style, 2 * C0}, B, 2 * C0, C0, st)));
   hipLaunchKernelGGL(fac_prep_kernel, dim3((T + 31) / 32, B), dim3(256), (size_t)C0 * 33 * 4, st, lat, w.style, C0, T, w.h0);
   FL_LAUNCH_CHECK();
   TRY((gemm_auto<DT>(LoadConvRows<DT, false>{w.h0, C0, T, 7, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, (const DT*)f->win, 7 * C0,

@@ -10,20 +10,32 @@
 //          MFMA j consumes element j — a permutation of the K order applied identically to A and W,
 //          so the result is an exact fp32 FMA chain (parity mode).
 #pragma once
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace fl {
 
 constexpr int kGemmThreads = 256;
 
-template <int BM, int BN, int KCH, class AL, class EP>
+// Optional per-column vector caches in LDS: a loader with kVec > 0 stages kVec floats per K column
+// (e.g. two modulation rows x (alpha, beta)) in its prologue; an epilogue with kEVec > 0 stages
+// kEVec floats per output column of its tile.  Detected by these traits (0 when absent).
+template <class T, class = void> struct kvec_of { static constexpr int value = 0; };
+template <class T> struct kvec_of<T, std::void_t<decltype(T::kVec)>> { static constexpr int value = T::kVec; };
+template <class T, class = void> struct kevec_of { static constexpr int value = 0; };
+template <class T> struct kevec_of<T, std::void_t<decltype(T::kEVec)>> { static constexpr int value = T::kEVec; };
+
+template <int BM, int BN, int KCH, int NSTAGE, class AL, class EP>
 struct GemmSmem {
-  static constexpr int ROWB = KCH * 16 + 16;
-  static constexpr int tiles = 2 * (BM + BN) * ROWB;
+  static constexpr int ROWB = KCH * 16;  // unpadded; 16-B chunks XOR-swizzled by row
+  static constexpr int tiles = NSTAGE * (BM + BN) * ROWB;
   static constexpr int a_stats = AL::stat_rows(BM) * 2 * 4;
   static constexpr int e_stats = EP::stat_rows(BM) * 2 * 4;
+  static constexpr int e_vec = kevec_of<EP>::value * BN * 4;
   static constexpr int red = BM * 2 * 4;
-  static constexpr int bytes = ((tiles > red ? tiles : red) + a_stats + e_stats + 15) / 16 * 16;
+  static constexpr int base = tiles > red ? tiles : red;
+  static constexpr int bytes = (base + a_stats + e_stats + e_vec + 15) / 16 * 16;  // + kVec*K*4 (runtime)
 };
 
 // LayerNorm row statistics from producer partials: S[m][NT] = (tile mean, tile M2) over `tw` columns.
@@ -43,27 +55,37 @@ __device__ __forceinline__ void row_stats_from_partials(const float* __restrict_
   rstd = 1.0f / sqrtf(var + eps);
 }
 
-template <int BM, int BN, int KCH, typename DT, class AL, class EP>
+// Byte offset of 16-B chunk `c` of LDS tile row `r`: rows of KCH chunks, chunk index XOR (r & 7).
+// For KCH = 8 the ds_read_b128 fragment pattern (lane&15 -> row, lane>>4 -> chunk) is conflict-free.
+template <int KCH>
+__device__ __forceinline__ int lds_off(int r, int c) {
+  return r * (KCH * 16) + ((c ^ (r & (KCH - 1) & 7)) << 4);
+}
+
+// NSTAGE = 2: LDS double buffer, loads issued one K-step ahead.
+// NSTAGE = 3: LDS ring of 3, two register stages, loads issued two K-steps ahead (small-M latency).
+template <int BM, int BN, int KCH, int NSTAGE, typename DT, class AL, class EP>
 __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __restrict__ W, int ldw, EP ep,
                                                              int M, int N, int K) {
-  using SM = GemmSmem<BM, BN, KCH, AL, EP>;
+  using SM = GemmSmem<BM, BN, KCH, NSTAGE, AL, EP>;
   constexpr int EPC = DTraits<DT>::EPC;
-  constexpr int ROWB = SM::ROWB;
   constexpr int BKE = KCH * EPC;
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int ACH = BM * KCH / kGemmThreads;
   constexpr int BCH = BN * KCH / kGemmThreads;
+  constexpr int TILE = (BM + BN) * SM::ROWB;
   static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
-  static_assert(KCH % 4 == 0, "KCH must be a multiple of 4 (64 B)");
+  static_assert(KCH == 8, "K-step is 128 B per row");
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "2 or 3 stages");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* tileA0 = smem;
-  char* tileA1 = smem + BM * ROWB;
-  char* tileB0 = smem + 2 * BM * ROWB;
-  char* tileB1 = tileB0 + BN * ROWB;
-  float* a_stats = reinterpret_cast<float*>(smem + (SM::tiles > SM::red ? SM::tiles : SM::red));
+  float* a_stats = reinterpret_cast<float*>(smem + SM::base);
   float* e_stats = a_stats + AL::stat_rows(BM) * 2;
+  float* e_vec = e_stats + EP::stat_rows(BM) * 2;
+  float* a_vec = e_vec + kevec_of<EP>::value * BN;
+  constexpr bool AV = kvec_of<AL>::value > 0;
+  constexpr bool EV = kevec_of<EP>::value > 0;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -72,44 +94,52 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
   const int bn = blockIdx.x * BN;
   const int bm = blockIdx.y * BM;
 
-  al.prologue(bm, BM, M, a_stats);
-  ep.prologue(bm, BM, M, e_stats);
+  bool a_uv = false, e_uv = false;
+  if constexpr (AV) a_uv = al.prologue_v(bm, BM, M, K, a_stats, a_vec);
+  else al.prologue(bm, BM, M, a_stats);
+  if constexpr (EV) e_uv = ep.prologue_v(bm, bn, BM, BN, M, e_stats, e_vec);
+  else ep.prologue(bm, BM, M, e_stats);
   __syncthreads();
 
-  typename AL::Raw ra[ACH];
-  uint4 rb[BCH];
+  typename AL::Raw ra0[ACH], ra1[ACH];
+  u32x4 rb0[BCH], rb1[BCH];
   const int nsteps = K / BKE;
 
-  auto issue = [&](int s) {
+  auto issue = [&](int s, typename AL::Raw (&ra)[ACH], u32x4 (&rb)[BCH]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < ACH; ++j) {
       int c = tid + j * kGemmThreads;
       int r = c / KCH, kc = c % KCH;
       int m = bm + r;
       m = m < M ? m : M - 1;
-      ra[j] = al.issue(m, s * BKE + kc * EPC);
+      if constexpr (AV) ra[j] = al.issue_v(m, s * BKE + kc * EPC, a_uv);
+      else ra[j] = al.issue(m, s * BKE + kc * EPC);
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
       int c = tid + j * kGemmThreads;
       int r = c / KCH, kc = c % KCH;
-      rb[j] = *reinterpret_cast<const uint4*>(W + (size_t)(bn + r) * ldw + s * BKE + kc * EPC);
+      rb[j] = *reinterpret_cast<const u32x4*>(W + (size_t)(bn + r) * ldw + s * BKE + kc * EPC);
     }
   };
-  auto commit = [&](int s, char* tA, char* tB) {
+  auto commit = [&](int s, const typename AL::Raw (&ra)[ACH], const u32x4 (&rb)[BCH], char* t) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < ACH; ++j) {
       int c = tid + j * kGemmThreads;
       int r = c / KCH, kc = c % KCH;
       int m = bm + r;
       m = m < M ? m : M - 1;
-      *reinterpret_cast<uint4*>(tA + r * ROWB + kc * 16) = al.template finish<DT>(ra[j], m, s * BKE + kc * EPC, a_stats, bm);
+      if constexpr (AV)
+        *reinterpret_cast<u32x4*>(t + lds_off<KCH>(r, kc)) = al.template finish_v<DT>(ra[j], m, s * BKE + kc * EPC, a_stats, a_vec, a_uv, bm);
+      else
+        *reinterpret_cast<u32x4*>(t + lds_off<KCH>(r, kc)) = al.template finish<DT>(ra[j], m, s * BKE + kc * EPC, a_stats, bm);
     }
+    char* tb = t + BM * SM::ROWB;
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
       int c = tid + j * kGemmThreads;
       int r = c / KCH, kc = c % KCH;
-      *reinterpret_cast<uint4*>(tB + r * ROWB + kc * 16) = rb[j];
+      *reinterpret_cast<u32x4*>(tb + lds_off<KCH>(r, kc)) = rb[j];
     }
   };
 
@@ -119,32 +149,23 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0);
-  commit(0, tileA0, tileB0);
-  __syncthreads();
-
   const int fr = lane & 15, fq = lane >> 4;
-  for (int s = 0; s < nsteps; ++s) {
-    const bool cur1 = (s & 1);
-    char* tA = cur1 ? tileA1 : tileA0;
-    char* tB = cur1 ? tileB1 : tileB0;
-    if (s + 1 < nsteps) issue(s + 1);
+  auto compute = [&](const char* t) __attribute__((always_inline)) {
+    const char* tb = t + BM * SM::ROWB;
 #pragma unroll
     for (int kk = 0; kk < KCH / 4; ++kk) {
-      uint4 a[FM], b[FN];
+      u32x4 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        a[i] = *reinterpret_cast<const uint4*>(tA + (wr * WTM + i * 16 + fr) * ROWB + (kk * 4 + fq) * 16);
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const u32x4*>(t + lds_off<KCH>(wr * WTM + i * 16 + fr, kk * 4 + fq));
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        b[j] = *reinterpret_cast<const uint4*>(tB + (wc * WTN + j * 16 + fr) * ROWB + (kk * 4 + fq) * 16);
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const u32x4*>(tb + lds_off<KCH>(wc * WTN + j * 16 + fr, kk * 4 + fq));
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           if constexpr (DTraits<DT>::kCode == 1) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&a[i]),
-                                                                *reinterpret_cast<bf16x8*>(&b[j]), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]),
+                                                                __builtin_bit_cast(bf16x8, b[j]), acc[i][j], 0, 0, 0);
           } else {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].x), __uint_as_float(b[j].x), acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[i].y), __uint_as_float(b[j].y), acc[i][j], 0, 0, 0);
@@ -153,12 +174,52 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
           }
         }
     }
-    if (s + 1 < nsteps) commit(s + 1, cur1 ? tileA0 : tileA1, cur1 ? tileB0 : tileB1);
+  };
+
+  if constexpr (NSTAGE == 2) {
+    issue(0, ra0, rb0);
+    commit(0, ra0, rb0, smem);
     __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      char* cur = smem + (s & 1) * TILE;
+      char* nxt = smem + ((s + 1) & 1) * TILE;
+      issue(s + 1 < nsteps ? s + 1 : s, ra0, rb0);  // unconditional (clamped) keeps the staging in VGPRs
+      compute(cur);
+      if (s + 1 < nsteps) commit(s + 1, ra0, rb0, nxt);
+      __syncthreads();
+    }
+  } else {
+    // invariant at iteration s: LDS holds steps s, s+1; register set (s&1) holds loads of step s+2
+    const int last = nsteps - 1;
+    issue(0, ra0, rb0);
+    issue(last < 1 ? last : 1, ra1, rb1);
+    commit(0, ra0, rb0, smem);
+    if (nsteps > 1) commit(1, ra1, rb1, smem + TILE);
+    issue(last < 2 ? last : 2, ra0, rb0);
+    __syncthreads();
+    int b0 = 0;  // LDS slot of step s
+    for (int s = 0; s < nsteps; s += 2) {
+      {  // even step: issue s+3 into set 1, commit set 0 (step s+2)
+        int b2 = b0 + 2 >= 3 ? b0 - 1 : b0 + 2;
+        issue(s + 3 < nsteps ? s + 3 : last, ra1, rb1);
+        compute(smem + b0 * TILE);
+        if (s + 2 < nsteps) commit(s + 2, ra0, rb0, smem + b2 * TILE);
+        __syncthreads();
+        b0 = b0 == 2 ? 0 : b0 + 1;
+      }
+      if (s + 1 < nsteps) {  // odd step: issue s+4 into set 0, commit set 1 (step s+3)
+        int b2 = b0 + 2 >= 3 ? b0 - 1 : b0 + 2;
+        issue(s + 4 < nsteps ? s + 4 : last, ra0, rb0);
+        compute(smem + b0 * TILE);
+        if (s + 3 < nsteps) commit(s + 3, ra1, rb1, smem + b2 * TILE);
+        __syncthreads();
+        b0 = b0 == 2 ? 0 : b0 + 1;
+      }
+    }
   }
 
-  // ---------------- epilogue ----------------
-  float val[FM][FN][4];
+  // ---------------- epilogue (values overwrite the accumulators in place) ----------------
+  auto& val = acc;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -168,7 +229,8 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
         int m = bm + wr * WTM + i * 16 + fq * 4 + r;
         int n = bn + wc * WTN + j * 16 + fr;
         int mc = m < M ? m : M - 1;
-        val[i][j][r] = ep.value(mc, n, acc[i][j][r], e_stats, bm);
+        if constexpr (EV) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn);
+        else val[i][j][r] = ep.value(mc, n, acc[i][j][r], e_stats, bm);
       }
 
   if constexpr (EP::kRowStats) {
@@ -238,11 +300,11 @@ template <typename DT>
 struct LoadPlain {
   const DT* __restrict__ p;
   int ld;
-  struct Raw { uint4 v; };
+  struct Raw { u32x4 v; };
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
-  __device__ Raw issue(int m, int k) const { return Raw{*reinterpret_cast<const uint4*>(p + (size_t)m * ld + k)}; }
-  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
+  __device__ Raw issue(int m, int k) const { return Raw{*reinterpret_cast<const u32x4*>(p + (size_t)m * ld + k)}; }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
 };
 
 // A = fp32 matrix converted to DT on the fly.
@@ -263,7 +325,7 @@ struct LoadF32 {
     }
     return r;
   }
-  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return pack_chunk<D>(r.v); }
 };
 
 // ------------------------------ generic epilogues ------------------------------
@@ -359,7 +421,7 @@ struct LoadConvRows {
     return r;
   }
   template <typename D>
-  __device__ uint4 finish(const Raw& r, int, int, const float* st, int bm) const {
+  __device__ u32x4 finish(const Raw& r, int, int, const float* st, int bm) const {
     float o[EPC];
     if (r.src < 0) {
 #pragma unroll
@@ -385,37 +447,64 @@ struct LoadConvPlain {
   int L;
   int KT;
   int dil;
-  struct Raw { uint4 v; };
+  struct Raw { u32x4 v; };
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
   __device__ Raw issue(int m, int k) const {
     int tap = k / Cin, c = k - tap * Cin;
     int off = (tap - KT / 2) * dil;
     int l = m % L + off;
-    if (l < 0 || l >= L) return Raw{make_uint4(0u, 0u, 0u, 0u)};
-    return Raw{*reinterpret_cast<const uint4*>(x + (size_t)(m + off) * Cin + c)};
+    if (l < 0 || l >= L) return Raw{u32x4{0u, 0u, 0u, 0u}};
+    return Raw{*reinterpret_cast<const u32x4*>(x + (size_t)(m + off) * Cin + c)};
   }
-  template <typename D> __device__ uint4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
 };
 
-// Host-side launcher.
-template <int BM, int BN, int KCH, typename DT, class AL, class EP>
-inline int launch_gemm(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+// Host-side launcher.  Tile configurations (BM, BN, NSTAGE) are selected by the callers:
+//   small M  : 32 x 64, 3-stage ring (latency-bound at ~400 rows: more workgroups, deeper prefetch)
+//   mid M    : 64 x 64, 3-stage
+//   large M  : 128 x 128 (or 128 x 64 for narrow N), 2-stage (MFMA-bound)
+template <int BM, int BN, int NSTAGE, typename DT, class AL, class EP>
+inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  constexpr int KCH = 8;
   constexpr int BKE = KCH * DTraits<DT>::EPC;
   FL_REQUIRE(M > 0 && N % BN == 0 && K % BKE == 0, "gemm: unsupported shape M=%d N=%d K=%d (BN=%d BK=%d)", M, N, K, BN, BKE);
-  using SM = GemmSmem<BM, BN, KCH, AL, EP>;
+  using SM = GemmSmem<BM, BN, KCH, NSTAGE, AL, EP>;
   dim3 grid(N / BN, (M + BM - 1) / BM);
-  auto kern = gemm_kernel<BM, BN, KCH, DT, AL, EP>;
-  if (SM::bytes > 64 * 1024) {
+  auto kern = gemm_kernel<BM, BN, KCH, NSTAGE, DT, AL, EP>;
+  const size_t bytes = SM::bytes + (size_t)kvec_of<AL>::value * K * 4;
+  FL_REQUIRE(bytes <= 160 * 1024, "gemm: LDS request %zu B too large (K=%d)", bytes, K);
+  if (bytes > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, SM::bytes));
+      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL(kern, grid, dim3(kGemmThreads), SM::bytes, st, al, W, ldw, ep, M, N, K);
+  hipLaunchKernelGGL(kern, grid, dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K);
   FL_LAUNCH_CHECK();
   return kOk;
+}
+
+// Tile selection by shape.  `BNf` fixes the N tile when the epilogue's row partials need a known
+// width (0 = free choice).
+enum GemmCfg { kCfgSmall = 0, kCfgMid = 1, kCfgLarge = 2 };
+inline GemmCfg pick_cfg(int M) { return M < 2048 ? kCfgSmall : (M < 8192 ? kCfgMid : kCfgLarge); }
+inline int cfg_bn(GemmCfg c) { return c == kCfgLarge ? 128 : 64; }
+
+template <typename DT, class AL, class EP>
+inline int launch_gemm_auto(GemmCfg c, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  if (c == kCfgSmall) return launch_gemm_cfg<32, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  if (c == kCfgMid) return launch_gemm_cfg<64, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  if (N % 128 == 0) return launch_gemm_cfg<128, 128, 2, DT>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm_cfg<128, 64, 2, DT>(al, W, ldw, ep, M, N, K, st);
+}
+
+// Shape-driven convenience: choose the config from M (row partial width = cfg_bn(pick_cfg(M)) when
+// N allows 128-wide tiles).
+template <typename DT, class AL, class EP>
+inline int launch_gemm(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  return launch_gemm_auto<DT>(pick_cfg(M), al, W, ldw, ep, M, N, K, st);
 }
 
 }  // namespace fl
