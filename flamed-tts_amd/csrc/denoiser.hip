@@ -247,9 +247,19 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   __shared__ float hs[SR * kDwCG];
   __shared__ float rs[SR * 2];
   __shared__ float red[RG * kDwCG * 3];
+  __shared__ float va[kDwCG], vb[kDwCG];
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * kDwCG, ts = blockIdx.y, b = blockIdx.z;
   const int t0 = ts * kDwTC;
+  // one modulation row for the whole utterance (sampling path): stage alpha/beta once
+  const bool uni = ((size_t)b * T) / mod.div == ((size_t)b * T + T - 1) / mod.div;
+  if (uni && tid < kDwCG) {
+    size_t mo = (((size_t)b * T) / mod.div) * mod.ms + c0 + tid;
+    float sc1 = 1.0f + mod.sc[mo];
+    float w = AFF ? lnw[c0 + tid] : 1.0f, bb = AFF ? lnb[c0 + tid] : 0.0f;
+    va[tid] = w * sc1;
+    vb[tid] = bb * sc1 + mod.sh[mo];
+  }
   if (tid < SR) {
     int t = t0 - HALO + tid;
     if (t >= 0 && t < T) row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rs[2 * tid], rs[2 * tid + 1]);
@@ -262,9 +272,14 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
     if (t >= 0 && t < T) {
       size_t m = (size_t)b * T + t;
       float xh = (X[m * H + c0 + cc] - rs[2 * r]) * rs[2 * r + 1];
-      if constexpr (AFF) xh = xh * lnw[c0 + cc] + lnb[c0 + cc];
-      size_t mo = (m / mod.div) * mod.ms + c0 + cc;
-      v = xh * (1.0f + mod.sc[mo]) + mod.sh[mo];
+      if (uni) {
+        v = xh * va[cc] + vb[cc];
+      } else {
+        size_t mo = (m / mod.div) * mod.ms + c0 + cc;
+        float sc1 = 1.0f + mod.sc[mo];
+        float w = AFF ? lnw[c0 + cc] : 1.0f, bb = AFF ? lnb[c0 + cc] : 0.0f;
+        v = xh * (w * sc1) + (bb * sc1 + mod.sh[mo]);
+      }
     }
     hs[idx] = v;
   }
@@ -318,9 +333,16 @@ __global__ void gn_finalize_kernel(const float* __restrict__ GP, float* __restri
   int b = blockIdx.y;
   if (c >= H) return;
   float n = 0.f, mu = 0.f, m2 = 0.f;
-  for (int ts = 0; ts < TS; ++ts) {
-    const float* p = GP + (((size_t)b * TS + ts) * H + c) * 3;
-    chan_combine(n, mu, m2, p[0], p[1], p[2]);
+  for (int t0 = 0; t0 < TS; t0 += 8) {  // batches of 8 chunk partials loaded together
+    float q[8][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float* p = GP + (((size_t)b * TS + (t0 + i < TS ? t0 + i : TS - 1)) * H + c) * 3;
+      q[i][0] = p[0]; q[i][1] = p[1]; q[i][2] = p[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (t0 + i < TS) chan_combine(n, mu, m2, q[i][0], q[i][1], q[i][2]);
   }
   GNS[((size_t)b * H + c) * 2] = mu;
   GNS[((size_t)b * H + c) * 2 + 1] = 1.0f / sqrtf(m2 / (float)T + eps);
@@ -523,7 +545,8 @@ extern "C" {
 
 FLAMED_API int flamed_den_create(int C, int H, int n_blocks, int kernel, int spk_dim, int dtype, flamed_den_t* out) {
   FL_REQUIRE(out, "flamed_den_create: null out");
-  FL_REQUIRE(C > 0 && C % 32 == 0 && H % 128 == 0 && n_blocks >= 1 && spk_dim % 32 == 0, "flamed_den_create: unsupported dims C=%d H=%d S=%d", C, H, spk_dim);
+  FL_REQUIRE(C > 0 && C % 64 == 0 && H % 256 == 0 && H <= 1024 && n_blocks >= 1 && spk_dim % 64 == 0,
+             "flamed_den_create: unsupported dims C=%d H=%d S=%d", C, H, spk_dim);
   FL_REQUIRE(kernel == 31, "flamed_den_create: only convnext kernel_size=31 is specialised (got %d)", kernel);
   FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16, "flamed_den_create: dtype must be FLAMED_F32 or FLAMED_BF16");
   Den* d = new Den();

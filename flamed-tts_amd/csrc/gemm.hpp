@@ -42,14 +42,21 @@ struct GemmSmem {
 __device__ __forceinline__ void row_stats_from_partials(const float* __restrict__ S, int m, int NT, int tw,
                                                         float eps, float& mean, float& rstd) {
   const float2* p = reinterpret_cast<const float2*>(S) + (size_t)m * NT;
+  // NT <= 16 partials: load them all before reducing (independent loads in flight together)
+  float2 q[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) q[i] = i < NT ? p[i] : make_float2(0.f, 0.f);
   float s = 0.f;
-  for (int i = 0; i < NT; ++i) s += p[i].x;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += q[i].x;
   mean = s / (float)NT;
   float m2 = 0.f;
-  for (int i = 0; i < NT; ++i) {
-    float2 q = p[i];
-    float d = q.x - mean;
-    m2 += q.y + (float)tw * d * d;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i < NT) {
+      float d = q[i].x - mean;
+      m2 += q[i].y + (float)tw * d * d;
+    }
   }
   float var = m2 / (float)(NT * tw);
   rstd = 1.0f / sqrtf(var + eps);
@@ -463,7 +470,8 @@ struct LoadConvPlain {
 // Host-side launcher.  Tile configurations (BM, BN, NSTAGE) are selected by the callers:
 //   small M  : 32 x 64, 3-stage ring (latency-bound at ~400 rows: more workgroups, deeper prefetch)
 //   mid M    : 64 x 64, 3-stage
-//   large M  : 128 x 128 (or 128 x 64 for narrow N), 2-stage (MFMA-bound)
+//   large M  : 128 x 128 (or 128 x 64 for narrow N), 3-stage (MFMA-bound; 1 wave/SIMD needs the
+//              2-step prefetch to cover load latency)
 template <int BM, int BN, int NSTAGE, typename DT, class AL, class EP>
 inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   constexpr int KCH = 8;
@@ -496,8 +504,8 @@ template <typename DT, class AL, class EP>
 inline int launch_gemm_auto(GemmCfg c, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   if (c == kCfgSmall) return launch_gemm_cfg<32, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
   if (c == kCfgMid) return launch_gemm_cfg<64, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
-  if (N % 128 == 0) return launch_gemm_cfg<128, 128, 2, DT>(al, W, ldw, ep, M, N, K, st);
-  return launch_gemm_cfg<128, 64, 2, DT>(al, W, ldw, ep, M, N, K, st);
+  if (N % 128 == 0) return launch_gemm_cfg<128, 128, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm_cfg<128, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
 }
 
 // Shape-driven convenience: choose the config from M (row partial width = cfg_bn(pick_cfg(M)) when
