@@ -1,0 +1,195 @@
+"""Flamed — top-level model (drop-in for reference flamed/models/flamed.py).
+
+`sample_batch` (reference :168-217) orchestrates prior -> prob -> decode exactly as the reference:
+PriorGenerator.sample (torch transformer + HIP PVA flow / length regulator), ProbGenerator.sample
+(HIP AdaLN precompute + graph-captured Euler solve), FACodecDecoder.inference (HIP decoder); `time`
+is recorded before the decode, as the reference does (:211 vs :214-215).  The returned dict has the
+reference's keys.  `sample` (:89-166) keeps its argument contract and errors.
+
+Offline differences (documented, SURVEY.md §7 hard part 6): the LibriSpeech lexicon and g2p_en are
+absent, so `_preprocess_english` uses a rule-based G2P fallback when the lexicon file is missing;
+raw-audio prompts need the FaCodec prompt encoder (§8(f) f3, not in this round) — pass
+`prompt_processed` + `timbre` instead.
+"""
+from __future__ import annotations
+
+import os
+import re
+import time
+from string import punctuation
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from flamed.text import text_to_sequence
+from flamed.models.synthesizer.prior_generator import PriorGenerator
+from flamed.models.synthesizer.prob_generator import ProbGenerator
+
+
+class Flamed(nn.Module):
+
+    @classmethod
+    def from_pretrained(cls, cfg, ckpt_path, device, weights_only=False, training_mode=False):
+        """reference :24-39.  Checkpoints are always read with torch.load(weights_only=True) (no pickle
+        execution); a Lightning checkpoint's 'state_dict' entry is used when weights_only is False."""
+        cfg["prob_generator"]["device"] = str(device)
+        cfg["prior_generator"]["device"] = str(device)
+        model = cls(cfg)
+        model.lexicon = model.read_lexicon()
+        model.g2p = _make_g2p()
+        ckpt = torch.load(ckpt_path, map_location=device, weights_only=True)
+        model.load_state_dict(ckpt if weights_only else ckpt["state_dict"])
+        del ckpt
+        if not training_mode:
+            model.eval()
+        return model.to(device)
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        self.prior_generator = PriorGenerator(cfg["prior_generator"])
+        self.prob_generator = ProbGenerator(cfg["prob_generator"])
+        self.lexicon = {}
+        self.g2p = None
+
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
+    def forward(self, phonemes, x_len, codes, y_len, phone_durations, sil_durations, embs, prompts, spks):
+        """Training losses (reference :48-87); runs on torch ops under autograd."""
+        prior_embs, tgt_masks, ar_losses = self.prior_generator.compute_loss(
+            texts=phonemes, src_lens=x_len, max_src_len=phonemes.size(-1), codes=codes, tgt_lens=y_len,
+            max_tgt_len=codes.size(-1), phone_durations=phone_durations, sil_durations=sil_durations,
+            prompts=prompts, prompts_len=prompts.size(-1))
+        prob_losses = self.prob_generator.compute_loss(x1=embs, cond=prior_embs, spk=spks, mask=~tgt_masks.unsqueeze(-1))
+        return ar_losses | prob_losses
+
+    @torch.inference_mode()
+    def sample(self, text: str = None, phonemes: torch.Tensor = None, prompt_raw=None, prompt_processed=None,
+               timbre: torch.Tensor = None, sr: int = 16000, codec_cfg=None, codec_encoder=None, codec_decoder=None,
+               temp_durgen: float = 0.3, temp_denoiser: float = 0.3, nsteps_durgen: int = 64,
+               nsteps_denoiser: int = 64, lexicon_path: str = None, cleaners=("english_cleaners",)):
+        """reference :89-166 (same argument validation and ValueErrors)."""
+        if codec_decoder is None or (codec_encoder is None and prompt_raw is not None):
+            if codec_cfg is None:
+                raise ValueError("The codec_encoder or codec_decoder is set to None. To initialize the codec encoder or "
+                                 "decoder, you need to provide a codec_cfg of type omegaconf.DictConfig.")
+            codec_encoder, codec_decoder = self._get_codec_models(codec_cfg)
+        text_provided = text is not None and phonemes is None
+        phonemes_provided = text is None and phonemes is not None
+        if not (text_provided or phonemes_provided):
+            raise ValueError("`text` and `phonemes` are mutually exclusive—only one should be provided, and the "
+                             "other must be None!")
+        raw_provided = prompt_raw is not None and prompt_processed is None
+        processed_provided = prompt_raw is None and prompt_processed is not None
+        if not (raw_provided or processed_provided):
+            raise ValueError("`prompt_raw` and `prompt_processed` are mutually exclusive—only one should be "
+                             "provided, and the other must be None!")
+        start = time.time()
+        if text_provided:
+            phonemes, _, _ = self._preprocess_english(text, lexicon_path, list(cleaners))
+        else:
+            phonemes = phonemes.unsqueeze(0).to(self.device)
+        if raw_provided:
+            acoustic_prompt = self._preprocess_acoustic_prompt(prompt_raw, sr)
+            enc_out = codec_encoder(acoustic_prompt)
+            _, prompts, _, _, timbre = codec_decoder(enc_out, eval_vq=False, vq=True)
+            prompts = prompts.permute(1, 0, 2)
+        else:
+            if timbre is None:
+                raise ValueError("`timbre` must be provided along with `prompt_processed`!")
+            timbre = timbre.unsqueeze(0).to(self.device)
+            prompts = prompt_processed.unsqueeze(0).to(self.device)
+        out = self.sample_batch(phonemes=phonemes,
+                                src_lens=torch.full((phonemes.size(0),), phonemes.size(-1), dtype=torch.long,
+                                                    device=self.device),
+                                prompts=prompts, timbres=timbre, codec_decoder=codec_decoder, temp_durgen=temp_durgen,
+                                temp_denoiser=temp_denoiser, nsteps_durgen=nsteps_durgen,
+                                nsteps_denoiser=nsteps_denoiser)
+        wav = out["wav"][0][0].detach().cpu().numpy()
+        return {"wav": wav, "time": time.time() - start}
+
+    @torch.inference_mode()
+    def sample_batch(self, phonemes, src_lens, prompts, timbres, codec_decoder=None, temp_durgen: float = 0.3,
+                     temp_denoiser: float = 0.3, nsteps_durgen: int = 64, nsteps_denoiser: int = 64):
+        """reference :168-217"""
+        start = time.time()
+        dev = self.device
+        phonemes, src_lens, prompts, timbres = phonemes.to(dev), src_lens.to(dev), prompts.to(dev), timbres.to(dev)
+        prior_emb_cond, prior_logits, tgt_mask = self.prior_generator.sample(
+            texts=phonemes, src_lens=src_lens, max_src_len=phonemes.size(-1), prompts=prompts,
+            prompts_len=prompts.size(-1), nfe=nsteps_durgen, temperature=temp_durgen)
+        latents = self.prob_generator.sample(cond=prior_emb_cond, spk=timbres, nfe=nsteps_denoiser,
+                                             temperature=temp_denoiser, mask=~tgt_mask.unsqueeze(-1))
+        if latents.is_cuda:
+            torch.cuda.synchronize(latents.device)  # 'time' covers the device work, as the eager reference does
+        outputs = {"prior_embs": prior_emb_cond, "prior_logits": prior_logits, "tgt_mask": tgt_mask,
+                   "latents": latents, "time": time.time() - start}
+        if codec_decoder is not None:
+            outputs["wav"] = codec_decoder.inference(latents, timbres)
+        return outputs
+
+    def _preprocess_acoustic_prompt(self, acoustic_prompt, sr=16000):
+        if isinstance(acoustic_prompt, str):
+            from flamed.utils.audio import load_wav
+            acoustic_prompt = torch.from_numpy(load_wav(acoustic_prompt, sr)).float().unsqueeze(0).unsqueeze(0)
+        elif isinstance(acoustic_prompt, np.ndarray):
+            acoustic_prompt = torch.from_numpy(acoustic_prompt).float().unsqueeze(0).unsqueeze(0)
+        elif not isinstance(acoustic_prompt, torch.Tensor):
+            raise ValueError("Acoustic prompt must be one of [str, np.ndarray, torch.tensor]!")
+        return acoustic_prompt.to(self.device)
+
+    def _get_codec_models(self, codec_cfg):
+        from flamed.models.facodec import FACodecDecoder
+        try:
+            from flamed.models.facodec import FACodecEncoder
+        except ImportError:
+            FACodecEncoder = None
+        enc = FACodecEncoder.from_pretrained(codec_cfg["encoder"]).eval() if FACodecEncoder else None
+        dec = FACodecDecoder.from_pretrained(codec_cfg["decoder"]).eval()
+        return enc, dec
+
+    def read_lexicon(self, lexicon_path=None):
+        """reference :238-249; an absent lexicon file yields an empty lexicon (offline snapshot)."""
+        if not lexicon_path:
+            lexicon_path = os.path.join(os.path.dirname(__file__), "..", "lexicon", "librispeech-lexicon.txt")
+        lexicon = {}
+        if not os.path.exists(lexicon_path):
+            return lexicon
+        with open(lexicon_path) as f:
+            for line in f:
+                parts = re.split(r"\s+", line.strip("\n"))
+                if parts[0].lower() not in lexicon:
+                    lexicon[parts[0].lower()] = parts[1:]
+        return lexicon
+
+    def _preprocess_english(self, text, lexicon_path=None, cleaners=("english_cleaners",)):
+        """reference :251-270"""
+        if lexicon_path:
+            self.lexicon = self.read_lexicon(lexicon_path)
+        if self.g2p is None:
+            self.g2p = _make_g2p()
+        text = text.rstrip(punctuation)
+        phones = []
+        for w in re.split(r"([,;.\-\?\!\s+])", text):
+            if w.lower() in self.lexicon:
+                phones += self.lexicon[w.lower()]
+            else:
+                phones += list(filter(lambda p: p != " ", self.g2p(w)))
+        phones = "{sp " + " ".join(phones) + "}"
+        phones = re.sub(r"\{[^\w\s]?\}", "{sp}", phones)
+        phones = phones.replace("}{", " ")
+        seq = np.array(text_to_sequence(phones, list(cleaners) if not isinstance(cleaners, str) else [cleaners]))
+        return torch.from_numpy(seq).unsqueeze(0).to(self.device), text, phones
+
+
+def _make_g2p():
+    try:
+        from g2p_en import G2p  # pragma: no cover - not installable offline
+        return G2p()
+    except Exception:
+        from flamed.text.g2p_fallback import G2pFallback
+        return G2pFallback()

@@ -1,0 +1,71 @@
+"""Offline text cleaners (reference flamed/text/cleaners.py).  `unidecode` and `inflect` are not
+available offline: ASCII folding uses unicodedata and numbers are spelled by a small built-in
+speller (integers and decimals), which covers the English cleaner pipeline used at inference."""
+import re
+import unicodedata
+
+_whitespace_re = re.compile(r"\s+")
+_abbreviations = [(re.compile(r"\b%s\." % a, re.IGNORECASE), b) for a, b in [
+    ("mrs", "misess"), ("mr", "mister"), ("dr", "doctor"), ("st", "saint"), ("co", "company"), ("jr", "junior"),
+    ("maj", "major"), ("gen", "general"), ("drs", "doctors"), ("rev", "reverend"), ("lt", "lieutenant"),
+    ("hon", "honorable"), ("sgt", "sergeant"), ("capt", "captain"), ("esq", "esquire"), ("ltd", "limited"),
+    ("col", "colonel"), ("ft", "fort")]]
+_ONES = "zero one two three four five six seven eight nine ten eleven twelve thirteen fourteen fifteen sixteen " \
+        "seventeen eighteen nineteen".split()
+_TENS = "_ _ twenty thirty forty fifty sixty seventy eighty ninety".split()
+
+
+def _spell_int(n: int) -> str:
+    if n < 20:
+        return _ONES[n]
+    if n < 100:
+        return _TENS[n // 10] + ("" if n % 10 == 0 else " " + _ONES[n % 10])
+    for div, name in ((10 ** 9, "billion"), (10 ** 6, "million"), (1000, "thousand"), (100, "hundred")):
+        if n >= div:
+            rest = n % div
+            return _spell_int(n // div) + " " + name + ("" if rest == 0 else " " + _spell_int(rest))
+    return str(n)
+
+
+def expand_numbers(text):
+    def rep(m):
+        s = m.group(0).replace(",", "")
+        if "." in s:
+            a, b = s.split(".", 1)
+            return _spell_int(int(a or 0)) + " point " + " ".join(_ONES[int(d)] for d in b if d.isdigit())
+        return _spell_int(int(s))
+    return re.sub(r"\d[\d,]*(\.\d+)?", rep, text)
+
+
+def expand_abbreviations(text):
+    for regex, replacement in _abbreviations:
+        text = re.sub(regex, replacement, text)
+    return text
+
+
+def lowercase(text):
+    return text.lower()
+
+
+def collapse_whitespace(text):
+    return re.sub(_whitespace_re, " ", text)
+
+
+def convert_to_ascii(text):
+    return unicodedata.normalize("NFKD", text).encode("ascii", "ignore").decode("ascii")
+
+
+def basic_cleaners(text):
+    return collapse_whitespace(lowercase(text))
+
+
+def transliteration_cleaners(text):
+    return collapse_whitespace(lowercase(convert_to_ascii(text)))
+
+
+def english_cleaners(text):
+    text = convert_to_ascii(text)
+    text = lowercase(text)
+    text = expand_numbers(text)
+    text = expand_abbreviations(text)
+    return collapse_whitespace(text)

@@ -1,0 +1,21 @@
+"""Build the drop-in Flamed + FaCodec decoder with the fixtures' seeded weights."""
+import os
+
+import yaml
+
+from _common import PKG, SEED, seeded
+from flamed.utils.seeded_init import fill_state_dict
+
+
+def build_flamed(device="cpu", dtype="f32"):
+    from flamed import Flamed
+    from flamed.models.facodec import FACodecDecoder
+    prior = yaml.safe_load(open(os.path.join(PKG, "configs", "prior.yaml")))
+    prob = yaml.safe_load(open(os.path.join(PKG, "configs", "prob.yaml")))
+    m = Flamed({"prior_generator": prior, "prob_generator": prob}).eval()
+    m.load_state_dict(fill_state_dict(m.state_dict(), SEED))
+    dec = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256).eval()
+    dec.load_state_dict(seeded("facodec_decoder"))
+    m.prob_generator.denoiser.hip_dtype = dtype
+    dec.hip_dtype = dtype
+    return m.to(device), dec.to(device)

@@ -255,7 +255,37 @@ def main():
     r3 = torch.randn((2, 3, 4))
     save("rng", r1=r1, r2=r2, r3=r3)
 
-    _ = flamed_mod  # imported to prove the top-level module graph imports with the stubs
+    # ---------------- full Flamed: PriorGenerator.sample + sample_batch end to end ----------------
+    from flamed.text.symbols import symbols as ref_symbols
+    with open(os.path.join(HERE, "symbols.json"), "w") as f:
+        json.dump(list(ref_symbols), f)
+    with torch.inference_mode():
+        model = flamed_mod.Flamed({"prior_generator": prior_cfg, "prob_generator": prob_cfg}).eval()
+        model.device = torch.device("cpu")  # a LightningModule property in the reference (stubbed here)
+        fsd = filler.fill_state_dict(model.state_dict(), SEED)
+        model.load_state_dict(fsd)
+        manifest["flamed"] = {k: list(v.shape) for k, v in fsd.items()}
+        g = torch.Generator().manual_seed(6)
+        n_sym = len(ref_symbols)
+        phon = torch.randint(1, n_sym, (2, 12), generator=g)
+        src_lens = torch.tensor([12, 9])
+        phon[1, 9:] = 0
+        prompts = torch.randint(0, 1024, (2, 6, 20), generator=g)
+        prompts[1, :, 15:] = 1024
+        timbres = torch.randn(2, 256, generator=g)
+        # PriorGenerator.sample alone (PVA noise from the global RNG)
+        torch.manual_seed(99)
+        pe, pl, tm = model.prior_generator.sample(texts=phon, src_lens=src_lens, max_src_len=12, prompts=prompts,
+                                                  prompts_len=20, nfe=4, temperature=0.3)
+        # sample_batch end to end with the decoder (one global-RNG stream: dur, sil, latent noise)
+        torch.manual_seed(99)
+        out = model.sample_batch(phonemes=phon, src_lens=src_lens, prompts=prompts, timbres=timbres,
+                                 codec_decoder=dec, temp_durgen=0.3, temp_denoiser=0.3, nsteps_durgen=4,
+                                 nsteps_denoiser=4)
+        save("flamed_sample", phonemes=phon, src_lens=src_lens, prompts=prompts, timbres=timbres,
+             prior_embs=pe, prior_logits_sum=pl.float().sum(dim=1), tgt_mask=tm,
+             sb_prior_embs=out["prior_embs"], sb_tgt_mask=out["tgt_mask"], sb_latents=out["latents"],
+             sb_wav=out["wav"], rng_seed=99, seed=SEED)
     with open(os.path.join(HERE, "state_dict_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=0, sort_keys=True)
     print("wrote state_dict_manifest.json")
