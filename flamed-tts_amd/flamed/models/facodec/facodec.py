@@ -1,14 +1,19 @@
-"""FaCodec decoder — inference path (drop-in for reference flamed/models/facodec/facodec.py).
+"""FaCodec encoder + decoder (drop-in for reference flamed/models/facodec/facodec.py).
 
-Implemented here: the waveform decoder used by Flamed.sample_batch (`FACodecDecoder.inference`,
-reference :630-638) with the same module tree and state-dict keys (`model.*` with weight-norm
-`weight_g`/`weight_v`, alias-free filter buffers, `timbre_linear.*`).  On a CUDA (ROCm) device the
-whole decoder runs in the gfx950 HIP library (weight norm folded at load, implicit-GEMM convs on MFMA,
-polyphase ConvTranspose, fused Activation1d, graph-captured); the library is mandatory there.
+Implemented with the reference's module tree and state-dict keys:
+  * `FACodecDecoder.inference` (reference :630-638), the waveform decoder used by
+    Flamed.sample_batch (`model.*` with weight-norm `weight_g`/`weight_v`, alias-free filter buffers,
+    `timbre_linear.*`).  On a CUDA (ROCm) device the whole decoder runs in the gfx950 HIP library
+    (weight norm folded at load, implicit-GEMM convs on MFMA, polyphase ConvTranspose, fused
+    Activation1d, graph-captured); the library is mandatory there.
+  * The prompt-encoding path: `FACodecEncoder.forward` (reference :158-244)
+    and `FACodecDecoder.forward(x, vq=True)` (:509-530): the prosody / content / residual factorized
+    RVQs (`quantizer.*`) and the timbre transformer (`timbre_encoder.*`), returning the 6 code streams
+    and the speaker embedding that Flamed.sample feeds to the prior.
 
-Not implemented in this round (prompt encoding): the quantizers, timbre encoder
-and the training-only predictor heads.  Their checkpoint entries are accepted by `load_state_dict`
-and kept in `self.unused_state` so the released decoder checkpoint loads for decoding.
+Not implemented: the training-only predictor heads (`f0_predictor`, `phone_predictor`,
+`res_*_predictor`, `x_timbre_predictor`, used only by `forward(vq=False)`).  Their checkpoint entries are
+accepted by `load_state_dict` and kept in `self.unused_state` so the released checkpoint loads.
 """
 from __future__ import annotations
 
@@ -23,6 +28,8 @@ from torch.nn.utils import weight_norm
 
 from flamed import _native as nat
 from .alias_free_torch import Activation1d
+from .quantize import ResidualVQ
+from .transformer import TransformerEncoder
 
 
 def WNConv1d(*args, **kwargs):
@@ -89,8 +96,62 @@ class DecoderBlock(nn.Module):
         return self.block(x)
 
 
+class EncoderBlock(nn.Module):
+    """3 residual units (dilation 1, 3, 9) at dim//2 -> act -> strided WNConv1d(k=2s) to dim
+    (reference :136-155)."""
+
+    def __init__(self, dim: int = 16, stride: int = 1):
+        super().__init__()
+        half = dim // 2
+        self.block = nn.Sequential(
+            ResidualUnit(half, dilation=1), ResidualUnit(half, dilation=3), ResidualUnit(half, dilation=9),
+            _act(half),
+            WNConv1d(half, dim, kernel_size=2 * stride, stride=stride, padding=stride // 2 + stride % 2))
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class FACodecEncoder(nn.Module):
+    """Waveform (B, 1, n) -> (B, out_channels, n/hop) (reference :158-244)."""
+
+    default_ckpt = os.path.join(os.path.dirname(__file__), "checkpoints", "ns3_facodec_encoder.bin")
+
+    @classmethod
+    def from_pretrained(cls, cfg, ckpt_path=None):
+        enc = cls(ngf=cfg["ngf"], up_ratios=cfg["up_ratios"], out_channels=cfg["out_channels"])
+        sd = torch.load(ckpt_path or cls.default_ckpt, map_location=cfg.get("device", "cpu"), weights_only=True)
+        enc.load_state_dict(sd)
+        return enc.eval()
+
+    def __init__(self, ngf=32, up_ratios=(2, 4, 5, 5), out_channels=1024):
+        super().__init__()
+        self.hop_length = int(np.prod(up_ratios))
+        self.up_ratios = list(up_ratios)
+        self.ngf = ngf
+        self.out_channels = out_channels
+        d = ngf
+        layers: List[nn.Module] = [WNConv1d(1, d, kernel_size=7, padding=3)]
+        for stride in self.up_ratios:
+            d *= 2
+            layers.append(EncoderBlock(d, stride=stride))
+        layers += [_act(d), WNConv1d(d, out_channels, kernel_size=3, padding=1)]
+        self.block = nn.Sequential(*layers)
+        self.enc_dim = d
+        for m in self.modules():
+            if isinstance(m, nn.Conv1d):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.constant_(m.bias, 0)
+
+    def forward(self, x):
+        return self.block(x)
+
+    def inference(self, x):
+        return self.block(x)
+
+
 class FACodecDecoder(nn.Module):
-    """FaCodec waveform decoder (reference :268-660, inference subset)."""
+    """FaCodec decoder (reference :268-660): waveform decoder + prompt-side quantizers / timbre encoder."""
 
     default_ckpt = os.path.join(os.path.dirname(__file__), "checkpoints", "ns3_facodec_decoder.bin")
 
@@ -117,6 +178,23 @@ class FACodecDecoder(nn.Module):
         super().__init__()
         self.in_channels = in_channels
         self.upsample_initial_channel = upsample_initial_channel
+        self.vq_num_q_p, self.vq_num_q_c, self.vq_num_q_r = vq_num_q_p, vq_num_q_c, vq_num_q_r
+        self.codebook_size_prosody = codebook_size_prosody
+        self.codebook_size_content = codebook_size_content
+        self.codebook_size_residual = codebook_size_residual
+        self.use_random_mask_residual = use_random_mask_residual
+        self.prob_random_mask_residual = prob_random_mask_residual
+        self.use_gr_content_f0, self.use_gr_prosody_phone = use_gr_content_f0, use_gr_prosody_phone
+        self.use_gr_residual_f0, self.use_gr_residual_phone = use_gr_residual_f0, use_gr_residual_phone
+        self.use_gr_x_timbre = use_gr_x_timbre
+        vq_kw = dict(dim=vq_dim, codebook_dim=codebook_dim, threshold_ema_dead_code=2, commitment=vq_commit_weight,
+                     weight_init=vq_weight_init, full_commit_loss=vq_full_commit_loss,
+                     quantizer_dropout=quantizer_dropout, dropout_type=dropout_type)
+        self.quantizer = nn.ModuleList([
+            ResidualVQ(num_quantizers=vq_num_q_p, codebook_size=codebook_size_prosody, **vq_kw),
+            ResidualVQ(num_quantizers=vq_num_q_c, codebook_size=codebook_size_content, **vq_kw)])
+        if vq_num_q_r > 0:
+            self.quantizer.append(ResidualVQ(num_quantizers=vq_num_q_r, codebook_size=codebook_size_residual, **vq_kw))
         self.hop_length = int(np.prod(up_ratios))
         self.ngf = ngf
         self.up_ratios = list(up_ratios)
@@ -128,6 +206,9 @@ class FACodecDecoder(nn.Module):
             out_dim = ch // 2 ** (i + 1)
         layers += [_act(out_dim), WNConv1d(out_dim, 1, kernel_size=7, padding=3), nn.Tanh()]
         self.model = nn.Sequential(*layers)
+        self.timbre_encoder = TransformerEncoder(enc_emb_tokens=None, encoder_layer=4, encoder_hidden=256,
+                                                 encoder_head=4, conv_filter_size=1024, conv_kernel_size=5,
+                                                 encoder_dropout=0.1, use_cln=False)
         self.timbre_linear = nn.Linear(in_channels, in_channels * 2)
         with torch.no_grad():
             self.timbre_linear.bias[:in_channels] = 1
@@ -150,6 +231,42 @@ class FACodecDecoder(nn.Module):
 
     def _use_hip(self, x):
         return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+
+    def quantize(self, x, n_quantizers=None):
+        """prosody and content RVQs on x, residual RVQ on x - (prosody + content) (reference :470-507)."""
+        outs, qs, losses, qbuf = 0, [], [], []
+        for i, q in enumerate(self.quantizer):
+            inp = x if i < 2 else x - (qbuf[0] + qbuf[1]).detach()
+            out, idx, loss, quantized = q(inp, n_quantizers=n_quantizers)
+            outs = outs + out
+            qs.append(idx)
+            qbuf.append(quantized.sum(0))
+            losses.append(loss)
+        return outs, torch.cat(qs, dim=0), torch.cat(losses, dim=0), qbuf
+
+    def forward(self, x, vq=True, get_vq=False, eval_vq=True, speaker_embedding=None, n_quantizers=None,
+                quantized=None):
+        """Prompt encoding (reference :509-530): encoder output (B, C, T) ->
+        (quantized sum, codes (n_q, B, T), commit losses, per-RVQ quantized, speaker embedding (B, C))."""
+        if get_vq:
+            return self.quantizer.get_emb() if hasattr(self.quantizer, "get_emb") else [q.get_emb() for q in self.quantizer]
+        if vq is not True:
+            raise NotImplementedError("FACodecDecoder.forward(vq=False) needs the training-only predictor heads, "
+                                      "which this build does not implement")
+        if eval_vq:
+            self.quantizer.eval()
+        outs, qs, commit_loss, qbuf = self.quantize(x, n_quantizers=n_quantizers)
+        spk = self.timbre_encoder(x.transpose(1, 2), None, None).transpose(1, 2).mean(dim=2)
+        return outs, qs, commit_loss, qbuf, spk
+
+    def vq2emb(self, vq, use_residual_code=True):
+        """codes (n_q, B, T) -> summed out-projected code vectors (reference :618-628)."""
+        self.quantizer = self.quantizer.eval()
+        p, c = self.vq_num_q_p, self.vq_num_q_c
+        out = self.quantizer[0].vq2emb(vq[0:p]) + self.quantizer[1].vq2emb(vq[p:p + c])
+        if self.vq_num_q_r > 0 and use_residual_code:
+            out = out + self.quantizer[2].vq2emb(vq[p + c:])
+        return out
 
     def inference(self, x, speaker_embedding):
         """latents (B, in_channels, T), speaker (B, in_channels) -> wav (B, 1, hop*T)."""

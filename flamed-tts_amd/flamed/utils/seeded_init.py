@@ -11,9 +11,9 @@ generation in this container) and this package's modules (GPU box) get bit-ident
 Rules (by key, applied to a template state dict whose keys/shapes define the model):
   * buffers that are deterministic constants are kept from the template: alias-free resampling
     filters (`*.filter`, reference `alias_free_torch/filter.py:27-58`) and sinusoid position tables
-    (`position_enc`);
+    (`position_enc`, FaCodec `position_emb.pe`, reference `facodec/transformer.py:35-51`);
   * SnakeBeta `alpha` / `beta` (log-scale) -> 0.1·N(0,1);
-  * other 1-D `weight` (norm gains) -> 1 + 0.1·N(0,1); 1-D `bias` -> 0.05·N(0,1);
+  * other 1-D `weight` (norm gains) -> 1 + 0.1·N(0,1); 1-D `bias` / `*_bias` -> 0.05·N(0,1);
   * weight-norm `weight_g` -> ||weight_v|| over all dims but 0 (effective weight = weight_v);
   * everything else -> N(0,1)/sqrt(numel/shape[0]).
 Pure torch on CPU; no GPU, no reference code.
@@ -26,7 +26,7 @@ from typing import Dict, Mapping
 
 import torch
 
-_KEEP_SUBSTRINGS = ("position_enc",)
+_KEEP_SUBSTRINGS = ("position_enc", "position_emb.pe")
 
 
 def _gen(seed: int, key: str) -> torch.Generator:
@@ -49,7 +49,7 @@ def seeded_value(key: str, template: torch.Tensor, seed: int) -> torch.Tensor:
     if leaf in ("alpha", "beta") and len(shape) == 1:
         return 0.1 * torch.randn(shape, generator=g)
     if len(shape) <= 1:
-        if leaf == "bias":
+        if leaf == "bias" or leaf.endswith("_bias"):
             return 0.05 * torch.randn(shape, generator=g)
         return 1.0 + 0.1 * torch.randn(shape, generator=g)
     fan_in = max(1, math.prod(shape[1:]))

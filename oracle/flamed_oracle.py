@@ -360,3 +360,102 @@ def facodec_decode(sd: SD, x: torch.Tensor, spk: torch.Tensor, up_ratios: Sequen
     h = activation1d(sd, f"{p}model.{n}", h)
     h = F.conv1d(h, wn_weight(sd, f"{p}model.{n + 1}"), sd[f"{p}model.{n + 1}.bias"], padding=3)
     return torch.tanh(h)
+
+
+# ============================ FaCodec prompt encoding ==========================
+
+def encoder_block(sd: SD, p: str, x: torch.Tensor, stride: int) -> torch.Tensor:
+    """EncoderBlock, facodec.py:136-155: 3 residual units (dil 1,3,9) -> Act1d -> strided WNConv1d."""
+    for j, d in enumerate((1, 3, 9)):
+        x = residual_unit(sd, f"{p}.block.{j}", x, d)
+    x = activation1d(sd, p + ".block.3", x)
+    return F.conv1d(x, wn_weight(sd, p + ".block.4"), sd[p + ".block.4.bias"], stride=stride,
+                    padding=stride // 2 + stride % 2)
+
+
+def facodec_encode(sd: SD, wav: torch.Tensor, up_ratios: Sequence[int] = (2, 4, 5, 5), p: str = "") -> torch.Tensor:
+    """FACodecEncoder.forward, facodec.py:183-216.  wav (B,1,n) -> (B,out_channels,n/hop)."""
+    h = F.conv1d(wav, wn_weight(sd, p + "block.0"), sd[p + "block.0.bias"], padding=3)
+    for i, s in enumerate(up_ratios):
+        h = encoder_block(sd, f"{p}block.{i + 1}", h, s)
+    n = len(up_ratios) + 1
+    h = activation1d(sd, f"{p}block.{n}", h)
+    return F.conv1d(h, wn_weight(sd, f"{p}block.{n + 1}"), sd[f"{p}block.{n + 1}.bias"], padding=1)
+
+
+def _wn_linear(sd: SD, p: str, x: torch.Tensor) -> torch.Tensor:
+    return F.linear(x, wn_weight(sd, p), sd[p + ".bias"])
+
+
+def fvq_quantize(sd: SD, p: str, z: torch.Tensor):
+    """FactorizedVectorQuantize.forward (eval), fvq.py:35-87 + decode_latents :102-116.
+    z (B,D,T) -> (z_q (B,D,T), indices (B,T) int64).  Nearest code under L2-normalised euclidean
+    distance (first index on ties, as torch.max), straight-through `z_e + (z_q - z_e)` kept."""
+    B, D, T = z.shape
+    z_e = _wn_linear(sd, p + ".in_proj", z.transpose(1, 2))                       # (B,T,d)
+    e = F.normalize(z_e.reshape(B * T, -1))
+    cb_raw = sd[p + "._codebook.weight"]
+    cb = F.normalize(cb_raw)
+    dist = e.pow(2).sum(1, keepdim=True) - 2 * e @ cb.t() + cb.pow(2).sum(1, keepdim=True).t()
+    idx = (-dist).max(1)[1].reshape(B, T)
+    z_q = cb_raw[idx]                                                               # (B,T,d)
+    z_q = z_e + (z_q - z_e)
+    return _wn_linear(sd, p + ".out_proj", z_q).transpose(1, 2), idx
+
+
+def rvq_quantize(sd: SD, p: str, x: torch.Tensor, n_layers: int):
+    """ResidualVQ.forward (eval), rvq.py:27-76.  Returns (sum, indices (n,B,T), quantized (n,B,D,T))."""
+    out, res, idx, qs = 0.0, x, [], []
+    for i in range(n_layers):
+        q, ind = fvq_quantize(sd, f"{p}.layers.{i}", res)
+        res = res - q
+        out = out + q
+        idx.append(ind)
+        qs.append(q)
+    return out, torch.stack(idx), torch.stack(qs)
+
+
+def positional_table(d: int, max_len: int = 5000) -> torch.Tensor:
+    """PositionalEncoding buffer `pe` (max_len, 1, d), facodec/transformer.py:35-47."""
+    pos = torch.arange(max_len).unsqueeze(1)
+    freq = torch.exp(torch.arange(0, d, 2) * (-math.log(10000.0) / d))
+    pe = torch.zeros(max_len, 1, d)
+    pe[:, 0, 0::2] = torch.sin(pos * freq)
+    pe[:, 0, 1::2] = torch.cos(pos * freq)
+    return pe
+
+
+def timbre_encoder(sd: SD, x: torch.Tensor, p: str = "timbre_encoder", n_layers: int = 4, heads: int = 4) -> torch.Tensor:
+    """TransformerEncoder.forward (use_cln False, no padding mask), transformer.py:154-234, with
+    nn.MultiheadAttention restated (scaled dot-product, softmax over keys).  x (B,T,d) -> (B,T,d).
+    PositionalEncoding adds pe[:B] — the batch index picks the position vector (:49-51)."""
+    B, T, d = x.shape
+    x = x + sd[p + ".position_emb.pe"][:B]
+    hd = d // heads
+    for i in range(n_layers):
+        q = f"{p}.layers.{i}"
+        h = F.layer_norm(x, (d,), sd[q + ".ln_1.weight"], sd[q + ".ln_1.bias"], 1e-5)
+        qkv = F.linear(h, sd[q + ".self_attn.in_proj_weight"], sd[q + ".self_attn.in_proj_bias"])
+        qq, kk, vv = (t.reshape(B, T, heads, hd).transpose(1, 2) for t in qkv.split(d, dim=-1))
+        att = torch.softmax((qq / math.sqrt(hd)) @ kk.transpose(-1, -2), dim=-1)
+        a = (att @ vv).transpose(1, 2).reshape(B, T, d)
+        x = x + F.linear(a, sd[q + ".self_attn.out_proj.weight"], sd[q + ".self_attn.out_proj.bias"])
+        h = F.layer_norm(x, (d,), sd[q + ".ln_2.weight"], sd[q + ".ln_2.bias"], 1e-5)
+        h = F.conv1d(h.transpose(1, 2), sd[q + ".ffn.ffn_1.weight"], sd[q + ".ffn.ffn_1.bias"],
+                     padding=sd[q + ".ffn.ffn_1.weight"].shape[-1] // 2).transpose(1, 2)
+        x = x + F.linear(F.relu(h), sd[q + ".ffn.ffn_2.weight"], sd[q + ".ffn.ffn_2.bias"])
+    return F.layer_norm(x, (d,), sd[p + ".last_ln.weight"], sd[p + ".last_ln.bias"], 1e-5)
+
+
+def decoder_vq(sd: SD, x: torch.Tensor, n_q=(1, 2, 3)):
+    """FACodecDecoder.forward(vq=True) (eval), facodec.py:470-530.  x (B,C,T) encoder output ->
+    (codes (sum n_q, B, T) int64 in [prosody, content, residual] order, spk (B,C)).  The residual RVQ
+    sees x - (sum of prosody layers + sum of content layers) (:495-497)."""
+    _, ip, qp = rvq_quantize(sd, "quantizer.0", x, n_q[0])
+    _, ic, qc = rvq_quantize(sd, "quantizer.1", x, n_q[1])
+    codes = [ip, ic]
+    if n_q[2] > 0:
+        _, ir, _ = rvq_quantize(sd, "quantizer.2", x - (qp.sum(0) + qc.sum(0)), n_q[2])
+        codes.append(ir)
+    spk = timbre_encoder(sd, x.transpose(1, 2)).transpose(1, 2).mean(dim=2)
+    return torch.cat(codes, dim=0), spk

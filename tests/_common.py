@@ -30,7 +30,12 @@ def template(name):
     t = {}
     filt = orc.kaiser_sinc_filter(0.25, 0.3, 12).reshape(1, 1, 12)
     for k, shape in manifest(name).items():
-        t[k] = filt.clone() if k.endswith(".filter") else torch.zeros(shape)
+        if k.endswith(".filter"):
+            t[k] = filt.clone()
+        elif k.endswith("position_emb.pe"):
+            t[k] = orc.positional_table(shape[-1], shape[0])
+        else:
+            t[k] = torch.zeros(shape)
     return t
 
 

@@ -19,3 +19,10 @@ def build_flamed(device="cpu", dtype="f32"):
     m.prob_generator.denoiser.hip_dtype = dtype
     dec.hip_dtype = dtype
     return m.to(device), dec.to(device)
+
+
+def build_codec_encoder(device="cpu"):
+    from flamed.models.facodec import FACodecEncoder
+    e = FACodecEncoder(ngf=32, up_ratios=[2, 4, 5, 5], out_channels=256).eval()
+    e.load_state_dict(seeded("facodec_encoder"))
+    return e.to(device)

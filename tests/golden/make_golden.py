@@ -13,6 +13,7 @@ The reference never leaves this container; only these data files are committed.
 from __future__ import annotations
 
 import argparse
+import math
 import importlib.util
 import json
 import os
@@ -97,7 +98,7 @@ def main():
 
     from flamed.models.synthesizer.prob_generator import ProbGenerator, SimpleMLPAdaLN
     from flamed.models.synthesizer.pva import PVA, LengthRegulator, ProbabilisticModule
-    from flamed.models.facodec import FACodecDecoder
+    from flamed.models.facodec import FACodecDecoder, FACodecEncoder
     from flamed.models.facodec.alias_free_torch import Activation1d
     from flamed.models.facodec.facodec import SnakeBeta
     from flamed.models import flamed as flamed_mod
@@ -248,6 +249,38 @@ def main():
         save("act1d", x=xa, y=ya, alpha=asd["act.alpha"], beta=asd["act.beta"],
              up_filter=asd["upsample.filter"], down_filter=asd["downsample.lowpass.filter"])
 
+    # ---------------- FaCodec prompt encoding: encoder + RVQ codes + timbre (§8(f) f3) ------------
+    with torch.inference_mode():
+        enc = FACodecEncoder(ngf=32, up_ratios=[2, 4, 5, 5], out_channels=256).eval()
+        esd = filler.fill_state_dict(enc.state_dict(), SEED)
+        enc.load_state_dict(esd)
+        manifest["facodec_encoder"] = {k: list(v.shape) for k, v in esd.items()}
+        g = torch.Generator().manual_seed(8)
+        n = 8000
+        tt = torch.arange(n, dtype=torch.float32) / 16000.0
+        wav = 0.3 * torch.sin(2 * math.pi * 220.0 * tt)[None, None, :] * torch.tensor([1.0, 0.5])[:, None, None] \
+            + 0.05 * torch.randn(2, 1, n, generator=g)
+        # top-2 distance gap of every FVQ decision (near-ties could flip on another device)
+        gaps = []
+
+        def _gap_hook(mod, inp, out):
+            z = inp[0]
+            ze = mod.in_proj(z.transpose(1, 2))
+            e = torch.nn.functional.normalize(ze.reshape(-1, ze.shape[-1]))
+            cb = torch.nn.functional.normalize(mod.codebook.weight)
+            d = e.pow(2).sum(1, keepdim=True) - 2 * e @ cb.t() + cb.pow(2).sum(1, keepdim=True).t()
+            top2 = torch.topk(-d, 2, dim=1).values
+            gaps.append(float((top2[:, 0] - top2[:, 1]).min()))
+
+        hooks = [layer.register_forward_hook(_gap_hook) for q in dec.quantizer for layer in q.layers]
+        enc_out = enc(wav)
+        qsum, codes, _, qbuf, spk = dec(enc_out, eval_vq=False, vq=True)
+        for h in hooks:
+            h.remove()
+        save("facodec_encode", wav=wav, enc_out=enc_out, codes=codes, spk=spk, qbuf=torch.stack(qbuf),
+             qsum=qsum, vq_gap_min=np.float32(min(gaps)), seed=SEED)
+        print("fvq top-2 gap min", min(gaps))
+
     # ---------------- CPU RNG stream (global generator, reference draw order) --------------------
     torch.manual_seed(0)
     r1 = torch.randn((2, 5))
@@ -286,6 +319,13 @@ def main():
              prior_embs=pe, prior_logits_sum=pl.float().sum(dim=1), tgt_mask=tm,
              sb_prior_embs=out["prior_embs"], sb_tgt_mask=out["tgt_mask"], sb_latents=out["latents"],
              sb_wav=out["wav"], rng_seed=99, seed=SEED)
+        # Flamed.sample with a raw prompt: frontend skipped (phonemes given), prompt encode, sample, decode
+        torch.manual_seed(101)
+        wav_prompt = wav[0, 0, :6000].numpy()
+        res = model.sample(phonemes=phon[1, :9], prompt_raw=wav_prompt, sr=16000, codec_encoder=enc,
+                           codec_decoder=dec, temp_durgen=0.3, temp_denoiser=0.3, nsteps_durgen=4,
+                           nsteps_denoiser=4)
+        save("flamed_sample_raw", phonemes=phon[1, :9], prompt=wav_prompt, wav=res["wav"], rng_seed=101, seed=SEED)
     with open(os.path.join(HERE, "state_dict_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=0, sort_keys=True)
     print("wrote state_dict_manifest.json")

@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from _common import golden, t32, rel_l2
-from _flamed_common import build_flamed
+from _flamed_common import build_flamed, build_codec_encoder
 
 
 @pytest.fixture(scope="module")
@@ -40,6 +40,20 @@ def test_sample_batch(models):
     assert rel_l2(out["latents"], g["sb_latents"]) < 1e-4
     assert out["wav"].shape == g["sb_wav"].shape
     assert rel_l2(out["wav"], g["sb_wav"]) < 1e-3
+
+
+def test_sample_raw_prompt(models):
+    """Flamed.sample with a raw waveform prompt: prompt encode (encoder + RVQ + timbre) -> sample_batch
+    -> decode, vs the reference (flamed.py:89-166)."""
+    m, dec = models
+    enc = build_codec_encoder("cpu")
+    g = golden("flamed_sample_raw")
+    torch.manual_seed(int(g["rng_seed"]))
+    res = m.sample(phonemes=t32(g["phonemes"]), prompt_raw=g["prompt"], sr=16000, codec_encoder=enc,
+                   codec_decoder=dec, temp_durgen=0.3, temp_denoiser=0.3, nsteps_durgen=4, nsteps_denoiser=4)
+    assert set(res) == {"wav", "time"}
+    assert res["wav"].shape == g["wav"].shape
+    assert rel_l2(res["wav"], g["wav"]) < 1e-3
 
 
 def test_sample_argument_contract(models):

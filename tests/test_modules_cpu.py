@@ -36,7 +36,11 @@ def test_state_dict_schemas_match_reference():
     d = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256)
     ref = manifest("facodec_decoder")
     assert all(ref[k] == list(v.shape) for k, v in d.state_dict().items())
-    assert set(ref) - set(d.state_dict()) == {k for k in ref if not k.startswith(("model.", "timbre_linear."))}
+    heads = ("f0_predictor.", "phone_predictor.", "res_f0_predictor.", "res_phone_predictor.", "x_timbre_predictor.")
+    assert set(ref) - set(d.state_dict()) == {k for k in ref if k.startswith(heads)}
+    from flamed.models.facodec import FACodecEncoder
+    e = FACodecEncoder(ngf=32, up_ratios=[2, 4, 5, 5], out_channels=256)
+    assert {k: list(v.shape) for k, v in e.state_dict().items()} == manifest("facodec_encoder")
 
 
 def test_hip_weight_lists():
@@ -93,3 +97,23 @@ def test_facodec_cpu_path():
     with torch.inference_mode():
         w = d.inference(t32(g["lat1"]), t32(g["spk1"]))
     assert rel_l2(w, g["wav1"]) < 1e-4
+
+
+def test_prompt_encode_cpu_path():
+    """FACodecEncoder + FACodecDecoder.forward(vq=True) (§8(f) f3) vs the reference fixture."""
+    from flamed.models.facodec import FACodecDecoder, FACodecEncoder
+    e = FACodecEncoder(ngf=32, up_ratios=[2, 4, 5, 5], out_channels=256).eval()
+    e.load_state_dict(seeded("facodec_encoder"))
+    d = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256).eval()
+    d.load_state_dict(seeded("facodec_decoder"))
+    g = golden("facodec_encode")
+    with torch.inference_mode():
+        z = e(t32(g["wav"]))
+        qsum, codes, losses, qbuf, spk = d(t32(g["enc_out"]), eval_vq=False, vq=True)
+        emb = d.vq2emb(codes)
+    assert rel_l2(z, g["enc_out"]) < TOL
+    assert torch.equal(codes, t32(g["codes"]))
+    assert rel_l2(spk, g["spk"]) < TOL
+    assert rel_l2(qsum, g["qsum"]) < TOL and rel_l2(torch.stack(qbuf), g["qbuf"]) < TOL
+    assert losses.shape == (6,) and float(losses.abs().sum()) == 0.0
+    assert rel_l2(emb, g["qsum"]) < 1e-4  # codes -> embeddings reproduces the quantized sum

@@ -116,3 +116,16 @@ def test_facodec_decode():
     assert rel_l2(w1, g["wav1"]) < 1e-4
     w2 = orc.facodec_decode(sd, t32(g["lat2"]), t32(g["spk2"]))
     assert rel_l2(w2, g["wav2"]) < 1e-4
+
+
+def test_facodec_encode_and_vq():
+    """Encoder, factorized RVQ codes (bit-exact) and timbre embedding vs the reference (§8(f) f3)."""
+    g = golden("facodec_encode")
+    esd = seeded("facodec_encoder")
+    dsd = seeded("facodec_decoder")
+    enc = orc.facodec_encode(esd, t32(g["wav"]))
+    assert rel_l2(enc, g["enc_out"]) < TOL
+    codes, spk = orc.decoder_vq(dsd, t32(g["enc_out"]))
+    assert torch.equal(codes, t32(g["codes"]))
+    assert rel_l2(spk, g["spk"]) < TOL
+    assert orc.positional_table(256).shape == (5000, 1, 256)
