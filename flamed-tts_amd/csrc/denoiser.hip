@@ -19,11 +19,24 @@ namespace fl {
 
 // ------------------------------ denoiser loaders / epilogues ------------------------------
 
+// Device-side Euler step index (graph replay of a few captured steps, see flamed_den_solve): the
+// modulation rows of step s live at mods + s * stride; a null `step` means offset 0.
+struct StepOff {
+  const int* __restrict__ step;
+  long long stride;
+  __device__ __forceinline__ long long get() const { return step ? (long long)(*step) * stride : 0; }
+};
+
 struct ModRef {  // AdaLN modulation vectors: row = m / div, stride `ms` floats
   const float* __restrict__ sh;
   const float* __restrict__ sc;
   int ms;
   int div;
+  StepOff so;
+  __device__ __forceinline__ ModRef at() const {  // pointers advanced to the current step
+    const long long o = so.get();
+    return ModRef{sh + o, sc + o, ms, div, StepOff{nullptr, 0}};
+  }
 };
 
 // LayerNorm (+ optional affine) + AdaLN modulate of fp32 rows, converted to DT (A-operand loader).
@@ -55,13 +68,14 @@ struct LoadLNMod {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / mod.div, r1 = last / mod.div;
     if (r1 - r0 > 1) return false;
+    const ModRef md = mod.at();
     for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * K; idx += blockDim.x) {
       int slot = idx / K, k = idx - slot * K;
-      size_t mo = (size_t)(r0 + slot) * mod.ms + k;
-      float sc1 = 1.0f + mod.sc[mo];
+      size_t mo = (size_t)(r0 + slot) * md.ms + k;
+      float sc1 = 1.0f + md.sc[mo];
       float w = AFF ? lnw[k] : 1.0f, b = AFF ? lnb[k] : 0.0f;
       vec[(2 * slot) * K + k] = w * sc1;
-      vec[(2 * slot + 1) * K + k] = b * sc1 + mod.sh[mo];
+      vec[(2 * slot + 1) * K + k] = b * sc1 + md.sh[mo];
     }
     return true;
   }
@@ -86,12 +100,13 @@ struct LoadLNMod {
 #pragma unroll
       for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - mean) * rstd) * va[j] + vb[j];
     } else {  // rare path (per-frame t or tiles spanning > 2 modulation rows): vectors from global
-      size_t mo = (size_t)(m / mod.div) * mod.ms + k;
+      const ModRef md = mod.at();
+      size_t mo = (size_t)(m / md.div) * md.ms + k;
 #pragma unroll
       for (int j = 0; j < EPC; ++j) {
-        float sc1 = 1.0f + mod.sc[mo + j];
+        float sc1 = 1.0f + md.sc[mo + j];
         float w = AFF ? lnw[k + j] : 1.0f, b = AFF ? lnb[k + j] : 0.0f;
-        o[j] = ((r.v[j] - mean) * rstd) * (w * sc1) + (b * sc1 + mod.sh[mo + j]);
+        o[j] = ((r.v[j] - mean) * rstd) * (w * sc1) + (b * sc1 + md.sh[mo + j]);
       }
     }
     return pack_chunk<D>(o);
@@ -144,14 +159,16 @@ struct EpiConvNeXtResid {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / mod.div, r1 = last / mod.div;
     if (r1 - r0 > 1) return false;
+    const long long so = mod.so.get();
+    const ModRef md = mod.at();
     for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {
       int slot = idx / BN, c = idx - slot * BN, n = bn + c;
-      size_t mo = (size_t)(r0 + slot) * mod.ms + n;
-      float sc1 = 1.0f + mod.sc[mo];
+      size_t mo = (size_t)(r0 + slot) * md.ms + n;
+      float sc1 = 1.0f + md.sc[mo];
       float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
       vec[c * 8 + slot * 3 + 0] = w * sc1;
-      vec[c * 8 + slot * 3 + 1] = b * sc1 + mod.sh[mo];
-      vec[c * 8 + slot * 3 + 2] = gate[mo];
+      vec[c * 8 + slot * 3 + 1] = b * sc1 + md.sh[mo];
+      vec[c * 8 + slot * 3 + 2] = gate[so + mo];
       if (slot == 0) vec[c * 8 + 6] = b3[n];
     }
     return true;
@@ -164,11 +181,13 @@ struct EpiConvNeXtResid {
       float h = xh * v[0] + v[1];
       return x + v[2] * (h + (acc + vec[(n - bn) * 8 + 6]));
     }
-    size_t mo = (size_t)(m / mod.div) * mod.ms + n;
-    float sc1 = 1.0f + mod.sc[mo];
+    const long long so = mod.so.get();
+    const ModRef md = mod.at();
+    size_t mo = (size_t)(m / md.div) * md.ms + n;
+    float sc1 = 1.0f + md.sc[mo];
     float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
-    float h = xh * (w * sc1) + (b * sc1 + mod.sh[mo]);
-    return x + gate[mo] * (h + (acc + b3[n]));
+    float h = xh * (w * sc1) + (b * sc1 + md.sh[mo]);
+    return x + gate[so + mo] * (h + (acc + b3[n]));
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
@@ -184,6 +203,7 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
   int ms, div;
   float* __restrict__ Sout;
   int NTout;
+  StepOff so;
   static constexpr bool kRowStats = true;
   static constexpr int kEVec = 4;
   static constexpr int stat_rows(int) { return 0; }
@@ -191,9 +211,10 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / div, r1 = last / div;
     if (r1 - r0 > 1) return false;
+    const float* g = gate + so.get();
     for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {
       int slot = idx / BN, c = idx - slot * BN, n = bn + c;
-      vec[c * 4 + slot] = gate[(size_t)(r0 + slot) * ms + n];
+      vec[c * 4 + slot] = g[(size_t)(r0 + slot) * ms + n];
       if (slot == 0) vec[c * 4 + 2] = b[n];
     }
     return true;
@@ -204,7 +225,7 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
       const float* v = vec + (n - bn) * 4;
       return x + v[m / div - bm / div] * (acc + v[2]);
     }
-    return x + gate[(size_t)(m / div) * ms + n] * (acc + b[n]);
+    return x + gate[so.get() + (size_t)(m / div) * ms + n] * (acc + b[n]);
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
@@ -251,6 +272,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * kDwCG, ts = blockIdx.y, b = blockIdx.z;
   const int t0 = ts * kDwTC;
+  mod = mod.at();
   // one modulation row for the whole utterance (sampling path): stage alpha/beta once
   const bool uni = ((size_t)b * T) / mod.div == ((size_t)b * T + T - 1) / mod.div;
   if (uni && tid < kDwCG) {
@@ -425,8 +447,9 @@ struct LoadGN {
 // FinalLayer conv_out (k=3, pad=1) from the tap-stacked GEMM Y[m] = [W_0; W_1; W_2] x_mod[m]:
 // v[t] = b + Y0[t-1] + Y1[t] + Y2[t+1] within each utterance; then xt += dt*v (or v_out = v).
 __global__ void conv3_combine_kernel(const float* __restrict__ Y, const float* __restrict__ bias, float* xt,
-                                     float* __restrict__ vout, int M, int T, int C, float dt) {
+                                     float* __restrict__ vout, int M, int T, int C, float dt, int* step_ctr) {
   size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (step_ctr && idx == 0) *step_ctr += 1;  // last kernel of the step; nothing in it reads the counter
   if (idx >= (size_t)M * C) return;
   int m = idx / C, n = idx - (size_t)m * C;
   int t = m % T;
@@ -501,6 +524,7 @@ struct Den {
   hipStream_t cap_stream = nullptr;
   int g_B = -1, g_T = -1, g_nfe = -1;
   const void *g_xt = nullptr, *g_mods = nullptr, *g_ws = nullptr;
+  int* ctr = nullptr;  // device Euler step counter for graph replay
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -561,6 +585,7 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
   if (!d) return kOk;
   if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
   if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
+  if (d->ctr) (void)hipFree(d->ctr);
   if (d->dev) (void)hipFree(d->dev);
   delete d;
   return kOk;
@@ -713,10 +738,13 @@ static inline void kt_mark(int c, hipStream_t st) {
 }
 
 // One velocity evaluation (+ Euler update when vout == nullptr).
+// `ctr` (optional): device step counter; when set the modulation rows are read at
+// mods + (*ctr) * B * MS and the last kernel increments it (graph replay of captured steps).
 template <typename DT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
-                         const DenWs& w, hipStream_t st) {
+                         const DenWs& w, int* ctr, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
+  const StepOff so{ctr, (long long)B * MS};
   const GemmCfg cfg = pick_cfg(M);
   const int BN = cfg_bn(cfg);
   const int NT = H / BN;
@@ -728,8 +756,8 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
-    ModRef mc{md, md + H, MS, mod_div};
-    ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div};
+    ModRef mc{md, md + H, MS, mod_div, so};
+    ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
     K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
     K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
     K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
@@ -740,11 +768,11 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     K_(5, (launch_gemm_auto<DT>(cfg, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
                                         EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
     K_(6, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
-                                        EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT}, M, H, H, st)));
+                                        EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
-  ModRef mc{mf, mf + H, MS, mod_div};
-  ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div};
+  ModRef mc{mf, mf + H, MS, mod_div, so};
+  ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div, so};
   const DenBlockW& F = d->fin;
   K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
   K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
@@ -756,7 +784,7 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
                                       EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
   {
     size_t n = (size_t)M * C;
-    hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt);
+    hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, ctr);
     FL_LAUNCH_CHECK();
     kt_mark(8, st);
   }
@@ -766,11 +794,19 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
 }
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
-                    hipStream_t st) {
+                    hipStream_t st, int* ctr = nullptr) {
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
-  if (d->dt == FLAMED_BF16) return den_step_impl<bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
-  return den_step_impl<float>(d, xt, mods, mod_div, B, T, dt, vout, w, st);
+  if (d->dt == FLAMED_BF16) return den_step_impl<bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+  return den_step_impl<float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+}
+
+// Steps per captured graph: the largest divisor of nfe that is <= 16 (the graph is replayed nfe/G
+// times per solve, so a new (B, T) costs one G-step capture instead of an nfe-step one).
+static int graph_chunk(int nfe) {
+  for (int g = 16; g > 1; --g)
+    if (nfe % g == 0) return g;
+  return 1;
 }
 
 }  // namespace fl
@@ -820,13 +856,16 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     }
     return kOk;
   }
+  const int G = graph_chunk(nfe);
+  if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
+  // the graph bakes in dt = 1/nfe, so nfe is part of the key
   const bool hit = d->gexec && d->g_B == B && d->g_T == T && d->g_nfe == nfe && d->g_xt == xt && d->g_mods == mods && d->g_ws == ws;
   if (!hit) {
     if (d->gexec) { FL_HIP(hipGraphExecDestroy(d->gexec)); d->gexec = nullptr; }
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
     int rc = kOk;
-    for (int s = 0; s < nfe && rc == kOk; ++s) rc = den_step(d, xt, mods + s * step_stride, T, B, T, dt, nullptr, ws, d->cap_stream);
+    for (int s = 0; s < G && rc == kOk; ++s) rc = den_step(d, xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
@@ -836,7 +875,8 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     FL_HIP(ie);
     d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
   }
-  FL_HIP(hipGraphLaunch(d->gexec, st));
+  FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
+  for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
   return kOk;
 }
 

@@ -52,7 +52,8 @@ __global__ void split_proj_kernel(const float* __restrict__ src, float* __restri
   else we[(size_t)r * D + c - 1] = src[i];
 }
 
-// conv1 A operand: out0[src] = P[src] + w0 * xt[src] + temb (zero outside the utterance)
+// conv1 A operand: out0[src] = P[src] + w0 * xt[src] + temb (zero outside the utterance).  With a
+// device step counter `ctr` the time-embedding row is temb + (*ctr) * Cin (graph replay).
 struct LoadDurIn {
   const float* __restrict__ P;
   const float* __restrict__ w0;
@@ -60,6 +61,7 @@ struct LoadDurIn {
   const float* __restrict__ temb;
   int Cin;
   int L;
+  const int* __restrict__ ctr;
   struct Raw { float v[4]; };
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
@@ -72,7 +74,8 @@ struct LoadDurIn {
       return r;
     }
     int src = m + tap - 1;
-    float4 p = ld4(P + (size_t)src * Cin + c), w = ld4(w0 + c), te = ld4(temb + c);
+    const float* tr = temb + (ctr ? (size_t)(*ctr) * Cin : 0);
+    float4 p = ld4(P + (size_t)src * Cin + c), w = ld4(w0 + c), te = ld4(tr + c);
     float x = xt[src];
     r.v[0] = (p.x + w.x * x) + te.x;
     r.v[1] = (p.y + w.y * x) + te.y;
@@ -88,8 +91,9 @@ template <int F>
 __global__ __launch_bounds__(256) void dur_head_kernel(const float* __restrict__ R2, const float* __restrict__ g,
                                                        const float* __restrict__ b, const float* __restrict__ wl,
                                                        const float* __restrict__ bl, const uint8_t* __restrict__ mask,
-                                                       float* xt, int M, float dt) {
+                                                       float* xt, int M, float dt, int* ctr) {
   constexpr int PER = F / 64;
+  if (ctr && blockIdx.x == 0 && threadIdx.x == 0) *ctr += 1;  // end of an Euler step (sil net head)
   int m = blockIdx.x * 4 + (threadIdx.x >> 6);
   int lane = threadIdx.x & 63;
   if (m >= M) return;
@@ -133,6 +137,7 @@ struct PvaGraph {
   hipGraphExec_t exec = nullptr;
   hipStream_t cap = nullptr;
   std::vector<const void*> key;
+  int* ctr = nullptr;  // device Euler step counter
 };
 static PvaGraph g_pva;  // one cached graph per process (durgen is tiny; recaptured on any change)
 
@@ -168,17 +173,17 @@ static int net_prepare(DurNet* n, const float* enc, int M, const float* ts, int 
 }
 
 static int net_step(DurNet* n, const float* P, const float* temb, float* xt, const uint8_t* mask, int B, int L, float dt,
-                    const PvaWs& w, hipStream_t st) {
+                    const PvaWs& w, hipStream_t st, const int* ctr = nullptr, int* ctr_inc = nullptr) {
   const int M = B * L, D = n->D, F = n->F;
   const int NT = F / 64;
   int rc;
-  if ((rc = launch_gemm_auto<float>(pick_cfg(M) == kCfgSmall ? kCfgSmall : kCfgMid, LoadDurIn{P, n->w0, xt, temb, D, L}, n->c1w, 3 * D,
+  if ((rc = launch_gemm_auto<float>(pick_cfg(M) == kCfgSmall ? kCfgSmall : kCfgMid, LoadDurIn{P, n->w0, xt, temb, D, L, ctr}, n->c1w, 3 * D,
                                           EpiBiasStatsT<true>{n->c1b, w.R1, F, w.S1, NT}, M, F, 3 * D, st)))
     return rc;
   if ((rc = launch_gemm<float>(LoadConvRows<float, true>{w.R1, F, L, 3, 1, w.S1, NT, 64, 1e-5f, n->g1, n->b1}, n->c2w,
                                           3 * F, EpiBiasAct<float, 3>{n->c2b, w.R2, F}, M, F, 3 * F, st)))
     return rc;
-  hipLaunchKernelGGL(dur_head_kernel<384>, dim3((M + 3) / 4), dim3(256), 0, st, w.R2, n->g2, n->b2, n->lw, n->lb, mask, xt, M, dt);
+  hipLaunchKernelGGL(dur_head_kernel<384>, dim3((M + 3) / 4), dim3(256), 0, st, w.R2, n->g2, n->b2, n->lw, n->lb, mask, xt, M, dt, ctr_inc);
   FL_LAUNCH_CHECK();
   return kOk;
 }
@@ -330,22 +335,29 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   int rc;
   if ((rc = net_prepare(nd, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBd, w.Pd, st))) return rc;
   if ((rc = net_prepare(ns, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBs, w.Ps, st))) return rc;
-  auto body = [&](hipStream_t s) -> int {
-    int r;
+  if (!use_graph) {
     for (int i = 0; i < nfe; ++i) {  // dur then sil on every step (pva.py:104-109)
-      if ((r = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, w, s))) return r;
-      if ((r = net_step(ns, w.Ps, w.TEMBs + (size_t)i * D, sil_t, mask, B, L, dt, w, s))) return r;
+      if ((rc = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, w, st))) return rc;
+      if ((rc = net_step(ns, w.Ps, w.TEMBs + (size_t)i * D, sil_t, mask, B, L, dt, w, st))) return rc;
     }
     return kOk;
-  };
-  if (!use_graph) return body(st);
+  }
+  // graph of G steps replayed nfe/G times; the step's time-embedding row comes from a device counter
+  int G = 1;
+  for (int g = 16; g > 1; --g)
+    if (nfe % g == 0) { G = g; break; }
+  if (!g_pva.ctr) FL_HIP(hipMalloc(&g_pva.ctr, 256));
   std::vector<const void*> key = {nd, ns, enc, mask, dur_t, sil_t, ts, ws, (const void*)(intptr_t)nfe,
                                   (const void*)(intptr_t)B, (const void*)(intptr_t)L, nd->dev, ns->dev};
   if (!g_pva.exec || g_pva.key != key) {
     if (g_pva.exec) { FL_HIP(hipGraphExecDestroy(g_pva.exec)); g_pva.exec = nullptr; }
     if (!g_pva.cap) FL_HIP(hipStreamCreateWithFlags(&g_pva.cap, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(g_pva.cap, hipStreamCaptureModeRelaxed));
-    int r = body(g_pva.cap);
+    int r = kOk;
+    for (int i = 0; i < G && r == kOk; ++i) {
+      r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, w, g_pva.cap, g_pva.ctr, nullptr);
+      if (r == kOk) r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, w, g_pva.cap, g_pva.ctr, g_pva.ctr);
+    }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(g_pva.cap, &g);
     if (r) { if (g) (void)hipGraphDestroy(g); return r; }
@@ -355,7 +367,8 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
     FL_HIP(ie);
     g_pva.key = key;
   }
-  FL_HIP(hipGraphLaunch(g_pva.exec, st));
+  FL_HIP(hipMemsetAsync(g_pva.ctr, 0, sizeof(int), st));
+  for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(g_pva.exec, st));
   return kOk;
 }
 

@@ -18,6 +18,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from flamed.utils.conv import GemmConv1d
+
 
 class StyleAdaptiveLayerNorm(nn.Module):
     """LN(x)·γ + β with (γ, β) = Linear(mean_T(condition)) (reference transformer.py:13-32)."""
@@ -62,7 +64,7 @@ class TransformerFFNLayer(nn.Module):
         self.conv_filter_size = conv_filter_size
         self.conv_kernel_size = conv_kernel_size
         self.encoder_dropout = encoder_dropout
-        self.ffn_1 = nn.Conv1d(encoder_hidden, conv_filter_size, conv_kernel_size, padding=conv_kernel_size // 2)
+        self.ffn_1 = GemmConv1d(encoder_hidden, conv_filter_size, conv_kernel_size, padding=conv_kernel_size // 2)
         self.ffn_2 = nn.Linear(conv_filter_size, encoder_hidden)
         with torch.no_grad():
             self.ffn_1.weight.normal_(0.0, 0.02)

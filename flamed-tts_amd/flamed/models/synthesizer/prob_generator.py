@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from flamed import _native as nat
+from flamed.utils.conv import GemmConv1d
 
 
 def modulate(x, shift, scale):
@@ -39,7 +40,7 @@ class Block1D(nn.Module):
 
     def __init__(self, dim, dim_out, groups=8):
         super().__init__()
-        self.block = nn.Sequential(nn.Conv1d(dim, dim_out, 1), nn.GroupNorm(groups, dim_out), nn.Mish())
+        self.block = nn.Sequential(GemmConv1d(dim, dim_out, 1), nn.GroupNorm(groups, dim_out), nn.Mish())
 
     def forward(self, x, mask):
         return self.block(x * mask) * mask
@@ -68,7 +69,7 @@ class ConditionDownSampler(nn.Module):
         ch = in_channel
         for _ in range(n_stages):
             self.resblocks.append(ResnetBlock1D(dim=ch, dim_out=ch))
-            self.downblocks.append(nn.Sequential(nn.Conv1d(ch, ch // 2, 1), nn.GroupNorm(n_groups, ch // 2), nn.ReLU()))
+            self.downblocks.append(nn.Sequential(GemmConv1d(ch, ch // 2, 1), nn.GroupNorm(n_groups, ch // 2), nn.ReLU()))
             ch //= 2
         self.proj_out = nn.Sequential(nn.Linear(ch, out_channel), nn.ReLU())
 

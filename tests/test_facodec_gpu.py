@@ -57,8 +57,9 @@ def _run(dec, lat, spk):
 def test_state_dict_schema_and_extra_keys(dec_f32):
     d, sd = dec_f32
     assert set(d.state_dict().keys()) <= set(sd.keys())
-    assert all(k.split(".")[0] in ("model", "timbre_linear") for k in d.state_dict())
+    assert all(k.split(".")[0] in ("model", "timbre_linear", "timbre_encoder", "quantizer") for k in d.state_dict())
     assert len(d.unused_state) == len(sd) - len(d.state_dict())
+    assert all(k.split(".")[0].endswith("_predictor") for k in d.unused_state)
 
 
 @pytest.mark.parametrize("case", ["1", "2"])

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from _common import golden, t32, rel_l2
-from _flamed_common import build_flamed
+from _flamed_common import build_flamed, build_codec_encoder
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -29,3 +29,29 @@ def test_sample_batch_gpu(dtype, lat_tol):
     if dtype == "f32":
         assert rel_l2(out["wav"].cpu(), g["sb_wav"]) < 2e-3
     assert out["time"] > 0
+
+
+def test_prompt_encode_gpu():
+    """FaCodec encoder + RVQ codes + timbre on the GPU vs the reference fixture (codes bit-exact; the
+    fixture's smallest top-2 code-distance gap is recorded as vq_gap_min)."""
+    _, dec = build_flamed(DEV, "f32")
+    enc = build_codec_encoder(DEV)
+    g = golden("facodec_encode")
+    with torch.inference_mode():
+        z = enc(t32(g["wav"]).to(DEV))
+        _, codes, _, _, spk = dec(t32(g["enc_out"]).to(DEV), eval_vq=False, vq=True)
+    assert rel_l2(z.cpu(), g["enc_out"]) < 1e-4
+    assert np.array_equal(codes.cpu().numpy(), g["codes"])
+    assert rel_l2(spk.cpu(), g["spk"]) < 1e-4
+
+
+def test_sample_raw_prompt_gpu():
+    """Flamed.sample with a raw prompt (encode -> prior/PVA -> denoiser -> decode) on the GPU."""
+    m, dec = build_flamed(DEV, "f32")
+    enc = build_codec_encoder(DEV)
+    g = golden("flamed_sample_raw")
+    torch.manual_seed(int(g["rng_seed"]))
+    res = m.sample(phonemes=t32(g["phonemes"]), prompt_raw=g["prompt"], sr=16000, codec_encoder=enc,
+                   codec_decoder=dec, temp_durgen=0.3, temp_denoiser=0.3, nsteps_durgen=4, nsteps_denoiser=4)
+    assert res["wav"].shape == g["wav"].shape
+    assert rel_l2(res["wav"], g["wav"]) < 2e-3

@@ -117,3 +117,19 @@ def test_prompt_encode_cpu_path():
     assert rel_l2(qsum, g["qsum"]) < TOL and rel_l2(torch.stack(qbuf), g["qbuf"]) < TOL
     assert losses.shape == (6,) and float(losses.abs().sum()) == 0.0
     assert rel_l2(emb, g["qsum"]) < 1e-4  # codes -> embeddings reproduces the quantized sum
+
+
+def test_conv1d_gemm_matches_conv1d():
+    """The GEMM form used for torch-side convs on ROCm devices (flamed/utils/conv.py) == F.conv1d."""
+    from flamed.utils.conv import conv1d_gemm
+    g = torch.Generator().manual_seed(0)
+    for (B, Cin, Cout, T, k, s, p, d, bias) in [(2, 8, 16, 37, 3, 1, 1, 1, True), (1, 4, 6, 20, 1, 1, 0, 1, True),
+                                                (3, 5, 7, 41, 7, 1, 9, 3, False), (2, 6, 4, 50, 4, 2, 1, 1, True),
+                                                (1, 3, 5, 33, 10, 5, 3, 1, True)]:
+        x = torch.randn(B, Cin, T, generator=g)
+        w = torch.randn(Cout, Cin, k, generator=g)
+        b = torch.randn(Cout, generator=g) if bias else None
+        ref = torch.nn.functional.conv1d(x, w, b, stride=s, padding=p, dilation=d)
+        out = conv1d_gemm(x, w, b, s, p, d)
+        assert out.shape == ref.shape
+        assert torch.allclose(out, ref, atol=1e-5, rtol=1e-5)
