@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--kernel-iters", type=int, default=10, help="eager steps timed in-context per kernel class")
+    ap.add_argument("--splitk-target", type=int, default=None, help="flamed_tune splitk_target (1 disables split-K)")
+    ap.add_argument("--splitk-max", type=int, default=None, help="flamed_tune splitk_max")
+    ap.add_argument("--dup-class", type=int, default=None, help="ablation: flamed_tune dup_class")
     return ap.parse_args()
 
 
@@ -97,6 +100,11 @@ def main():
     from flamed.models.synthesizer.prob_generator import ProbGenerator
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
+
+    for key in ("splitk_target", "splitk_max", "dup_class"):
+        v = getattr(args, key)
+        if v is not None:
+            nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")
 
     cfg = yaml.safe_load(open(os.path.join(REPO, "flamed-tts_amd", "configs", "prob.yaml")))
     pg = ProbGenerator(cfg).eval()

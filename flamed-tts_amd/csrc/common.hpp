@@ -103,4 +103,22 @@ template <typename DT> __device__ __forceinline__ void store_val(DT* p, float v)
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// ---- phase stamps (diagnostic build only: -DFL_STAMPS, libflamed_hip_stamps.so) ----
+// Thread 0 of every block writes s_memtime at numbered checkpoints into fl_stamp_buf[block][8]
+// when the host has pointed fl_stamp_buf at a buffer (one chosen kernel class per step).
+#ifdef FL_STAMPS
+static __device__ unsigned long long* fl_stamp_buf = nullptr;  // per translation unit (no -fgpu-rdc)
+__device__ __forceinline__ void fl_stamp(int i) {
+  if (threadIdx.x == 0 && fl_stamp_buf) {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    const size_t blk = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+    fl_stamp_buf[blk * 8 + i] = t;
+  }
+}
+#define FL_STAMP(i) ::fl::fl_stamp(i)
+#else
+#define FL_STAMP(i) ((void)0)
+#endif
+
 }  // namespace fl

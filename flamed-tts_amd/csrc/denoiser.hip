@@ -13,9 +13,29 @@
 #include "flamed_hip.h"
 #include "gemm.hpp"
 
+#include <string>
 #include <vector>
 
 namespace fl {
+
+thread_local SplitCtx* g_split = nullptr;
+// Tuning knobs (flamed_tune): split-K workgroup target and maximum split for small-M GEMMs.
+static int g_tune_split_target = 1;  // split-K off by default: measured slower at B=1 (profiles/r01_splitk_sweep.txt)
+static int g_tune_split_max = 4;
+// Ablation (flamed_tune "dup_class"): launch every kernel of this class twice per step, so the solve
+// time delta is the class's in-graph cost.  -1 = off.
+static int g_dup_class = -1;
+// Diagnostic stamps (FL_STAMPS builds): kernel class whose launches point fl_stamp_buf at g_stamp_dev.
+static int g_stamp_class = -1;
+static unsigned long long* g_stamp_dev = nullptr;
+#ifdef FL_STAMPS
+static void stamp_select(int cls, hipStream_t st) {
+  unsigned long long* p = (cls == g_stamp_class) ? g_stamp_dev : nullptr;
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(fl_stamp_buf), &p, sizeof(p), 0, hipMemcpyHostToDevice, st);
+}
+#else
+static void stamp_select(int, hipStream_t) {}
+#endif
 
 // ------------------------------ denoiser loaders / epilogues ------------------------------
 
@@ -59,27 +79,54 @@ struct LoadLNMod {
   static constexpr int kVec = 4;  // 2 slots x (alpha, beta)
   struct Raw { float v[EPC]; };
   static constexpr int stat_rows(int BM) { return BM; }
+  // Staging loads (float4, two passes kept in registers) are issued before the row statistics' loads
+  // so both groups are in flight together.
   __device__ bool prologue_v(int bm, int BM, int M, int K, float* st, float* vec) const {
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int r0 = bm / mod.div, r1 = last / mod.div;
+    const bool ok = r1 - r0 <= 1;
+    const int K4 = K / 4, n4 = ok ? (r1 - r0 + 1) * K4 : 0;
+    const ModRef md = mod.at();
+    constexpr int P = 2;
+    float4 sc[P], sh[P], w[P], b[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int q = threadIdx.x + p * blockDim.x;
+      if (q < n4) {
+        const int slot = q / K4, k = (q - slot * K4) * 4;
+        const size_t mo = (size_t)(r0 + slot) * md.ms + k;
+        sc[p] = ld4(md.sc + mo);
+        sh[p] = ld4(md.sh + mo);
+        w[p] = AFF ? ld4(lnw + k) : make_float4(1.f, 1.f, 1.f, 1.f);
+        b[p] = AFF ? ld4(lnb + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
     for (int r = threadIdx.x; r < BM; r += blockDim.x) {
       int m = bm + r;
       m = m < M ? m : M - 1;
       row_stats_from_partials(S, m, NT, tw, eps, st[2 * r], st[2 * r + 1]);
     }
-    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
-    const int r0 = bm / mod.div, r1 = last / mod.div;
-    if (r1 - r0 > 1) return false;
-    const ModRef md = mod.at();
-    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * K; idx += blockDim.x) {
-      int slot = idx / K, k = idx - slot * K;
-      size_t mo = (size_t)(r0 + slot) * md.ms + k;
-      float sc1 = 1.0f + md.sc[mo];
-      float w = AFF ? lnw[k] : 1.0f, b = AFF ? lnb[k] : 0.0f;
-      vec[(2 * slot) * K + k] = w * sc1;
-      vec[(2 * slot + 1) * K + k] = b * sc1 + md.sh[mo];
+    auto put = [&](int q, float4 c, float4 h, float4 ww, float4 bb) {
+      const int slot = q / K4, k = (q - slot * K4) * 4;
+      const float4 s1 = make_float4(1.f + c.x, 1.f + c.y, 1.f + c.z, 1.f + c.w);
+      *reinterpret_cast<float4*>(vec + (size_t)(2 * slot) * K + k) = make_float4(ww.x * s1.x, ww.y * s1.y, ww.z * s1.z, ww.w * s1.w);
+      *reinterpret_cast<float4*>(vec + (size_t)(2 * slot + 1) * K + k) =
+          make_float4(bb.x * s1.x + h.x, bb.y * s1.y + h.y, bb.z * s1.z + h.z, bb.w * s1.w + h.w);
+    };
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int q = threadIdx.x + p * blockDim.x;
+      if (q < n4) put(q, sc[p], sh[p], w[p], b[p]);
     }
-    return true;
+    for (int q = threadIdx.x + P * blockDim.x; q < n4; q += blockDim.x) {  // K > 2 * 4 * blockDim / slots
+      const int slot = q / K4, k = (q - slot * K4) * 4;
+      const size_t mo = (size_t)(r0 + slot) * md.ms + k;
+      put(q, ld4(md.sc + mo), ld4(md.sh + mo), AFF ? ld4(lnw + k) : make_float4(1.f, 1.f, 1.f, 1.f),
+          AFF ? ld4(lnb + k) : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    return ok;
   }
-  __device__ Raw issue_v(int m, int k, bool) const {
+  __device__ Raw issue_v(int m, int k) const {
     Raw r;
     const float* px = x + (size_t)m * ld + k;
 #pragma unroll
@@ -148,33 +195,54 @@ struct EpiConvNeXtResid {
   float* __restrict__ Sout;
   int NTout;
   static constexpr bool kRowStats = true;
+  static constexpr bool kPre = true;  // X[m][n] prefetched before the main loop
   static constexpr int kEVec = 8;
   static constexpr int stat_rows(int BM) { return BM; }
+  __device__ float pre(int m, int n) const { return X[(size_t)m * ld + n]; }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int r0 = bm / mod.div, r1 = last / mod.div;
+    const bool ok = r1 - r0 <= 1;
+    const int cnt = ok ? (r1 - r0 + 1) * BN : 0;
+    const long long so = mod.so.get();
+    const ModRef md = mod.at();
+    // this thread's staging values (one pass: cnt <= 2 * BN <= blockDim) load before the row statistics
+    const int idx = threadIdx.x;
+    float sc1 = 0.f, shv = 0.f, gv = 0.f, w = 1.f, b = 0.f, b3v = 0.f;
+    int slot = 0, c = 0;
+    if (idx < cnt) {
+      slot = idx / BN; c = idx - slot * BN;
+      const int n = bn + c;
+      const size_t mo = (size_t)(r0 + slot) * md.ms + n;
+      sc1 = 1.0f + md.sc[mo];
+      shv = md.sh[mo];
+      gv = gate[so + mo];
+      if (AFF) { w = lnw[n]; b = lnb[n]; }
+      b3v = b3[n];
+    }
     for (int r = threadIdx.x; r < BM; r += blockDim.x) {
       int m = bm + r;
       m = m < M ? m : M - 1;
       row_stats_from_partials(Sin, m, NTin, twin, eps, st[2 * r], st[2 * r + 1]);
     }
-    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
-    const int r0 = bm / mod.div, r1 = last / mod.div;
-    if (r1 - r0 > 1) return false;
-    const long long so = mod.so.get();
-    const ModRef md = mod.at();
-    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {
-      int slot = idx / BN, c = idx - slot * BN, n = bn + c;
-      size_t mo = (size_t)(r0 + slot) * md.ms + n;
-      float sc1 = 1.0f + md.sc[mo];
-      float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
+    if (idx < cnt) {
       vec[c * 8 + slot * 3 + 0] = w * sc1;
-      vec[c * 8 + slot * 3 + 1] = b * sc1 + md.sh[mo];
-      vec[c * 8 + slot * 3 + 2] = gate[so + mo];
-      if (slot == 0) vec[c * 8 + 6] = b3[n];
+      vec[c * 8 + slot * 3 + 1] = b * sc1 + shv;
+      vec[c * 8 + slot * 3 + 2] = gv;
+      if (slot == 0) vec[c * 8 + 6] = b3v;
     }
-    return true;
+    for (int q = idx + blockDim.x; q < cnt; q += blockDim.x) {  // BN > blockDim / 2 (not used by the tile configs)
+      const int sl = q / BN, cc = q - sl * BN, n = bn + cc;
+      const size_t mo = (size_t)(r0 + sl) * md.ms + n;
+      const float s1 = 1.0f + md.sc[mo];
+      vec[cc * 8 + sl * 3 + 0] = (AFF ? lnw[n] : 1.0f) * s1;
+      vec[cc * 8 + sl * 3 + 1] = (AFF ? lnb[n] : 0.0f) * s1 + md.sh[mo];
+      vec[cc * 8 + sl * 3 + 2] = gate[so + mo];
+      if (sl == 0) vec[cc * 8 + 6] = b3[n];
+    }
+    return ok;
   }
-  __device__ float value_v(int m, int n, float acc, const float* st, const float* vec, bool use, int bm, int bn) const {
-    float x = X[(size_t)m * ld + n];
+  __device__ float value_v(int m, int n, float acc, const float* st, const float* vec, bool use, int bm, int bn, float x) const {
     float xh = (x - st[2 * (m - bm)]) * st[2 * (m - bm) + 1];
     if (use) {
       const float* v = vec + (n - bn) * 8 + (m / mod.div - bm / mod.div) * 3;
@@ -205,8 +273,10 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
   int NTout;
   StepOff so;
   static constexpr bool kRowStats = true;
+  static constexpr bool kPre = true;  // X[m][n] prefetched before the main loop
   static constexpr int kEVec = 4;
   static constexpr int stat_rows(int) { return 0; }
+  __device__ float pre(int m, int n) const { return X[(size_t)m * ld + n]; }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float*, float* vec) const {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / div, r1 = last / div;
@@ -219,8 +289,7 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
     }
     return true;
   }
-  __device__ float value_v(int m, int n, float acc, const float*, const float* vec, bool use, int bm, int bn) const {
-    float x = X[(size_t)m * ld + n];
+  __device__ float value_v(int m, int n, float acc, const float*, const float* vec, bool use, int bm, int bn, float x) const {
     if (use) {
       const float* v = vec + (n - bn) * 4;
       return x + v[m / div - bm / div] * (acc + v[2]);
@@ -263,57 +332,81 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
                                                            int NT, int tw, float eps_ln, ModRef mod,
                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                            const float* __restrict__ dww, const float* __restrict__ dwb,
-                                                           float* __restrict__ D, float* __restrict__ GP, int T, int TS) {
+                                                           float* __restrict__ D, float* __restrict__ GP, int T, int TS,
+                                                           int* __restrict__ gcnt, float* __restrict__ GNS) {
   constexpr int HALO = KS / 2, SR = kDwTC + 2 * HALO, RG = 256 / kDwCG, RPT = kDwTC / RG, WIN = RPT + KS - 1;
+  constexpr int C4 = kDwCG / 4;                      // float4 chunks per staged row
+  constexpr int NX = (SR * C4 + 255) / 256;          // float4 loads per thread for the X tile
+  FL_STAMP(0);
   __shared__ float hs[SR * kDwCG];
   __shared__ float rs[SR * 2];
-  __shared__ float red[RG * kDwCG * 3];
+  __shared__ float red[RG * kDwCG * 3 + 1];  // + "last arriver" flag
   __shared__ float va[kDwCG], vb[kDwCG];
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * kDwCG, ts = blockIdx.y, b = blockIdx.z;
   const int t0 = ts * kDwTC;
+  const int cl = tid % kDwCG, rg = tid / kDwCG, c = c0 + cl;
   mod = mod.at();
+  // every independent global load is issued up front: X tile (float4), conv taps, LN stats, alpha/beta
+  float4 xv[NX];
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    const int q = tid + j * 256;
+    const int r = q / C4, c4 = q - r * C4;
+    const int t = t0 - HALO + r;
+    xv[j] = (q < SR * C4 && t >= 0 && t < T) ? ld4(X + ((size_t)b * T + t) * H + c0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float w[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) w[j] = dww[(size_t)c * KS + j];
+  const float bias = dwb[c];
   // one modulation row for the whole utterance (sampling path): stage alpha/beta once
   const bool uni = ((size_t)b * T) / mod.div == ((size_t)b * T + T - 1) / mod.div;
   if (uni && tid < kDwCG) {
     size_t mo = (((size_t)b * T) / mod.div) * mod.ms + c0 + tid;
     float sc1 = 1.0f + mod.sc[mo];
-    float w = AFF ? lnw[c0 + tid] : 1.0f, bb = AFF ? lnb[c0 + tid] : 0.0f;
-    va[tid] = w * sc1;
-    vb[tid] = bb * sc1 + mod.sh[mo];
+    float lw = AFF ? lnw[c0 + tid] : 1.0f, lb = AFF ? lnb[c0 + tid] : 0.0f;
+    va[tid] = lw * sc1;
+    vb[tid] = lb * sc1 + mod.sh[mo];
   }
   if (tid < SR) {
     int t = t0 - HALO + tid;
     if (t >= 0 && t < T) row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rs[2 * tid], rs[2 * tid + 1]);
   }
   __syncthreads();
-  for (int idx = tid; idx < SR * kDwCG; idx += 256) {
-    int r = idx / kDwCG, cc = idx - r * kDwCG;
-    int t = t0 - HALO + r;
-    float v = 0.f;
+  FL_STAMP(1);
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    const int q = tid + j * 256;
+    if (q >= SR * C4) break;
+    const int r = q / C4, c4 = q - r * C4;
+    const int t = t0 - HALO + r;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
     if (t >= 0 && t < T) {
-      size_t m = (size_t)b * T + t;
-      float xh = (X[m * H + c0 + cc] - rs[2 * r]) * rs[2 * r + 1];
-      if (uni) {
-        v = xh * va[cc] + vb[cc];
-      } else {
-        size_t mo = (m / mod.div) * mod.ms + c0 + cc;
-        float sc1 = 1.0f + mod.sc[mo];
-        float w = AFF ? lnw[c0 + cc] : 1.0f, bb = AFF ? lnb[c0 + cc] : 0.0f;
-        v = xh * (w * sc1) + (bb * sc1 + mod.sh[mo]);
+      const float xs[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
+      const float mean = rs[2 * r], rstd = rs[2 * r + 1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int cc = 4 * c4 + e;
+        const float xh = (xs[e] - mean) * rstd;
+        if (uni) {
+          o[e] = xh * va[cc] + vb[cc];
+        } else {
+          size_t m = (size_t)b * T + t;
+          size_t mo = (m / mod.div) * mod.ms + c0 + cc;
+          float sc1 = 1.0f + mod.sc[mo];
+          float lw = AFF ? lnw[c0 + cc] : 1.0f, lb = AFF ? lnb[c0 + cc] : 0.0f;
+          o[e] = xh * (lw * sc1) + (lb * sc1 + mod.sh[mo]);
+        }
       }
     }
-    hs[idx] = v;
+    *reinterpret_cast<float4*>(hs + r * kDwCG + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
-  const int cl = tid % kDwCG, rg = tid / kDwCG, c = c0 + cl;
-  float w[KS];
-#pragma unroll
-  for (int j = 0; j < KS; ++j) w[j] = dww[(size_t)c * KS + j];
+  FL_STAMP(2);
   float win[WIN];
 #pragma unroll
   for (int j = 0; j < WIN; ++j) win[j] = hs[(rg * RPT + j) * kDwCG + cl];
-  const float bias = dwb[c];
   float vals[RPT];
   float cn = 0.f, cs = 0.f;
 #pragma unroll
@@ -339,6 +432,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   red[(rg * kDwCG + cl) * 3 + 0] = cn;
   red[(rg * kDwCG + cl) * 3 + 1] = cm;
   red[(rg * kDwCG + cl) * 3 + 2] = c2;
+  FL_STAMP(3);
   __syncthreads();
   if (tid < kDwCG) {
     float n = 0.f, mu = 0.f, m2 = 0.f;
@@ -347,6 +441,43 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
     float* o = GP + (((size_t)b * TS + ts) * H + c0 + tid) * 3;
     o[0] = n; o[1] = mu; o[2] = m2;
   }
+  FL_STAMP(4);
+  if (!gcnt) return;
+  // GroupNorm finalize fused: the last T-chunk block of this (utterance, channel group) combines the
+  // TS chunk partials in chunk order (as gn_finalize_kernel) and writes GNS = (mean, rstd).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(red + RG * kDwCG * 3);
+  if (tid == 0) {
+    int* cnt = gcnt + (size_t)b * gridDim.x + blockIdx.x;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == TS - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *cnt = 0;
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag || tid >= kDwCG) return;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int t0c = 0; t0c < TS; t0c += 8) {
+    float q[8][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float* p = GP + (((size_t)b * TS + (t0c + i < TS ? t0c + i : TS - 1)) * H + c0 + tid) * 3;
+      q[i][0] = p[0]; q[i][1] = p[1]; q[i][2] = p[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (t0c + i < TS) chan_combine(n, mu, m2, q[i][0], q[i][1], q[i][2]);
+  }
+  GNS[((size_t)b * H + c0 + tid) * 2] = mu;
+  GNS[((size_t)b * H + c0 + tid) * 2 + 1] = 1.0f / sqrtf(m2 / (float)T + 1e-5f);
+  FL_STAMP(5);
 }
 
 // GroupNorm(H,H) statistics over all T frames of each (utterance, channel): GNS[b][c] = (mean, rstd).
@@ -371,17 +502,19 @@ __global__ void gn_finalize_kernel(const float* __restrict__ GP, float* __restri
 }
 
 template <bool AFF>
+// part 1: conv + partials (+ GroupNorm finalize fused in when gcnt is given); part 2: standalone
+// finalize (used only without counters).
 static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw,
                                const float* lnb, const float* dww, const float* dwb, float* D, float* GP, float* GNS,
-                               int B, int T, hipStream_t st, int part) {
+                               int B, int T, hipStream_t st, int part, int* gcnt) {
   FL_REQUIRE(H % kDwCG == 0 && H % 256 == 0, "dwconv: H=%d must be a multiple of 256", H);
   const int TS = (T + kDwTC - 1) / kDwTC;
   if (part != 2) {
     hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
-                       mod, lnw, lnb, dww, dwb, D, GP, T, TS);
+                       mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     FL_LAUNCH_CHECK();
   }
-  if (part != 1) {
+  if (part != 1 && !gcnt) {
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(H / 256, B), dim3(256), 0, st, GP, GNS, H, T, TS, 1e-5f);
     FL_LAUNCH_CHECK();
   }
@@ -405,17 +538,41 @@ struct LoadGN {
   __device__ bool prologue_v(int bm, int BM, int M, int K, float*, float* vec) const {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int b0 = bm / T, b1 = last / T;
-    if (b1 - b0 > 1) return false;
-    for (int idx = threadIdx.x; idx < (b1 - b0 + 1) * K; idx += blockDim.x) {
-      int slot = idx / K, k = idx - slot * K;
-      const float* g = gns + ((size_t)(b0 + slot) * H + k) * 2;
-      vec[(2 * slot) * K + k] = g[0];
-      vec[(2 * slot + 1) * K + k] = g[1] * gnw[k];
-      if (slot == 0) vec[4 * K + k] = gnb[k];
+    const bool ok = b1 - b0 <= 1;
+    const int K4 = K / 4, n4 = ok ? (b1 - b0 + 1) * K4 : 0;
+    constexpr int P = 2;  // passes whose loads are all issued before any use
+    float4 g0[P], g1[P], w[P], bb[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int q = threadIdx.x + p * blockDim.x;
+      if (q < n4) {
+        const int slot = q / K4, k = (q - slot * K4) * 4;
+        const float* g = gns + ((size_t)(b0 + slot) * H + k) * 2;
+        g0[p] = ld4(g);
+        g1[p] = ld4(g + 4);
+        w[p] = ld4(gnw + k);
+        bb[p] = ld4(gnb + k);
+      }
     }
-    return true;
+    auto put = [&](int q, float4 a, float4 c, float4 ww, float4 b) {
+      const int slot = q / K4, k = (q - slot * K4) * 4;
+      *reinterpret_cast<float4*>(vec + (size_t)(2 * slot) * K + k) = make_float4(a.x, a.z, c.x, c.z);
+      *reinterpret_cast<float4*>(vec + (size_t)(2 * slot + 1) * K + k) = make_float4(a.y * ww.x, a.w * ww.y, c.y * ww.z, c.w * ww.w);
+      if (slot == 0) *reinterpret_cast<float4*>(vec + (size_t)4 * K + k) = b;
+    };
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int q = threadIdx.x + p * blockDim.x;
+      if (q < n4) put(q, g0[p], g1[p], w[p], bb[p]);
+    }
+    for (int q = threadIdx.x + P * blockDim.x; q < n4; q += blockDim.x) {
+      const int slot = q / K4, k = (q - slot * K4) * 4;
+      const float* g = gns + ((size_t)(b0 + slot) * H + k) * 2;
+      put(q, ld4(g), ld4(g + 4), ld4(gnw + k), ld4(gnb + k));
+    }
+    return ok;
   }
-  __device__ Raw issue_v(int m, int k, bool) const {
+  __device__ Raw issue_v(int m, int k) const {
     Raw r;
     const float* pd = D + (size_t)m * H + k;
 #pragma unroll
@@ -525,6 +682,10 @@ struct Den {
   int g_B = -1, g_T = -1, g_nfe = -1;
   const void *g_xt = nullptr, *g_mods = nullptr, *g_ws = nullptr;
   int* ctr = nullptr;  // device Euler step counter for graph replay
+  int* scnt = nullptr;  // split-K tile counters (zeroed at load; every launch leaves them zero)
+  static constexpr int kSplitCounters = 16384;
+  int* gcnt = nullptr;  // fused GroupNorm-finalize counters, one per (utterance, 64-channel group)
+  static constexpr int kGnCounters = 65536;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -538,24 +699,36 @@ struct DenWs {
   float* GP;   // GroupNorm chunk partials, B x TS x H x 3
   float* GNS;  // GroupNorm (mean, rstd), B x H x 2
   float* Y;    // conv_out tap-stacked GEMM output, M x 3C
+  float* SL;   // split-K slabs (small-M GEMMs), SLn floats
+  size_t SLn;
 };
+
+// split-K slab capacity: 32 x 64 tiles of the widest GEMM (max(H, 3C) columns) x 4 slices, small M only
+static size_t den_slab_floats(const Den* d, int B, int T) {
+  const size_t M = (size_t)B * T;
+  if (M >= 2048) return 0;
+  const size_t nmax = (size_t)(d->H > 3 * d->C ? d->H : 3 * d->C);
+  return ((M + 31) / 32) * (nmax / 64) * 4 * 32 * 64;
+}
 
 static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t M = (size_t)B * T;
   size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
   size_t NTmax = d->H / 64;
   size_t TS = (T + 63) / 64;
-  size_t sizes[8] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
-                     8 * (size_t)B * d->H, 12 * M * d->C};
+  const size_t sl = den_slab_floats(d, B, T);
+  size_t sizes[9] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
+                     8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl};
   size_t off = 0;
-  void* ptrs[8];
-  for (int i = 0; i < 8; ++i) {
+  void* ptrs[9];
+  for (int i = 0; i < 9; ++i) {
     ptrs[i] = base ? (char*)base + off : nullptr;
     off += align256(sizes[i]);
   }
   if (w) {
     w->X = (float*)ptrs[0]; w->S0 = (float*)ptrs[1]; w->S1 = (float*)ptrs[2]; w->D = (float*)ptrs[3];
     w->U = ptrs[4]; w->GP = (float*)ptrs[5]; w->GNS = (float*)ptrs[6]; w->Y = (float*)ptrs[7];
+    w->SL = (float*)ptrs[8]; w->SLn = sl;
   }
   return off;
 }
@@ -586,6 +759,8 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
   if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
   if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
   if (d->ctr) (void)hipFree(d->ctr);
+  if (d->scnt) (void)hipFree(d->scnt);
+  if (d->gcnt) (void)hipFree(d->gcnt);
   if (d->dev) (void)hipFree(d->dev);
   delete d;
   return kOk;
@@ -674,6 +849,10 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   }
 #undef TRY
   (void)KS;
+  if (!d->scnt) FL_HIP(hipMalloc(&d->scnt, sizeof(int) * Den::kSplitCounters));
+  FL_HIP(hipMemsetAsync(d->scnt, 0, sizeof(int) * Den::kSplitCounters, st));
+  if (!d->gcnt) FL_HIP(hipMalloc(&d->gcnt, sizeof(int) * Den::kGnCounters));
+  FL_HIP(hipMemsetAsync(d->gcnt, 0, sizeof(int) * Den::kGnCounters, st));
   if (d->gexec) { (void)hipGraphExecDestroy(d->gexec); d->gexec = nullptr; }
   return kOk;
 }
@@ -745,21 +924,27 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
                          const DenWs& w, int* ctr, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const StepOff so{ctr, (long long)B * MS};
+  SplitCtx sctx;
+  sctx.slab = w.SL; sctx.slab_floats = w.SLn; sctx.cnt = d->scnt; sctx.cnt_n = Den::kSplitCounters;
+  sctx.target = g_tune_split_target; sctx.max_split = g_tune_split_max;
+  SplitScope split_scope(w.SLn ? &sctx : nullptr);
+  // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
+  int* gcnt = (d->gcnt && (size_t)B * (H / kDwCG) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;
   const GemmCfg cfg = pick_cfg(M);
   const int BN = cfg_bn(cfg);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
-#define K_(cls, x) do { TRY(x); kt_mark(cls, st); } while (0)
+#define K_(cls, x) do { if (g_stamp_class >= 0) stamp_select(cls, st); TRY(x); if (g_dup_class == (cls)) TRY(x); kt_mark(cls, st); } while (0)
   K_(0, (launch_gemm_auto<DT>(cfg, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div, so};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
-    K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
-    K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
+    K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
+    K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
     K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
                                         EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
     K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
@@ -774,8 +959,8 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   ModRef mc{mf, mf + H, MS, mod_div, so};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div, so};
   const DenBlockW& F = d->fin;
-  K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1)));
-  K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2)));
+  K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
+  K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
   K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                       EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
@@ -786,6 +971,10 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     size_t n = (size_t)M * C;
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, ctr);
     FL_LAUNCH_CHECK();
+    if (g_dup_class == 8) {  // duplicate without a second counter increment
+      hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, nullptr);
+      FL_LAUNCH_CHECK();
+    }
     kt_mark(8, st);
   }
 #undef K_
@@ -883,6 +1072,28 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
 }  // extern "C"
 
 extern "C" {
+
+// Diagnostic: device buffer (blocks x 8 u64) that FL_STAMPS kernels of the selected class write into.
+FLAMED_API int flamed_stamp_buffer(void* buf) {
+  g_stamp_dev = reinterpret_cast<unsigned long long*>(buf);
+#ifdef FL_STAMPS
+  return kOk;
+#else
+  set_error("flamed_stamp_buffer: library built without FL_STAMPS");
+  return kBadArg;
+#endif
+}
+
+FLAMED_API int flamed_tune(const char* key, int value) {
+  FL_REQUIRE(key, "flamed_tune: null key");
+  const std::string k(key);
+  if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
+  if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "dup_class") { FL_REQUIRE(value >= -1 && value < FLAMED_DEN_KERNEL_CLASSES, "flamed_tune: dup_class in [-1, %d)", FLAMED_DEN_KERNEL_CLASSES); g_dup_class = value; return kOk; }
+  if (k == "splitk_max") { FL_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8 || value == 16, "flamed_tune: splitk_max must be a power of two <= 16"); g_tune_split_max = value; return kOk; }
+  set_error("flamed_tune: unknown key '%s'", key);
+  return kBadArg;
+}
 
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                        size_t ws_bytes, int iters, float* ms_out, hipStream_t st) {

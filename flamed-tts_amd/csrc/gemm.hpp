@@ -25,6 +25,11 @@ template <class T, class = void> struct kvec_of { static constexpr int value = 0
 template <class T> struct kvec_of<T, std::void_t<decltype(T::kVec)>> { static constexpr int value = T::kVec; };
 template <class T, class = void> struct kevec_of { static constexpr int value = 0; };
 template <class T> struct kevec_of<T, std::void_t<decltype(T::kEVec)>> { static constexpr int value = T::kEVec; };
+// Epilogues with kPre read one global value per output element (e.g. the residual X); the kernel
+// fetches it through ep.pre(m, n) before the main loop (small tiles) so its latency is hidden, and
+// passes it to value_v as the last argument.
+template <class T, class = void> struct kpre_of { static constexpr bool value = false; };
+template <class T> struct kpre_of<T, std::void_t<decltype(T::kPre)>> { static constexpr bool value = T::kPre; };
 
 template <int BM, int BN, int KCH, int NSTAGE, class AL, class EP>
 struct GemmSmem {
@@ -34,8 +39,20 @@ struct GemmSmem {
   static constexpr int e_stats = EP::stat_rows(BM) * 2 * 4;
   static constexpr int e_vec = kevec_of<EP>::value * BN * 4;
   static constexpr int red = BM * 2 * 4;
-  static constexpr int base = tiles > red ? tiles : red;
+  static constexpr int base = (tiles > red ? tiles : red) + 16;  // + 16 B: split-K "last arriver" flag
+  static constexpr int flag = base - 16;
   static constexpr int bytes = (base + a_stats + e_stats + e_vec + 15) / 16 * 16;  // + kVec*K*4 (runtime)
+};
+
+// Split-K over gridDim.z (small-M GEMMs, where one block's K chain is the latency).  Every slice
+// stores its fp32 partial tile as a slab in MFMA-fragment order, then takes a ticket on the tile's
+// counter (agent-scope release before, acquire after — cdna_hip_programming.md §5 "Projection GEMM
+// at M = 256" item 2); the last arriver sums all `n` slabs in slice order (deterministic), resets the
+// counter and runs the fused epilogue.  n == 1: no split.
+struct SplitK {
+  int n;
+  float* slab;  // tiles x n x BM x BN floats
+  int* cnt;     // tiles counters, zero between launches
 };
 
 // LayerNorm row statistics from producer partials: S[m][NT] = (tile mean, tile M2) over `tw` columns.
@@ -73,7 +90,7 @@ __device__ __forceinline__ int lds_off(int r, int c) {
 // NSTAGE = 3: LDS ring of 3, two register stages, loads issued two K-steps ahead (small-M latency).
 template <int BM, int BN, int KCH, int NSTAGE, typename DT, class AL, class EP>
 __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __restrict__ W, int ldw, EP ep,
-                                                             int M, int N, int K) {
+                                                             int M, int N, int K, SplitK sk) {
   using SM = GemmSmem<BM, BN, KCH, NSTAGE, AL, EP>;
   constexpr int EPC = DTraits<DT>::EPC;
   constexpr int BKE = KCH * EPC;
@@ -84,16 +101,18 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
   constexpr int TILE = (BM + BN) * SM::ROWB;
   static_assert(ACH >= 1 && BCH >= 1, "tile too small for 256 threads");
   static_assert(KCH == 8, "K-step is 128 B per row");
-  static_assert(NSTAGE == 2 || NSTAGE == 3, "2 or 3 stages");
+  static_assert(NSTAGE >= 2 && NSTAGE <= 7 && (NSTAGE <= 3 || (NSTAGE - 1) % 2 == 0), "2, 3, 5 or 7 stages");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* a_stats = reinterpret_cast<float*>(smem + SM::base);
+  int* s_flag = reinterpret_cast<int*>(smem + SM::flag);
   float* e_stats = a_stats + AL::stat_rows(BM) * 2;
   float* e_vec = e_stats + EP::stat_rows(BM) * 2;
   float* a_vec = e_vec + kevec_of<EP>::value * BN;
   constexpr bool AV = kvec_of<AL>::value > 0;
   constexpr bool EV = kevec_of<EP>::value > 0;
 
+  FL_STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -101,16 +120,12 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
   const int bn = blockIdx.x * BN;
   const int bm = blockIdx.y * BM;
 
-  bool a_uv = false, e_uv = false;
-  if constexpr (AV) a_uv = al.prologue_v(bm, BM, M, K, a_stats, a_vec);
-  else al.prologue(bm, BM, M, a_stats);
-  if constexpr (EV) e_uv = ep.prologue_v(bm, bn, BM, BN, M, e_stats, e_vec);
-  else ep.prologue(bm, BM, M, e_stats);
-  __syncthreads();
-
+  bool a_uv = false, e_uv = false;  // set by the prologue (per-column vectors staged in LDS)
   typename AL::Raw ra0[ACH], ra1[ACH];
   u32x4 rb0[BCH], rb1[BCH];
-  const int nsteps = K / BKE;
+  const int kslice = K / sk.n;
+  const int k0 = blockIdx.z * kslice;
+  const int nsteps = kslice / BKE;
 
   auto issue = [&](int s, typename AL::Raw (&ra)[ACH], u32x4 (&rb)[BCH]) __attribute__((always_inline)) {
 #pragma unroll
@@ -119,14 +134,14 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
       int r = c / KCH, kc = c % KCH;
       int m = bm + r;
       m = m < M ? m : M - 1;
-      if constexpr (AV) ra[j] = al.issue_v(m, s * BKE + kc * EPC, a_uv);
-      else ra[j] = al.issue(m, s * BKE + kc * EPC);
+      if constexpr (AV) ra[j] = al.issue_v(m, k0 + s * BKE + kc * EPC);
+      else ra[j] = al.issue(m, k0 + s * BKE + kc * EPC);
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
       int c = tid + j * kGemmThreads;
       int r = c / KCH, kc = c % KCH;
-      rb[j] = *reinterpret_cast<const u32x4*>(W + (size_t)(bn + r) * ldw + s * BKE + kc * EPC);
+      rb[j] = *reinterpret_cast<const u32x4*>(W + (size_t)(bn + r) * ldw + k0 + s * BKE + kc * EPC);
     }
   };
   auto commit = [&](int s, const typename AL::Raw (&ra)[ACH], const u32x4 (&rb)[BCH], char* t) __attribute__((always_inline)) {
@@ -137,9 +152,9 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
       int m = bm + r;
       m = m < M ? m : M - 1;
       if constexpr (AV)
-        *reinterpret_cast<u32x4*>(t + lds_off<KCH>(r, kc)) = al.template finish_v<DT>(ra[j], m, s * BKE + kc * EPC, a_stats, a_vec, a_uv, bm);
+        *reinterpret_cast<u32x4*>(t + lds_off<KCH>(r, kc)) = al.template finish_v<DT>(ra[j], m, k0 + s * BKE + kc * EPC, a_stats, a_vec, a_uv, bm);
       else
-        *reinterpret_cast<u32x4*>(t + lds_off<KCH>(r, kc)) = al.template finish<DT>(ra[j], m, s * BKE + kc * EPC, a_stats, bm);
+        *reinterpret_cast<u32x4*>(t + lds_off<KCH>(r, kc)) = al.template finish<DT>(ra[j], m, k0 + s * BKE + kc * EPC, a_stats, bm);
     }
     char* tb = t + BM * SM::ROWB;
 #pragma unroll
@@ -183,8 +198,37 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
     }
   };
 
+  // The first K-steps' operand loads go out before the fused prologue (LN statistics, per-column
+  // vectors, epilogue prefetch), whose own loads then overlap them.
+  constexpr bool PRE = kpre_of<EP>::value;
+  constexpr bool PRE_EARLY = PRE && FM * FN <= 4;
+  float pre[FM][FN][4];
+  auto fetch_pre = [&]() __attribute__((always_inline)) {
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int m = bm + wr * WTM + i * 16 + fq * 4 + r;
+            pre[i][j][r] = ep.pre(m < M ? m : M - 1, bn + wc * WTN + j * 16 + fr);
+          }
+    }
+  };
+  auto prologue = [&]() __attribute__((always_inline)) {
+    if constexpr (PRE_EARLY) fetch_pre();
+    if constexpr (AV) a_uv = al.prologue_v(bm, BM, M, K, a_stats, a_vec);
+    else al.prologue(bm, BM, M, a_stats);
+    if constexpr (EV) e_uv = ep.prologue_v(bm, bn, BM, BN, M, e_stats, e_vec);
+    else ep.prologue(bm, BM, M, e_stats);
+    __syncthreads();
+    FL_STAMP(1);
+  };
+
   if constexpr (NSTAGE == 2) {
     issue(0, ra0, rb0);
+    prologue();
     commit(0, ra0, rb0, smem);
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
@@ -195,11 +239,42 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
       if (s + 1 < nsteps) commit(s + 1, ra0, rb0, nxt);
       __syncthreads();
     }
+  } else if constexpr (NSTAGE >= 4) {
+    // Deep register prefetch for latency-bound (small-M) GEMMs whose weights stream from MALL/HBM:
+    // R = NSTAGE-1 register sets keep R K-steps of loads in flight; LDS is double-buffered.
+    // At step s: compute LDS[s&1]; commit step s+1 (register set (s+1)%R) into LDS[(s+1)&1]; reissue
+    // that set with step s+1+R (clamped, so the loads stay unconditional); barrier.
+    constexpr int R = NSTAGE - 1;
+    typename AL::Raw ra[R][ACH];
+    u32x4 rb[R][BCH];
+    const int last = nsteps - 1;
+#pragma unroll
+    for (int u = 0; u < R; ++u) issue(u < last ? u : last, ra[u], rb[u]);
+    prologue();
+    commit(0, ra[0], rb[0], smem);
+    issue(R < last ? R : last, ra[0], rb[0]);
+    __syncthreads();
+    for (int s0 = 0; s0 < nsteps; s0 += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int s = s0 + u;
+        if (s < nsteps) {
+          compute(smem + (u & 1) * TILE);
+          if (s + 1 < nsteps) {
+            commit(s + 1, ra[(u + 1) % R], rb[(u + 1) % R], smem + ((u + 1) & 1) * TILE);
+            const int nx = s + 1 + R;
+            issue(nx < last ? nx : last, ra[(u + 1) % R], rb[(u + 1) % R]);
+          }
+          __syncthreads();
+        }
+      }
+    }
   } else {
     // invariant at iteration s: LDS holds steps s, s+1; register set (s&1) holds loads of step s+2
     const int last = nsteps - 1;
     issue(0, ra0, rb0);
     issue(last < 1 ? last : 1, ra1, rb1);
+    prologue();
     commit(0, ra0, rb0, smem);
     if (nsteps > 1) commit(1, ra1, rb1, smem + TILE);
     issue(last < 2 ? last : 2, ra0, rb0);
@@ -225,7 +300,46 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
     }
   }
 
+  FL_STAMP(2);
+  // ---------------- split-K: slab hand-off, the last arriver reduces ----------------
+  if (sk.n > 1) {
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    float* slabs = sk.slab + (size_t)tile * sk.n * (BM * BN);
+    float* mine = slabs + (size_t)blockIdx.z * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(mine + ((i * FN + j) * kGemmThreads + tid) * 4) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(sk.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == sk.n - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sk.cnt[tile] = 0;  // ready for the next launch
+      }
+      *s_flag = last;
+    }
+    __syncthreads();
+    if (!*s_flag) return;  // block-uniform
+    // load every slab (own included: no per-element register/load select), then sum in slice order
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float* p = slabs + ((i * FN + j) * kGemmThreads + tid) * 4;
+        f32x4 sum = *reinterpret_cast<const f32x4*>(p);
+        for (int z = 1; z < sk.n; ++z) sum += *reinterpret_cast<const f32x4*>(p + (size_t)z * (BM * BN));
+        acc[i][j] = sum;
+      }
+  }
+
   // ---------------- epilogue (values overwrite the accumulators in place) ----------------
+  if constexpr (PRE && !PRE_EARLY) fetch_pre();
   auto& val = acc;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -236,10 +350,12 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
         int m = bm + wr * WTM + i * 16 + fq * 4 + r;
         int n = bn + wc * WTN + j * 16 + fr;
         int mc = m < M ? m : M - 1;
-        if constexpr (EV) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn);
+        if constexpr (PRE) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn, pre[i][j][r]);
+        else if constexpr (EV) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn);
         else val[i][j][r] = ep.value(mc, n, acc[i][j][r], e_stats, bm);
       }
 
+  FL_STAMP(3);
   if constexpr (EP::kRowStats) {
     float* red = reinterpret_cast<float*>(smem);  // tiles are dead after the final barrier
     float mean[FM][4];
@@ -298,6 +414,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
         int n = bn + wc * WTN + j * 16 + fr;
         if (m < M) ep.store(m, n, val[i][j][r]);
       }
+  FL_STAMP(4);
 }
 
 // ------------------------------ generic loaders ------------------------------
@@ -470,15 +587,46 @@ struct LoadConvPlain {
 // Host-side launcher.  Tile configurations (BM, BN, NSTAGE) are selected by the callers:
 //   small M  : 32 x 64, 3-stage ring (latency-bound at ~400 rows: more workgroups, deeper prefetch)
 //   mid M    : 64 x 64, 3-stage
-//   large M  : 128 x 128 (or 128 x 64 for narrow N), 3-stage (MFMA-bound; 1 wave/SIMD needs the
-//              2-step prefetch to cover load latency)
+//   large M  : 128 x 64, 3-stage (measured with flamed_probe_gemm at M = 25600, N = 1024: 461 TF at
+//              K = 1024 vs 358 TF for 128 x 128, whose 4x4 fragments per wave double the VGPRs)
+// Split-K context: a caller that owns slab memory and zeroed counters installs it (SplitScope) around
+// its launches; launch_gemm_cfg then splits bf16 GEMMs whose tile grid is small.
+struct SplitCtx {
+  float* slab = nullptr;
+  size_t slab_floats = 0;
+  int* cnt = nullptr;
+  int cnt_n = 0;
+  int target = 1;  // aim for about this many workgroups (tiles x splits); 1 = no split
+  int max_split = 4;
+};
+extern thread_local SplitCtx* g_split;
+struct SplitScope {
+  SplitCtx* prev;
+  explicit SplitScope(SplitCtx* c) : prev(g_split) { g_split = c; }
+  ~SplitScope() { g_split = prev; }
+};
+
+template <int BM, int BN, typename DT>
+inline SplitK choose_split(int M, int N, int K) {
+  constexpr int BKE = 8 * DTraits<DT>::EPC;
+  SplitK sk{1, nullptr, nullptr};
+  SplitCtx* c = g_split;
+  if (!c || DTraits<DT>::kCode != 1) return sk;  // fp32 parity mode keeps one exact FMA chain
+  const int tiles = (N / BN) * ((M + BM - 1) / BM);
+  int n = 1;
+  while (n * 2 <= c->max_split && tiles * n * 2 <= c->target && (K / BKE) % (n * 2) == 0 && K / (n * 2) >= 2 * BKE) n *= 2;
+  if (n == 1 || tiles > c->cnt_n || (size_t)tiles * n * BM * BN > c->slab_floats) return sk;
+  return SplitK{n, c->slab, c->cnt};
+}
+
 template <int BM, int BN, int NSTAGE, typename DT, class AL, class EP>
 inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   constexpr int KCH = 8;
   constexpr int BKE = KCH * DTraits<DT>::EPC;
   FL_REQUIRE(M > 0 && N % BN == 0 && K % BKE == 0, "gemm: unsupported shape M=%d N=%d K=%d (BN=%d BK=%d)", M, N, K, BN, BKE);
   using SM = GemmSmem<BM, BN, KCH, NSTAGE, AL, EP>;
-  dim3 grid(N / BN, (M + BM - 1) / BM);
+  const SplitK sk = choose_split<BM, BN, DT>(M, N, K);
+  dim3 grid(N / BN, (M + BM - 1) / BM, sk.n);
   auto kern = gemm_kernel<BM, BN, KCH, NSTAGE, DT, AL, EP>;
   const size_t bytes = SM::bytes + (size_t)kvec_of<AL>::value * K * 4;
   FL_REQUIRE(bytes <= 160 * 1024, "gemm: LDS request %zu B too large (K=%d)", bytes, K);
@@ -489,7 +637,7 @@ inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL(kern, grid, dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K);
+  hipLaunchKernelGGL(kern, grid, dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K, sk);
   FL_LAUNCH_CHECK();
   return kOk;
 }
@@ -498,13 +646,12 @@ inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int
 // width (0 = free choice).
 enum GemmCfg { kCfgSmall = 0, kCfgMid = 1, kCfgLarge = 2 };
 inline GemmCfg pick_cfg(int M) { return M < 2048 ? kCfgSmall : (M < 8192 ? kCfgMid : kCfgLarge); }
-inline int cfg_bn(GemmCfg c) { return c == kCfgLarge ? 128 : 64; }
+inline int cfg_bn(GemmCfg) { return 64; }
 
 template <typename DT, class AL, class EP>
 inline int launch_gemm_auto(GemmCfg c, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   if (c == kCfgSmall) return launch_gemm_cfg<32, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
   if (c == kCfgMid) return launch_gemm_cfg<64, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
-  if (N % 128 == 0) return launch_gemm_cfg<128, 128, 3, DT>(al, W, ldw, ep, M, N, K, st);
   return launch_gemm_cfg<128, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
 }
 

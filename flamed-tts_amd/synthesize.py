@@ -10,6 +10,10 @@ Same flags, modes, validation errors and RTF bookkeeping as the reference (synth
 On a ROCm device the denoiser solve, PVA flow + length regulator and FaCodec decoder run in the gfx950
 HIP library (flamed/_native); `--device cpu` runs the torch path.
 
+Multi-GPU: launched under torchrun (one process per GPU, `--master-addr 127.0.0.1`), each rank takes a
+round-robin shard of the prompts / metadata entries on cuda:LOCAL_RANK; there is no data-path
+collective, only the timing records are gathered for the RTF printed by rank 0.
+
 Additions (all optional; the reference's invocations behave the same):
   * `--codec-ckpt-dir DIR` — where ns3_facodec_{encoder,decoder}.bin live (reference: fixed path under
     flamed/models/facodec/checkpoints, :72-73);
@@ -34,6 +38,7 @@ if CURDIR not in sys.path:
 
 from flamed import Flamed  # noqa: E402
 from flamed.models.facodec import FACodecEncoder, FACodecDecoder  # noqa: E402
+from flamed.utils import dist as fdist  # noqa: E402
 from flamed.utils.audio import load_wav, write_wav  # noqa: E402
 
 SR = 16000
@@ -64,6 +69,9 @@ def resolve_device(device_str: str) -> torch.device:
     if device.type.startswith("cuda") and not torch.cuda.is_available():
         print("CUDA not available. Falling back to CPU.")
         return torch.device("cpu")
+    _, world, local = fdist.dist_env()
+    if device.type == "cuda" and world > 1:  # one GPU per rank
+        device = torch.device("cuda", local)
     return device
 
 
@@ -165,6 +173,14 @@ class RtfMeter:
         self.times.append(seconds)
         self.durations.append(n_samples / SR)
 
+    def gathered(self) -> "RtfMeter":
+        """A meter holding every rank's records (this one when not distributed)."""
+        g = RtfMeter()
+        for t, d in fdist.gather_records(list(zip(self.times, self.durations))):
+            g.times.append(t)
+            g.durations.append(d)
+        return g
+
     def rtf(self):
         if not self.times:
             return None
@@ -181,7 +197,8 @@ def synthesize_with_prompts(model: Flamed, codec_encoder, codec_decoder, text: s
     """One `Flamed.sample` per prompt (reference :194-217)."""
     os.makedirs(output_dir, exist_ok=True)
     meter = meter if meter is not None else RtfMeter()
-    for prompt_name in _progress(prompt_list, desc="Synthesizing prompts"):
+    rank, world, _ = fdist.dist_env()
+    for prompt_name in _progress(fdist.shard(prompt_list, rank, world), desc="Synthesizing prompts"):
         audio_prompt = load_audio(_resolve_prompt_path(prompt_dir, prompt_name))
         res = model.sample(text=text, prompt_raw=audio_prompt, sr=SR, codec_encoder=codec_encoder,
                            codec_decoder=codec_decoder, nsteps_durgen=nsteps_durgen, nsteps_denoiser=nsteps_denoiser,
@@ -216,6 +233,8 @@ def synthesize_with_metadata(model: Flamed, codec_encoder, codec_decoder, metada
             continue
         pending.append({"filename": filename, "prompt_path": _resolve_prompt_path(prompt_dir, prompt_filename),
                         "text": transcript, "out_path": out_path})
+    rank, world, _ = fdist.dist_env()
+    pending = fdist.shard(pending, rank, world)
     if not pending:
         return None
     for batch in _progress(chunked(pending, batch_size), total=math.ceil(len(pending) / batch_size),
@@ -294,6 +313,7 @@ def main(args: Optional[argparse.Namespace] = None):
             parser.error(str(exc))
         raise
     device = resolve_device(args.device)
+    distributed = fdist.init(device.type)
     codec_encoder, codec_decoder = get_codec(device, getattr(args, "codec_ckpt_dir", None))
     model = prepare_model(args.cfg_path, args.ckpt_path, device, args.weights_only)
     meter = RtfMeter()
@@ -305,12 +325,20 @@ def main(args: Optional[argparse.Namespace] = None):
                                        batch_size=args.batch_size, **common)
     else:
         rtf = synthesize_with_prompts(text=args.text, prompt_list=args.prompt_list, **common)
-    if rtf is not None:
-        print("=" * 20, "Avg RTF", "=" * 20)
-        print(">" * 5, "RTF:", round(rtf, 3))
-        print(">" * 5, "latent frames/s:", round(meter.frames_per_second(), 1))
+    if distributed:  # every rank's records; each rank's frames/s summed over the ranks' wall time
+        local_fps = meter.frames_per_second() if meter.times else 0.0
+        meter = meter.gathered()
+        rtf = meter.rtf()
+        total_fps = sum(fdist.gather_records([local_fps]))
     else:
-        print("No samples were generated.")
+        total_fps = meter.frames_per_second() if meter.times else 0.0
+    if fdist.dist_env()[0] == 0:
+        if rtf is not None:
+            print("=" * 20, "Avg RTF", "=" * 20)
+            print(">" * 5, "RTF:", round(rtf, 3))
+            print(">" * 5, "latent frames/s:", round(total_fps, 1))
+        else:
+            print("No samples were generated.")
     return rtf
 
 

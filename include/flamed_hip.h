@@ -91,13 +91,39 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
  * IN CONTEXT: `iters` full steps run eagerly with a HIP event recorded on `stream` after every
  * launch (the interval before a launch's end event = that kernel, incl. its dispatch gap).
  * Classes: 0 proj_in GEMM, 1 LN/mod+depthwise conv (+GN
- * partials), 2 GroupNorm finalize, 3 GN-apply+conv_2 GEMM+GELU, 4 conv_3 GEMM+gated residual,
+ * partials, + GroupNorm finalize by the last-arriving T-chunk), 2 standalone GroupNorm finalize (only
+ * when B x H/64 exceeds the handle's counters; otherwise ~0), 3 GN-apply+conv_2 GEMM+GELU, 4 conv_3 GEMM+gated residual,
  * 5 LN/mod+mlp.0 GEMM+SiLU, 6 mlp.2 GEMM+gated residual, 7 LN/mod+conv_out tap-stacked GEMM,
  * 8 conv_out tap combine.  ms_out must hold FLAMED_DEN_KERNEL_CLASSES floats.  Runs dt = 0 steps
  * (xt unchanged); clobbers the workspace. */
 enum { FLAMED_DEN_KERNEL_CLASSES = 9 };
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                        size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);
+
+/* Tuning knobs (process-wide; diagnostic / benchmarking).  Keys:
+ *   "splitk_target" — bf16 small-M GEMMs (M < 2048 rows) split K over workgroups until about this
+ *                     many workgroups are launched (default 1 = off: slower at B = 1 on gfx950);
+ *   "splitk_max"    — maximum number of K slices (power of two <= 16, default 4).
+ *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
+ *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.
+ * Split-K sums the slices in a fixed order (deterministic).  Returns 1001 for an unknown key. */
+FLAMED_API int flamed_tune(const char* key, int value);
+
+/* Diagnostic (libflamed_hip_stamps.so only, built with -DFL_STAMPS): device buffer of blocks x 8
+ * u64 into which the denoiser kernels of class `flamed_tune("stamp_class", c)` write s_memtime at
+ * their phase boundaries (eager steps only).  Returns 1001 in the regular library. */
+FLAMED_API int flamed_stamp_buffer(void* buf);
+
+/* Diagnostic probes: average device time (us) per launch inside a graph of `reps` back-to-back
+ * launches.  flamed_probe_gemm: C[M][N] (bf16) = A[M][K] (bf16) . W[N][K]^T with tile variant
+ * 0: 32x64 3-stage, 1: 64x64 3-stage, 2: 32x64 2-stage, 3: 128x128, 4: 64x128, 5: 128x64,
+ * 6: 32x64 with 4 K-steps of register prefetch, 7: 32x64 with 6, 8: 64x64 with 4.  Launch i reads
+ * weight matrix i % wbufs of W (wbufs x N x K), so a large wbufs streams weights from MALL/HBM as
+ * in a real Euler step.
+ * flamed_probe_empty: an empty kernel of `blocks` x 256 threads (the per-node floor). */
+FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int wbufs, const void* A, const void* W,
+                                 void* C, float* us_out, hipStream_t stream);
+FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t stream);
 
 /* ==================== PVA duration / silence generators + length regulator ====================
  * Replaces ProbabilisticModule.forward (pva.py:221-238) inside the Euler loop of PVA.sample

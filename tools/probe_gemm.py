@@ -1,0 +1,54 @@
+"""GEMM / graph-node latency probes on the GPU (flamed_probe_gemm / flamed_probe_empty).
+Per-launch us inside a graph of back-to-back launches for tile/pipeline variants, with weights either
+L2-hot (one buffer) or streamed (24 rotating 2 MB buffers, as the 21 GEMMs of a denoiser step)."""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "flamed-tts_amd"))
+from flamed import _native as nat  # noqa: E402
+
+VARIANTS = {0: "32x64s3", 1: "64x64s3", 2: "32x64s2", 6: "32x64r4", 7: "32x64r6", 8: "64x64r4", 5: "128x64s3",
+            3: "128x128s3"}
+
+
+def main():
+    dev = torch.device("cuda:0")
+    L = nat.lib()
+    st = nat.stream_ptr(dev)
+    us = ctypes.c_float()
+    nat.check(L.flamed_probe_empty(256, 64, ctypes.byref(us), st), "empty")
+    print(f"empty kernel: {us.value:6.2f} us/launch")
+    N = 1024
+    for M in (400, 1600, 25600):
+        for K in ((1024,) if M != 400 else (256, 1024)):
+            A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            nb = 24
+            W = torch.randn(nb * N, K, device=dev).to(torch.bfloat16)
+            C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ref = (A.float() @ W[:N].float().t())
+            for wb in (1, nb):
+                row = []
+                for v, name in VARIANTS.items():
+                    if v == 3 and M < 1600:
+                        continue
+                    reps = 48 if M < 4000 else 24
+                    rc = L.flamed_probe_gemm(v, M, N, K, reps, wb, nat.ptr(A), nat.ptr(W), nat.ptr(C), ctypes.byref(us), st)
+                    if rc:
+                        row.append(f"{name}=ERR({nat.lib().flamed_last_error().decode()[:40]})")
+                        continue
+                    tf = 2 * M * N * K / (us.value * 1e-6) / 1e12
+                    row.append(f"{name}={us.value:6.2f}({tf:4.0f}TF)")
+                    if M <= 1600:  # correctness of this variant (launch 0 reads buffer 0)
+                        nat.check(L.flamed_probe_gemm(v, M, N, K, 1, 1, nat.ptr(A), nat.ptr(W), nat.ptr(C),
+                                                      ctypes.byref(us), st), "chk")
+                        torch.cuda.synchronize()
+                        err = (C.float() - ref).abs().max().item() / ref.abs().max().item()
+                        assert err < 2e-2, (name, err)
+                print(f"M={M:6d} K={K:5d} wbufs={wb:2d}: " + " ".join(row))
+
+
+if __name__ == "__main__":
+    main()
