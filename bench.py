@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--splitk-target", type=int, default=None, help="flamed_tune splitk_target (1 disables split-K)")
     ap.add_argument("--splitk-max", type=int, default=None, help="flamed_tune splitk_max")
     ap.add_argument("--dup-class", type=int, default=None, help="ablation: flamed_tune dup_class")
+    ap.add_argument("--small-stages", type=int, default=None, help="flamed_tune small_stages (3, 5, 7)")
     return ap.parse_args()
 
 
@@ -101,7 +102,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")

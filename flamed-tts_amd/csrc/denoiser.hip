@@ -19,6 +19,7 @@
 namespace fl {
 
 thread_local SplitCtx* g_split = nullptr;
+int g_small_stages = 3;
 // Tuning knobs (flamed_tune): split-K workgroup target and maximum split for small-M GEMMs.
 static int g_tune_split_target = 1;  // split-K off by default: measured slower at B=1 (profiles/r01_splitk_sweep.txt)
 static int g_tune_split_max = 4;
@@ -439,37 +440,42 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
 #pragma unroll
     for (int g = 0; g < RG; ++g) chan_combine(n, mu, m2, red[(g * kDwCG + tid) * 3], red[(g * kDwCG + tid) * 3 + 1], red[(g * kDwCG + tid) * 3 + 2]);
     float* o = GP + (((size_t)b * TS + ts) * H + c0 + tid) * 3;
-    o[0] = n; o[1] = mu; o[2] = m2;
+    if (gcnt) {  // handed to another workgroup: write-through (sc1) stores, no release fence needed
+      __hip_atomic_store(o, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 1, mu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 2, m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      o[0] = n; o[1] = mu; o[2] = m2;
+    }
   }
   FL_STAMP(4);
   if (!gcnt) return;
   // GroupNorm finalize fused: the last T-chunk block of this (utterance, channel group) combines the
   // TS chunk partials in chunk order (as gn_finalize_kernel) and writes GNS = (mean, rstd).
+  // Hand-off (cdna_hip_programming.md §6 Guideline 16, sc1 form): partials stored write-through and
+  // drained, one relaxed agent-scope ticket; the last arriver reads them with sc1 (agent atomic) loads.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int* flag = reinterpret_cast<int*>(red + RG * kDwCG * 3);
   if (tid == 0) {
     int* cnt = gcnt + (size_t)b * gridDim.x + blockIdx.x;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == TS - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *cnt = 0;
-    }
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
     *flag = last;
   }
   __syncthreads();
   if (!*flag || tid >= kDwCG) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
   float n = 0.f, mu = 0.f, m2 = 0.f;
   for (int t0c = 0; t0c < TS; t0c += 8) {
     float q[8][3];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float* p = GP + (((size_t)b * TS + (t0c + i < TS ? t0c + i : TS - 1)) * H + c0 + tid) * 3;
-      q[i][0] = p[0]; q[i][1] = p[1]; q[i][2] = p[2];
+      q[i][0] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q[i][1] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q[i][2] = __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -945,12 +951,12 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
     K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
     K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
-    K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
+    K_(3, (launch_gemm_auto<DT>(cfg, kWideA, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
                                         EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
     K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
                                         EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
                                         M, H, H, st)));
-    K_(5, (launch_gemm_auto<DT>(cfg, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
+    K_(5, (launch_gemm_auto<DT>(cfg, kWideA, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
                                         EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
     K_(6, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
                                         EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st)));
@@ -961,11 +967,11 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   const DenBlockW& F = d->fin;
   K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
   K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
-  K_(3, (launch_gemm_auto<DT>(cfg, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  K_(3, (launch_gemm_auto<DT>(cfg, kWideA, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                       EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
                                       M, H, H, st)));
-  K_(7, (launch_gemm_auto<DT>(cfg, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
+  K_(7, (launch_gemm_auto<DT>(cfg, kWideA, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
                                       EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
   {
     size_t n = (size_t)M * C;
@@ -1089,6 +1095,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   const std::string k(key);
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "small_stages") { FL_REQUIRE(value == 3 || value == 5 || value == 7, "flamed_tune: small_stages must be 3, 5 or 7"); g_small_stages = value; return kOk; }
   if (k == "dup_class") { FL_REQUIRE(value >= -1 && value < FLAMED_DEN_KERNEL_CLASSES, "flamed_tune: dup_class in [-1, %d)", FLAMED_DEN_KERNEL_CLASSES); g_dup_class = value; return kOk; }
   if (k == "splitk_max") { FL_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8 || value == 16, "flamed_tune: splitk_max must be a power of two <= 16"); g_tune_split_max = value; return kOk; }
   set_error("flamed_tune: unknown key '%s'", key);

@@ -1,4 +1,5 @@
-// FaCodec decoder (inference) on gfx950.  Reference: flamed/models/facodec/facodec.py:27-32
+// FaCodec decoder (inference) and encoder (prompt path) on gfx950.  Reference:
+// flamed/models/facodec/facodec.py:136-244 (EncoderBlock, FACodecEncoder), :27-32
 // (WNConv1d / WNConvTranspose1d), :57-118 (SnakeBeta), :121-133 (ResidualUnit), :246-265
 // (DecoderBlock), :398-415 (model stack), :630-638 (FACodecDecoder.inference);
 // alias_free_torch/act.py:7-29, resample.py:9-57, filter.py:27-96 (Activation1d).
@@ -33,16 +34,16 @@ __global__ __launch_bounds__(256) void wn_fold_kernel(const float* __restrict__ 
   for (int k = threadIdx.x; k < inner; k += 256) w[(size_t)i * inner + k] = vi[k] * sc;
 }
 
-// conv (N, Cin, KT) -> (N, KT, Cin) in DT
+// conv (N, Cin, KT) -> rows of (KT, Cin) in DT with row stride ldk >= KT*Cin (pad pre-zeroed)
 template <typename DT>
-__global__ void pack_conv_kernel(const float* __restrict__ src, DT* __restrict__ dst, int N, int Cin, int KT) {
+__global__ void pack_conv_kernel(const float* __restrict__ src, DT* __restrict__ dst, int N, int Cin, int KT, int ldk) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)N * Cin * KT) return;
   int k = i % KT;
   size_t t = i / KT;
   int c = t % Cin;
   int n = t / Cin;
-  store_val<DT>(dst + ((size_t)n * KT + k) * Cin + c, src[i]);
+  store_val<DT>(dst + (size_t)n * ldk + (size_t)k * Cin + c, src[i]);
 }
 
 // convT (Cin, Cout, 2s) -> per phase r: (Cout, 2, Cin) with tap 0 = kernel index r, tap 1 = r + s
@@ -61,15 +62,16 @@ __global__ void pack_convt_kernel(const float* __restrict__ src, DT* __restrict_
 
 // ------------------------------ fused Activation1d ------------------------------
 constexpr int kActA = 64;  // output samples per workgroup
-constexpr int kActCG = 64; // channels per workgroup
 
-template <typename OT>
+// kActCG channels per workgroup (64, or 32 for the encoder's first stage)
+template <typename OT, int kActCG>
 __global__ __launch_bounds__(256) void act1d_kernel(const float* __restrict__ x, int C, int n,
                                                     const float* __restrict__ alpha, const float* __restrict__ beta,
                                                     const float* __restrict__ fu, const float* __restrict__ fd,
                                                     OT* __restrict__ out) {
   constexpr int XR = kActA + 13;      // x rows a0-6 .. a0+A+6
   constexpr int SR = 2 * kActA + 12;  // snake samples j = 2a0-5 .. 2a0+2A+6
+  constexpr int RGS = 256 / kActCG;   // row groups
   __shared__ float xs[XR * kActCG];
   __shared__ float ss[SR * kActCG];
   __shared__ float filt[24];
@@ -85,11 +87,11 @@ __global__ __launch_bounds__(256) void act1d_kernel(const float* __restrict__ x,
     xs[idx] = xb[(size_t)a * C + c0 + cc];
   }
   __syncthreads();
-  const int cc = tid & 63, rg = tid >> 6;
+  const int cc = tid % kActCG, rg = tid / kActCG;
   const float ea = expf(alpha[c0 + cc]);
   const float ib = 1.0f / (expf(beta[c0 + cc]) + 1e-9f);
   const int n2 = 2 * n;
-  for (int jj = rg; jj < SR; jj += 4) {
+  for (int jj = rg; jj < SR; jj += RGS) {
     int j = 2 * a0 - 5 + jj;
     j = j < 0 ? 0 : (j >= n2 ? n2 - 1 : j);
     const int ap = j >> 1;
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(256) void act1d_kernel(const float* __restrict__ x,
   }
   __syncthreads();
   OT* ob = out + (size_t)b * n * C;
-  for (int q = rg; q < kActA; q += 4) {
+  for (int q = rg; q < kActA; q += RGS) {
     int a = a0 + q;
     if (a >= n) break;
     float acc = 0.f;
@@ -280,9 +282,12 @@ static size_t fac_ws_layout(const Fac* f, int B, int T, void* base, FacWs* w) {
 
 template <typename DT>
 static int launch_act(const FacAct& a, const float* x, int C, int n, int B, DT* out, hipStream_t st) {
-  FL_REQUIRE(C % kActCG == 0, "act1d: C=%d must be a multiple of 64", C);
-  hipLaunchKernelGGL(act1d_kernel<DT>, dim3(C / kActCG, (n + kActA - 1) / kActA, B), dim3(256), 0, st, x, C, n, a.alpha,
-                     a.beta, a.fu, a.fd, out);
+  FL_REQUIRE(C % 32 == 0, "act1d: C=%d must be a multiple of 32", C);
+  const int na = (n + kActA - 1) / kActA;
+  if (C % 64 == 0)
+    hipLaunchKernelGGL((act1d_kernel<DT, 64>), dim3(C / 64, na, B), dim3(256), 0, st, x, C, n, a.alpha, a.beta, a.fu, a.fd, out);
+  else
+    hipLaunchKernelGGL((act1d_kernel<DT, 32>), dim3(C / 32, na, B), dim3(256), 0, st, x, C, n, a.alpha, a.beta, a.fu, a.fd, out);
   FL_LAUNCH_CHECK();
   return kOk;
 }
@@ -427,8 +432,8 @@ FLAMED_API int flamed_fac_load(flamed_fac_t h, const float* const* w, int nw, hi
     size_t total = (size_t)cv.N * cv.Cin * cv.KT;
     dim3 grid((total + 255) / 256);
     if (cv.kind == 0) {
-      if (f->dt == FLAMED_BF16) hipLaunchKernelGGL(pack_conv_kernel<bf16>, grid, dim3(256), 0, st, tmp, (bf16*)(f->dev + cv.off), cv.N, cv.Cin, cv.KT);
-      else hipLaunchKernelGGL(pack_conv_kernel<float>, grid, dim3(256), 0, st, tmp, (float*)(f->dev + cv.off), cv.N, cv.Cin, cv.KT);
+      if (f->dt == FLAMED_BF16) hipLaunchKernelGGL(pack_conv_kernel<bf16>, grid, dim3(256), 0, st, tmp, (bf16*)(f->dev + cv.off), cv.N, cv.Cin, cv.KT, cv.Cin * cv.KT);
+      else hipLaunchKernelGGL(pack_conv_kernel<float>, grid, dim3(256), 0, st, tmp, (float*)(f->dev + cv.off), cv.N, cv.Cin, cv.KT, cv.Cin * cv.KT);
     } else {
       if (f->dt == FLAMED_BF16) hipLaunchKernelGGL(pack_convt_kernel<bf16>, grid, dim3(256), 0, st, tmp, (bf16*)(f->dev + cv.off), cv.Cin, cv.N, cv.s);
       else hipLaunchKernelGGL(pack_convt_kernel<float>, grid, dim3(256), 0, st, tmp, (float*)(f->dev + cv.off), cv.Cin, cv.N, cv.s);
@@ -489,6 +494,346 @@ FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const flo
     f->gkey = key;
   }
   FL_HIP(hipGraphLaunch(f->gexec, st));
+  return kOk;
+}
+
+}  // extern "C"
+
+// ======================================================================================
+// FaCodec encoder (prompt encoding): facodec.py:136-244.
+//   conv_in WNConv1d(1 -> ngf, k7, p3)                       -> enc_in_kernel (direct, fp32)
+//   per EncoderBlock(d, s): 3 x ResidualUnit(d/2, dil 1/3/9)  -> act1d + K-padded conv GEMMs + EpiResAdd
+//                           Activation1d + WNConv1d(d/2 -> d, k=2s, stride s, pad ceil(s/2))
+//                                                             -> strided-gather GEMM (LoadConvStride)
+//   Activation1d + WNConv1d(d -> out, k3, p1)                 -> GEMM, channels-first store (B, out, T)
+// Lengths follow Conv1d: n_out = floor((n + 2p - k) / s) + 1 at every stride.
+// ======================================================================================
+namespace fl {
+
+// Direct Conv1d(1 -> C, k7, pad 3): X[(b*n + t)*C + c] = bias[c] + sum_k w[c][k] wav[b][t + k - 3]
+__global__ __launch_bounds__(256) void enc_in_kernel(const float* __restrict__ wav, int n, int C, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, float* __restrict__ X, size_t total) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C;
+  const size_t bt = i / C;
+  const int t = bt % n;
+  const float* wb = wav + (bt - t);
+  float acc = bias[c];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int src = t + k - 3;
+    if (src >= 0 && src < n) acc += w[c * 7 + k] * wb[src];
+  }
+  X[i] = acc;
+}
+
+// Dilated conv tap gather over a DT activation with K zero-padded to the GEMM K-step: k >= kreal -> 0.
+template <typename DT>
+struct LoadConvPad {
+  const DT* __restrict__ x;
+  int Cin, L, KT, dil, kreal;
+  struct Raw { u32x4 v; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    if (k >= kreal) return Raw{u32x4{0u, 0u, 0u, 0u}};
+    int tap = k / Cin, c = k - tap * Cin;
+    int off = (tap - KT / 2) * dil;
+    int l = m % L + off;
+    if (l < 0 || l >= L) return Raw{u32x4{0u, 0u, 0u, 0u}};
+    return Raw{*reinterpret_cast<const u32x4*>(x + (size_t)(m + off) * Cin + c)};
+  }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
+};
+
+// Strided conv gather: output row m = (b, o), o < nout; tap t reads x[b][o*s + t - p] (zero outside).
+template <typename DT>
+struct LoadConvStride {
+  const DT* __restrict__ x;
+  int Cin, nin, nout, s, p;
+  struct Raw { u32x4 v; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    const int b = m / nout, o = m - b * nout;
+    const int tap = k / Cin, c = k - tap * Cin;
+    const int i = o * s + tap - p;
+    if (i < 0 || i >= nin) return Raw{u32x4{0u, 0u, 0u, 0u}};
+    return Raw{*reinterpret_cast<const u32x4*>(x + ((size_t)b * nin + i) * Cin + c)};
+  }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int, const float*, int) const { return r.v; }
+};
+
+// out (B, N, T) channels-first = acc + bias (the encoder's (B, C, T) output layout)
+struct EpiStoreCF {
+  const float* __restrict__ bias;
+  float* __restrict__ out;
+  int N, T;
+  static constexpr bool kRowStats = false;
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ float value(int, int col, float acc, const float*, int) const { return acc + bias[col]; }
+  __device__ void store(int m, int col, float v) const {
+    const int b = m / T, t = m - b * T;
+    out[((size_t)b * N + col) * T + t] = v;
+  }
+  __device__ void store_stats(int, int, float, float) const {}
+};
+
+// N = 32 (the encoder's first stage) runs a 64 x 32 tile; every other width the shape-driven configs.
+template <typename DT, class AL, class EP>
+static int enc_gemm(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  if (N % 64 != 0) return launch_gemm_cfg<64, 32, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm<DT>(al, W, ldw, ep, M, N, K, st);
+}
+
+struct EncRU { FacAct a1, a2; void* w7; const float* b7; int k7; void* w1; const float* b1; int k1; int dil; };
+struct EncBlk { EncRU ru[3]; FacAct a; void* wc; const float* bc; int s, cin, cout; };
+
+struct Enc {
+  int ngf, NDN, cout, dt;
+  int ratios[8];
+  float* w_in = nullptr; const float* b_in = nullptr;
+  EncBlk blk[8];
+  FacAct afin;
+  void* wfin = nullptr; const float* bfin = nullptr;
+  int cfin;
+  char* dev = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  hipStream_t cap = nullptr;
+  std::vector<const void*> gkey;
+};
+
+static int kpad64(int k) { return (k + 63) / 64 * 64; }
+
+static int enc_len_after(const Enc* e, int n, int upto) {  // sequence length after `upto` blocks
+  for (int i = 0; i < upto; ++i) {
+    const int s = e->ratios[i], p = s / 2 + s % 2;
+    n = (n + 2 * p - 2 * s) / s + 1;
+  }
+  return n;
+}
+
+struct EncWs { float* X; float* Z; void* A; };
+static size_t enc_ws_layout(const Enc* e, int B, int n, void* base, EncWs* w) {
+  // largest (length x channels) over the stages (block i runs at ngf * 2^i / 2 channels ... d)
+  size_t maxcn = (size_t)n * e->ngf;
+  int len = n, d = e->ngf;
+  for (int i = 0; i < e->NDN; ++i) {
+    maxcn = maxcn > (size_t)len * d ? maxcn : (size_t)len * d;
+    const int s = e->ratios[i], p = s / 2 + s % 2;
+    len = (len + 2 * p - 2 * s) / s + 1;
+    d *= 2;
+    maxcn = maxcn > (size_t)len * d ? maxcn : (size_t)len * d;
+  }
+  const size_t es = e->dt == FLAMED_BF16 ? 2 : 4;
+  const size_t sizes[3] = {4 * B * maxcn, 4 * B * maxcn, es * B * maxcn};
+  size_t off = 0;
+  char* p[3];
+  for (int i = 0; i < 3; ++i) {
+    p[i] = base ? (char*)base + off : nullptr;
+    off += al256(sizes[i]);
+  }
+  if (w) *w = EncWs{(float*)p[0], (float*)p[1], p[2]};
+  return off;
+}
+
+template <typename DT>
+static int enc_impl(Enc* e, const float* wav, int B, int n, float* out, const EncWs& w, hipStream_t st) {
+  int rc;
+#define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
+  DT* A = reinterpret_cast<DT*>(w.A);
+  {
+    const size_t total = (size_t)B * n * e->ngf;
+    hipLaunchKernelGGL(enc_in_kernel, dim3((total + 255) / 256), dim3(256), 0, st, wav, n, e->ngf, e->w_in, e->b_in, w.X, total);
+    FL_LAUNCH_CHECK();
+  }
+  int len = n;
+  for (int i = 0; i < e->NDN; ++i) {
+    const EncBlk& bk = e->blk[i];
+    const int C = bk.cin;
+    for (int j = 0; j < 3; ++j) {
+      const EncRU& ru = bk.ru[j];
+      TRY(launch_act<DT>(ru.a1, w.X, C, len, B, A, st));
+      TRY((enc_gemm<DT>(LoadConvPad<DT>{A, C, len, 7, ru.dil, 7 * C}, (const DT*)ru.w7, ru.k7, EpiBiasAct<float, 0>{ru.b7, w.Z, C},
+                        B * len, C, ru.k7, st)));
+      TRY(launch_act<DT>(ru.a2, w.Z, C, len, B, A, st));
+      TRY((enc_gemm<DT>(LoadConvPad<DT>{A, C, len, 1, 1, C}, (const DT*)ru.w1, ru.k1, EpiResAdd{ru.b1, w.X, C}, B * len, C, ru.k1, st)));
+    }
+    TRY(launch_act<DT>(bk.a, w.X, C, len, B, A, st));
+    const int s = bk.s, p = s / 2 + s % 2;
+    const int nout = (len + 2 * p - 2 * s) / s + 1;
+    FL_REQUIRE(nout > 0, "flamed_enc_encode: input too short for the stride-%d stage", s);
+    TRY((enc_gemm<DT>(LoadConvStride<DT>{A, C, len, nout, s, p}, (const DT*)bk.wc, 2 * s * C, EpiBiasAct<float, 0>{bk.bc, w.X, bk.cout},
+                      B * nout, bk.cout, 2 * s * C, st)));
+    len = nout;
+  }
+  const int cf = e->cfin;
+  TRY(launch_act<DT>(e->afin, w.X, cf, len, B, A, st));
+  TRY((enc_gemm<DT>(LoadConvPad<DT>{A, cf, len, 3, 1, 3 * cf}, (const DT*)e->wfin, kpad64(3 * cf), EpiStoreCF{e->bfin, out, e->cout, len},
+                    B * len, e->cout, kpad64(3 * cf), st)));
+#undef TRY
+  return kOk;
+}
+
+}  // namespace fl
+
+extern "C" {
+
+FLAMED_API int flamed_enc_create(int ngf, int n_down, const int* ratios, int out_channels, int dtype, flamed_enc_t* out) {
+  FL_REQUIRE(out && ratios, "flamed_enc_create: null args");
+  FL_REQUIRE(n_down >= 1 && n_down <= 8, "flamed_enc_create: n_down=%d unsupported", n_down);
+  FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16, "flamed_enc_create: bad dtype");
+  FL_REQUIRE(ngf % 32 == 0 && ngf <= 256, "flamed_enc_create: ngf=%d must be a multiple of 32", ngf);
+  FL_REQUIRE(out_channels % 64 == 0, "flamed_enc_create: out_channels=%d must be a multiple of 64", out_channels);
+  Enc* e = new Enc();
+  e->ngf = ngf; e->NDN = n_down; e->cout = out_channels; e->dt = dtype;
+  for (int i = 0; i < n_down; ++i) {
+    FL_REQUIRE(ratios[i] >= 1 && ratios[i] <= 8, "flamed_enc_create: ratio %d unsupported", ratios[i]);
+    e->ratios[i] = ratios[i];
+  }
+  *out = reinterpret_cast<flamed_enc_t>(e);
+  return kOk;
+}
+
+FLAMED_API int flamed_enc_destroy(flamed_enc_t h) {
+  Enc* e = reinterpret_cast<Enc*>(h);
+  if (!e) return kOk;
+  if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
+  if (e->cap) (void)hipStreamDestroy(e->cap);
+  if (e->dev) (void)hipFree(e->dev);
+  delete e;
+  return kOk;
+}
+
+FLAMED_API int flamed_enc_num_weights(flamed_enc_t h) {
+  Enc* e = reinterpret_cast<Enc*>(h);
+  return e ? 3 + FLAMED_ENC_BLOCK_W * e->NDN + 7 : -1;
+}
+
+FLAMED_API int flamed_enc_out_len(flamed_enc_t h, int n) {
+  Enc* e = reinterpret_cast<Enc*>(h);
+  return e ? enc_len_after(e, n, e->NDN) : -1;
+}
+
+FLAMED_API int flamed_enc_load(flamed_enc_t h, const float* const* w, int nw, hipStream_t st) {
+  Enc* e = reinterpret_cast<Enc*>(h);
+  FL_REQUIRE(e && w, "flamed_enc_load: null args");
+  FL_REQUIRE(nw == flamed_enc_num_weights(h), "flamed_enc_load: expected %d weights, got %d", flamed_enc_num_weights(h), nw);
+  for (int i = 0; i < nw; ++i) FL_REQUIRE(w[i], "flamed_enc_load: weight %d is null", i);
+  const size_t es = e->dt == FLAMED_BF16 ? 2 : 4;
+  struct Conv { const float *g, *v; int N, Cin, KT, ldk; size_t off; };
+  std::vector<Conv> convs;
+  size_t off = 0, maxfold = 0;
+  auto add = [&](const float* g, const float* v, int N, int Cin, int KT, int ldk) -> int {
+    convs.push_back(Conv{g, v, N, Cin, KT, ldk, off});
+    off = al256(off + es * (size_t)N * ldk);
+    maxfold = maxfold > (size_t)N * Cin * KT ? maxfold : (size_t)N * Cin * KT;
+    return (int)convs.size() - 1;
+  };
+  // conv_in (ngf, 1, 7): folded fp32 for the direct kernel
+  const size_t o_in = off;
+  off = al256(off + 4ull * e->ngf * 7);
+  e->b_in = w[2];
+  std::vector<int> i7(e->NDN * 3), i1(e->NDN * 3), ic(e->NDN);
+  int d = e->ngf;
+  for (int i = 0; i < e->NDN; ++i) {
+    const float* const* bw = w + 3 + FLAMED_ENC_BLOCK_W * i;
+    EncBlk& bk = e->blk[i];
+    bk.cin = d; bk.cout = 2 * d; bk.s = e->ratios[i];
+    const int dils[3] = {1, 3, 9};
+    for (int j = 0; j < 3; ++j) {
+      const float* const* rw = bw + 14 * j;
+      EncRU& ru = bk.ru[j];
+      ru.dil = dils[j];
+      ru.a1 = FacAct{rw[0], rw[1], rw[2], rw[3]};
+      ru.k7 = kpad64(7 * d);
+      i7[i * 3 + j] = add(rw[4], rw[5], d, d, 7, ru.k7);
+      ru.b7 = rw[6];
+      ru.a2 = FacAct{rw[7], rw[8], rw[9], rw[10]};
+      ru.k1 = kpad64(d);
+      i1[i * 3 + j] = add(rw[11], rw[12], d, d, 1, ru.k1);
+      ru.b1 = rw[13];
+    }
+    bk.a = FacAct{bw[42], bw[43], bw[44], bw[45]};
+    ic[i] = add(bw[46], bw[47], 2 * d, d, 2 * bk.s, 2 * bk.s * d);
+    bk.bc = bw[48];
+    d *= 2;
+  }
+  e->cfin = d;
+  const float* const* fw = w + 3 + FLAMED_ENC_BLOCK_W * e->NDN;
+  e->afin = FacAct{fw[0], fw[1], fw[2], fw[3]};
+  const int ifin = add(fw[4], fw[5], e->cout, d, 3, kpad64(3 * d));
+  e->bfin = fw[6];
+  const size_t o_tmp = off;
+  off = al256(off + 4 * maxfold);
+  if (e->dev) { FL_HIP(hipFree(e->dev)); e->dev = nullptr; }
+  FL_HIP(hipMalloc(&e->dev, off));
+  FL_HIP(hipMemsetAsync(e->dev, 0, o_tmp, st));  // zero K padding of the packed weights
+  float* tmp = reinterpret_cast<float*>(e->dev + o_tmp);
+  hipLaunchKernelGGL(wn_fold_kernel, dim3(e->ngf), dim3(256), 0, st, w[0], w[1], 7, reinterpret_cast<float*>(e->dev + o_in));
+  FL_LAUNCH_CHECK();
+  e->w_in = reinterpret_cast<float*>(e->dev + o_in);
+  for (const Conv& cv : convs) {
+    hipLaunchKernelGGL(wn_fold_kernel, dim3(cv.N), dim3(256), 0, st, cv.g, cv.v, cv.Cin * cv.KT, tmp);
+    FL_LAUNCH_CHECK();
+    const size_t total = (size_t)cv.N * cv.Cin * cv.KT;
+    const dim3 grid((total + 255) / 256);
+    if (e->dt == FLAMED_BF16) hipLaunchKernelGGL(pack_conv_kernel<bf16>, grid, dim3(256), 0, st, tmp, (bf16*)(e->dev + cv.off), cv.N, cv.Cin, cv.KT, cv.ldk);
+    else hipLaunchKernelGGL(pack_conv_kernel<float>, grid, dim3(256), 0, st, tmp, (float*)(e->dev + cv.off), cv.N, cv.Cin, cv.KT, cv.ldk);
+    FL_LAUNCH_CHECK();
+  }
+  for (int i = 0; i < e->NDN; ++i) {
+    for (int j = 0; j < 3; ++j) {
+      e->blk[i].ru[j].w7 = e->dev + convs[i7[i * 3 + j]].off;
+      e->blk[i].ru[j].w1 = e->dev + convs[i1[i * 3 + j]].off;
+    }
+    e->blk[i].wc = e->dev + convs[ic[i]].off;
+  }
+  e->wfin = e->dev + convs[ifin].off;
+  FL_HIP(hipStreamSynchronize(st));  // fold scratch reused per conv
+  if (e->gexec) { (void)hipGraphExecDestroy(e->gexec); e->gexec = nullptr; }
+  return kOk;
+}
+
+FLAMED_API size_t flamed_enc_workspace_size(flamed_enc_t h, int B, int n) {
+  Enc* e = reinterpret_cast<Enc*>(h);
+  return e ? enc_ws_layout(e, B, n, nullptr, nullptr) : 0;
+}
+
+FLAMED_API int flamed_enc_encode(flamed_enc_t h, const float* wav, int B, int n, float* out, void* ws, size_t ws_bytes,
+                                 int use_graph, hipStream_t st) {
+  Enc* e = reinterpret_cast<Enc*>(h);
+  FL_REQUIRE(e && e->dev, "flamed_enc_encode: handle not loaded");
+  FL_REQUIRE(wav && out && ws && B > 0 && n > 0, "flamed_enc_encode: bad args");
+  FL_REQUIRE(enc_len_after(e, n, e->NDN) > 0, "flamed_enc_encode: n=%d too short", n);
+  if (ws_bytes < enc_ws_layout(e, B, n, nullptr, nullptr)) {
+    set_error("flamed_enc_encode: workspace too small");
+    return kNoWorkspace;
+  }
+  EncWs w;
+  enc_ws_layout(e, B, n, ws, &w);
+  auto run = [&](hipStream_t s) -> int {
+    return e->dt == FLAMED_BF16 ? enc_impl<bf16>(e, wav, B, n, out, w, s) : enc_impl<float>(e, wav, B, n, out, w, s);
+  };
+  if (!use_graph) return run(st);
+  std::vector<const void*> key = {wav, out, ws, (const void*)(intptr_t)B, (const void*)(intptr_t)n, e->dev};
+  if (!e->gexec || e->gkey != key) {
+    if (e->gexec) { FL_HIP(hipGraphExecDestroy(e->gexec)); e->gexec = nullptr; }
+    if (!e->cap) FL_HIP(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+    FL_HIP(hipStreamBeginCapture(e->cap, hipStreamCaptureModeRelaxed));
+    int r = run(e->cap);
+    hipGraph_t g = nullptr;
+    hipError_t er = hipStreamEndCapture(e->cap, &g);
+    if (r) { if (g) (void)hipGraphDestroy(g); return r; }
+    FL_HIP(er);
+    hipError_t ie = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    FL_HIP(ie);
+    e->gkey = key;
+  }
+  FL_HIP(hipGraphLaunch(e->gexec, st));
   return kOk;
 }
 

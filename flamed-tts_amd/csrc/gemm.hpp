@@ -600,6 +600,9 @@ struct SplitCtx {
   int max_split = 4;
 };
 extern thread_local SplitCtx* g_split;
+// Pipeline depth of the small-M (32 x 64) config: 3 = LDS ring of 3 / 2 K-steps in flight,
+// 5 / 7 = 4 / 6 K-steps of register prefetch (flamed_tune "small_stages").
+extern int g_small_stages;
 struct SplitScope {
   SplitCtx* prev;
   explicit SplitScope(SplitCtx* c) : prev(g_split) { g_split = c; }
@@ -650,9 +653,25 @@ inline int cfg_bn(GemmCfg) { return 64; }
 
 template <typename DT, class AL, class EP>
 inline int launch_gemm_auto(GemmCfg c, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
-  if (c == kCfgSmall) return launch_gemm_cfg<32, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  if (c == kCfgSmall) {
+    if (g_small_stages == 5) return launch_gemm_cfg<32, 64, 5, DT>(al, W, ldw, ep, M, N, K, st);
+    if (g_small_stages == 7) return launch_gemm_cfg<32, 64, 7, DT>(al, W, ldw, ep, M, N, K, st);
+    return launch_gemm_cfg<32, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  }
   if (c == kCfgMid) return launch_gemm_cfg<64, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
   return launch_gemm_cfg<128, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
+}
+
+// kWideA: the A loader transforms fp32 rows (LayerNorm / GroupNorm apply); at large M a 128 x 128 tile
+// halves how often those rows are re-read (B = 64 measurement: 128 x 64 slowed these GEMMs by ~30 %).
+constexpr bool kWideA = true;
+
+template <typename DT, class AL, class EP>
+inline int launch_gemm_auto(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
+                            hipStream_t st) {
+  if (c == kCfgLarge && wide_a && N % 128 == 0 && !EP::kRowStats)
+    return launch_gemm_cfg<128, 128, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm_auto<DT>(c, al, W, ldw, ep, M, N, K, st);
 }
 
 // Shape-driven convenience: choose the config from M (row partial width = cfg_bn(pick_cfg(M)) when

@@ -52,6 +52,13 @@ SIGNATURES = {
     "flamed_fac_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
     "flamed_fac_workspace_size": (c_size_t, [P, c_int, c_int]),
     "flamed_fac_decode": (c_int, [P, P, P, c_int, c_int, P, P, c_size_t, c_int, P]),
+    "flamed_enc_create": (c_int, [c_int, c_int, ctypes.POINTER(c_int), c_int, c_int, ctypes.POINTER(P)]),
+    "flamed_enc_destroy": (c_int, [P]),
+    "flamed_enc_num_weights": (c_int, [P]),
+    "flamed_enc_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_enc_out_len": (c_int, [P, c_int]),
+    "flamed_enc_workspace_size": (c_size_t, [P, c_int, c_int]),
+    "flamed_enc_encode": (c_int, [P, P, c_int, c_int, P, P, c_size_t, c_int, P]),
 }
 
 FLAMED_F32, FLAMED_BF16 = 0, 1

@@ -138,16 +138,29 @@ class FACodecEncoder(nn.Module):
         layers += [_act(d), WNConv1d(d, out_channels, kernel_size=3, padding=1)]
         self.block = nn.Sequential(*layers)
         self.enc_dim = d
+        # On ROCm tensors the encoder runs in the HIP library; "f32" (default) is the exact-fp32 MFMA
+        # mode: the RVQ argmax downstream turns small activation errors into different prompt codes.
+        self.hip_dtype = "f32"
+        self.hip_graph = True
+        self._hip = None
         for m in self.modules():
             if isinstance(m, nn.Conv1d):
                 nn.init.trunc_normal_(m.weight, std=0.02)
                 nn.init.constant_(m.bias, 0)
 
+    def _use_hip(self, x):
+        return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+
     def forward(self, x):
+        """waveform (B, 1, n) -> (B, out_channels, T) (reference :215-217)."""
+        if self._use_hip(x):
+            if self._hip is None or self._hip.dtype_name != self.hip_dtype:
+                self._hip = EncoderHIP(self, self.hip_dtype)
+            return self._hip.encode(x)
         return self.block(x)
 
     def inference(self, x):
-        return self.block(x)
+        return self.forward(x)
 
 
 class FACodecDecoder(nn.Module):
@@ -359,3 +372,86 @@ class FacDecoderHIP:
                                       nat.ptr(ws), ws.numel(), int(bool(self.dec.hip_graph)), nat.stream_ptr(dev)),
                   "flamed_fac_decode")
         return bufs["wav"].clone()
+
+
+def enc_weight_list(enc: FACodecEncoder) -> List[torch.Tensor]:
+    """Weights in the order flamed_enc_load expects (include/flamed_hip.h)."""
+
+    def act(a):
+        return [a.act.alpha, a.act.beta, a.upsample.filter, a.downsample.lowpass.filter]
+
+    def wn(c):
+        return [c.weight_g, c.weight_v, c.bias]
+
+    b = enc.block
+    w = wn(b[0])
+    for i in range(len(enc.up_ratios)):
+        blk = b[1 + i].block
+        for j in range(3):
+            ru = blk[j].block
+            w += act(ru[0]) + wn(ru[1]) + act(ru[2]) + wn(ru[3])
+        w += act(blk[3]) + wn(blk[4])
+    n = len(enc.up_ratios) + 1
+    w += act(b[n]) + wn(b[n + 1])
+    return w
+
+
+class EncoderHIP:
+    """Owns one flamed_enc_t handle (FaCodec encoder on gfx950)."""
+
+    def __init__(self, enc: FACodecEncoder, dtype_name: str):
+        self.enc = enc
+        self.dtype_name = dtype_name
+        self.handle = None
+        self._sig = None
+        self._keep = []
+        self.ws = nat.Workspace()
+        self._bufs = {}
+
+    def __del__(self):
+        try:
+            if self.handle is not None:
+                nat.lib().flamed_enc_destroy(self.handle)
+        except Exception:
+            pass
+
+    def _ensure(self, dev):
+        params = enc_weight_list(self.enc)
+        sig = tuple((p.data_ptr(), p._version) for p in params) + (str(dev),)
+        if sig == self._sig:
+            return
+        L = nat.lib()
+        if self.handle is None:
+            h = ctypes.c_void_p()
+            ups = (ctypes.c_int * len(self.enc.up_ratios))(*self.enc.up_ratios)
+            nat.check(L.flamed_enc_create(self.enc.ngf, len(self.enc.up_ratios), ups, self.enc.out_channels,
+                                          nat.dtype_code(self.dtype_name), ctypes.byref(h)), "flamed_enc_create")
+            self.handle = h
+        keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
+        arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
+        nat.check(L.flamed_enc_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_enc_load")
+        self._keep = keep
+        self._sig = sig
+        self._bufs = {}
+
+    def encode(self, x):
+        if x.dim() != 3 or x.shape[1] != 1:
+            raise ValueError(f"FACodecEncoder expects (B, 1, n) audio, got {tuple(x.shape)}")
+        dev = x.device
+        self._ensure(dev)
+        B, _, n = x.shape
+        L = nat.lib()
+        T = L.flamed_enc_out_len(self.handle, n)
+        if T <= 0:
+            raise ValueError(f"audio of {n} samples is too short for the encoder")
+        key = (B, n)
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            bufs = {"x": torch.empty((B, n), dtype=torch.float32, device=dev),
+                    "out": torch.empty((B, self.enc.out_channels, T), dtype=torch.float32, device=dev)}
+            self._bufs = {key: bufs}
+        bufs["x"].copy_(x.reshape(B, n))
+        ws = self.ws.get(L.flamed_enc_workspace_size(self.handle, B, n), dev)
+        nat.check(L.flamed_enc_encode(self.handle, nat.ptr(bufs["x"]), B, n, nat.ptr(bufs["out"]), nat.ptr(ws), ws.numel(),
+                                      int(bool(self.enc.hip_graph)), nat.stream_ptr(dev)), "flamed_enc_encode")
+        return bufs["out"].clone()

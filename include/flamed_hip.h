@@ -104,6 +104,8 @@ FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* m
  *   "splitk_target" — bf16 small-M GEMMs (M < 2048 rows) split K over workgroups until about this
  *                     many workgroups are launched (default 1 = off: slower at B = 1 on gfx950);
  *   "splitk_max"    — maximum number of K slices (power of two <= 16, default 4).
+ *   "small_stages"  — pipeline of the small-M GEMM tile (M < 2048 rows): 3 (LDS ring, 2 K-steps in
+ *                     flight), 5 or 7 (4 or 6 K-steps of register prefetch);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.
  * Split-K sums the slices in a fixed order (deterministic).  Returns 1001 for an unknown key. */
@@ -180,6 +182,31 @@ FLAMED_API size_t flamed_fac_workspace_size(flamed_fac_t h, int B, int T);
  * wav: (B, hop*T) with hop = prod(up_ratios).  use_graph != 0 replays a cached hipGraph. */
 FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const float* spk, int B, int T, float* wav,
                                  void* ws, size_t ws_bytes, int use_graph, hipStream_t stream);
+
+/* ============================ FaCodec encoder (prompt encoding) ============================
+ * Replaces FACodecEncoder.forward (facodec.py:183-216; EncoderBlock :136-155), SURVEY.md §8(f) f3.
+ * Weight order for flamed_enc_load (fp32 device tensors as in the encoder state dict):
+ *   block.0.{weight_g,weight_v,bias},
+ *   per EncoderBlock block.{1..n_down}.block (FLAMED_ENC_BLOCK_W = 49 each):
+ *     for each ResidualUnit j in 0,1,2: j.block.0.act.{alpha,beta}, j.block.0.upsample.filter,
+ *     j.block.0.downsample.lowpass.filter, j.block.1.{weight_g,weight_v,bias}, j.block.2.act.{alpha,beta},
+ *     j.block.2.upsample.filter, j.block.2.downsample.lowpass.filter, j.block.3.{weight_g,weight_v,bias};
+ *     then 3.act.{alpha,beta}, 3.upsample.filter, 3.downsample.lowpass.filter, 4.{weight_g,weight_v,bias}
+ *   final: block.{n_down+1}.act.{alpha,beta}, .upsample.filter, .downsample.lowpass.filter,
+ *          block.{n_down+2}.{weight_g,weight_v,bias}
+ * Channels: ngf at the input, doubled by every block (ngf * 2^n_down before the output conv). */
+enum { FLAMED_ENC_BLOCK_W = 49 };
+typedef struct flamed_enc_s* flamed_enc_t;
+FLAMED_API int flamed_enc_create(int ngf, int n_down, const int* ratios, int out_channels, int dtype, flamed_enc_t* out);
+FLAMED_API int flamed_enc_destroy(flamed_enc_t h);
+FLAMED_API int flamed_enc_num_weights(flamed_enc_t h);
+FLAMED_API int flamed_enc_load(flamed_enc_t h, const float* const* weights, int n_weights, hipStream_t stream);
+/* Output frames for an n-sample input (Conv1d length arithmetic at every stride); -1 for a bad handle. */
+FLAMED_API int flamed_enc_out_len(flamed_enc_t h, int n);
+FLAMED_API size_t flamed_enc_workspace_size(flamed_enc_t h, int B, int n);
+/* wav: (B, n) fp32 (the reference's (B, 1, n)); out: (B, out_channels, flamed_enc_out_len(n)) fp32. */
+FLAMED_API int flamed_enc_encode(flamed_enc_t h, const float* wav, int B, int n, float* out, void* ws, size_t ws_bytes,
+                                 int use_graph, hipStream_t stream);
 
 #ifdef __cplusplus
 }
