@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--splitk-max", type=int, default=None, help="flamed_tune splitk_max")
     ap.add_argument("--dup-class", type=int, default=None, help="ablation: flamed_tune dup_class")
     ap.add_argument("--small-stages", type=int, default=None, help="flamed_tune small_stages (3, 5, 7)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary rows (PVA flow + LR, FaCodec decode / prompt encode, end-to-end RTF)")
     return ap.parse_args()
 
 
@@ -83,6 +85,82 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int):
     if cls == 7:
         return M * H * 4 + stats + 3 * C * H * es + M * 3 * C * 4, 2 * M * 3 * C * H, 1
     return M * 3 * C * 4 + 2 * M * C * 4, 4 * M * C, 1
+
+
+def _time_ms(fn, dev, reps=5, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def secondary_measurements(dev, nfe):
+    """The other §8 hot-path rows on the GPU, B = 1 (seeded random weights, synthetic inputs):
+    PVA duration/silence flow + length regulator (a8-a10), FaCodec decode (a11-a13) and prompt encode
+    (f3), and the end-to-end Flamed.sample_batch RTF in both reference definitions (a14/a15)."""
+    from flamed.models.synthesizer.pva import PVA
+    from flamed.utils.random_ckpt import codec_models, load_yaml
+    from flamed.utils.seeded_init import fill_state_dict, randomize_module
+    out = {}
+    g = torch.Generator().manual_seed(7)
+    prior_cfg = load_yaml("prior.yaml")
+    pva = PVA(prior_cfg["variance_adaptor"]).eval()
+    randomize_module(pva, 20251205)
+    pva = pva.to(dev)
+    enc_m, dec = codec_models(load_yaml("codec.yaml"))
+    dec.load_state_dict(fill_state_dict(dec.state_dict(), 20251205))
+    enc_m.load_state_dict(fill_state_dict(enc_m.state_dict(), 20251205))
+    dec, enc_m = dec.eval().to(dev), enc_m.eval().to(dev)
+    from flamed import Flamed
+    m = Flamed({"prior_generator": prior_cfg, "prob_generator": load_yaml("prob.yaml")}).eval()
+    m.load_state_dict(fill_state_dict(m.state_dict(), 20251205))
+    m = m.to(dev)
+    with torch.inference_mode():
+        L, nfe_d = 60, 64
+        enc = torch.randn(1, L, 192, generator=g).to(dev)
+        src_len = torch.tensor([L], device=dev)
+        mask = torch.zeros(1, L, dtype=torch.bool, device=dev)
+        ms = _time_ms(lambda: pva.sample(enc, src_len, mask, nfe=nfe_d, temperature=0.3), dev)
+        out["pva_flow_lr"] = {"ms": round(ms, 3), "phonemes": L, "nsteps_durgen": nfe_d,
+                              "us_per_net_eval": round(ms * 1e3 / (2 * nfe_d), 2), "dtype": "f32 (exact MFMA)"}
+        T = 400
+        lat = torch.randn(1, 256, T, generator=g).to(dev)
+        spk = torch.randn(1, 256, generator=g).to(dev)
+        ms = _time_ms(lambda: dec.inference(lat, spk), dev)
+        out["facodec_decode"] = {"ms": round(ms, 3), "frames": T, "samples": T * 200,
+                                 "samples_per_s": round(T * 200 / ms * 1e3, 1), "rtf": round(ms / 1e3 / (T / 80), 6),
+                                 "dtype": dec.hip_dtype}
+        wav = (0.1 * torch.randn(1, 1, 48000, generator=g)).to(dev)
+        ms = _time_ms(lambda: enc_m(wav), dev)
+        out["facodec_prompt_encode"] = {"ms": round(ms, 3), "samples": 48000, "dtype": enc_m.hip_dtype}
+        # end to end: Flamed.sample_batch (prior transformer + PVA + cond fold + denoiser) + decode
+        phon = torch.randint(1, 300, (1, L), generator=g).to(dev)
+        z = enc_m(wav)
+        _, codes, _, _, timbre = dec(z, eval_vq=False, vq=True)
+        prompts = codes.permute(1, 0, 2).contiguous()
+        res = {}
+
+        def run():
+            torch.manual_seed(0)
+            res["o"] = m.sample_batch(phonemes=phon, src_lens=torch.tensor([L], device=dev), prompts=prompts,
+                                      timbres=timbre, codec_decoder=dec, nsteps_durgen=nfe_d, nsteps_denoiser=nfe)
+        total_ms = _time_ms(run, dev, reps=3, warm=1)
+        o = res["o"]
+        frames = int((~o["tgt_mask"]).sum().item())
+        audio_s = o["wav"].shape[-1] / 16000.0
+        t_sb = float(o["time"])
+        out["end_to_end"] = {
+            "frames": frames, "audio_s": round(audio_s, 3), "phonemes": L, "prompt_frames": int(prompts.shape[-1]),
+            "nsteps_durgen": nfe_d, "nsteps_denoiser": nfe,
+            "sample_batch_ms": round(t_sb * 1e3, 3), "with_decode_ms": round(total_ms, 3),
+            "rtf_metadata_mode": round(t_sb / audio_s, 5),
+            "rtf_with_decode": round(total_ms / 1e3 / audio_s, 5),
+            "note": "random-init weights: the utterance length T comes from the seeded duration flow"}
+    return out
 
 
 def main():
@@ -210,6 +288,13 @@ def main():
                          f"({tk:.2f} s), extrapolated to the full solve ({solve_s:.2f} s)",
                "cpu": platform.processor() or platform.machine()}
 
+    secondary = None
+    if rank == 0 and world == 1 and not args.no_secondary:
+        try:
+            secondary = secondary_measurements(dev, nfe)
+        except Exception as e:  # reported, never fatal for the headline line
+            secondary = {"error": f"{type(e).__name__}: {e}"}
+
     audio_s = T * 200 / 16000.0
     value = world * B * T / sec
     line = {
@@ -226,6 +311,7 @@ def main():
         "kernels": [{k: v for k, v in kk.items() if k not in ("bytes", "flops")} for kk in kernels],
         "cpu_baseline": cpu,
         "finite": finite,
+        "secondary": secondary,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

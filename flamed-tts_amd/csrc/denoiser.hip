@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   }
   float w[KS];
 #pragma unroll
-  for (int j = 0; j < KS; ++j) w[j] = dww[(size_t)c * KS + j];
+  for (int j = 0; j < KS; ++j) w[j] = dww[(size_t)j * H + c];  // tap-major (KS, H) copy: coalesced
   const float bias = dwb[c];
   // one modulation row for the whole utterance (sampling path): stage alpha/beta once
   const bool uni = ((size_t)b * T) / mod.div == ((size_t)b * T + T - 1) / mod.div;
@@ -642,6 +642,14 @@ __global__ void tfreq_kernel(const float* __restrict__ t, int R, int dim, float*
   F[idx] = j < half ? cosf(a) : sinf(a);
 }
 
+// depthwise taps (H, 1, KS) -> tap-major (KS, H), so a wave's 64 channels read one contiguous line per tap
+__global__ void taps_t_kernel(const float* __restrict__ src, float* __restrict__ dst, int H, int KS) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)H * KS) return;
+  const int c = i / KS, j = i - (size_t)c * KS;
+  dst[(size_t)j * H + c] = src[i];
+}
+
 __global__ void cast_kernel_bf16(const float* __restrict__ src, bf16* __restrict__ dst, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = (bf16)src[i];
@@ -795,6 +803,8 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   for (int i = 0; i < NB; ++i) o_blk[i] = take(es * 4ull * H * H);
   size_t o_fin = take(es * 2ull * H * H);
   size_t o_out = take(es * (size_t)C * 3 * H);
+  std::vector<size_t> o_dw(NB + 1);
+  for (int i = 0; i <= NB; ++i) o_dw[i] = take(4ull * KS * H);
   if (d->dev) { FL_HIP(hipFree(d->dev)); d->dev = nullptr; }
   FL_HIP(hipMalloc(&d->dev, off));
   d->dev_bytes = off;
@@ -833,7 +843,9 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     TRY(cast(ob + 2 * es * H * H, bw[14], (size_t)H * H));
     TRY(cast(ob + 3 * es * H * H, bw[16], (size_t)H * H));
     B.w2 = base + ob; B.w3 = base + ob + es * H * H; B.m0 = base + ob + 2 * es * H * H; B.m2 = base + ob + 3 * es * H * H;
-    B.lnw = bw[2]; B.lnb = bw[3]; B.dww = bw[4]; B.dwb = bw[5]; B.gnw = bw[6]; B.gnb = bw[7];
+    hipLaunchKernelGGL(taps_t_kernel, dim3((H * KS + 255) / 256), dim3(256), 0, st, bw[4], reinterpret_cast<float*>(base + o_dw[i]), H, KS);
+    FL_LAUNCH_CHECK();
+    B.lnw = bw[2]; B.lnb = bw[3]; B.dww = reinterpret_cast<float*>(base + o_dw[i]); B.dwb = bw[5]; B.gnw = bw[6]; B.gnb = bw[7];
     B.b2 = bw[9]; B.b3 = bw[11]; B.lnmw = bw[12]; B.lnmb = bw[13]; B.mb0 = bw[15]; B.mb2 = bw[17];
   }
   {
@@ -841,7 +853,9 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     TRY(cpy(o_adaw + 4ull * (size_t)NB * 6 * H * H, fw[0], 5ull * H * H));
     TRY(cpy(o_adab + 4ull * (size_t)NB * 6 * H, fw[1], 5ull * H));
     DenBlockW& F = d->fin;
-    F.dww = fw[2]; F.dwb = fw[3]; F.gnw = fw[4]; F.gnb = fw[5];
+    hipLaunchKernelGGL(taps_t_kernel, dim3((H * KS + 255) / 256), dim3(256), 0, st, fw[2], reinterpret_cast<float*>(base + o_dw[NB]), H, KS);
+    FL_LAUNCH_CHECK();
+    F.dww = reinterpret_cast<float*>(base + o_dw[NB]); F.dwb = fw[3]; F.gnw = fw[4]; F.gnb = fw[5];
     TRY(cast(o_fin, fw[6], (size_t)H * H)); F.b2 = fw[7];
     TRY(cast(o_fin + es * H * H, fw[8], (size_t)H * H)); F.b3 = fw[9];
     F.w2 = base + o_fin; F.w3 = base + o_fin + es * H * H;
@@ -854,7 +868,6 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     d->wout = base + o_out; d->bout = fw[11];
   }
 #undef TRY
-  (void)KS;
   if (!d->scnt) FL_HIP(hipMalloc(&d->scnt, sizeof(int) * Den::kSplitCounters));
   FL_HIP(hipMemsetAsync(d->scnt, 0, sizeof(int) * Den::kSplitCounters, st));
   if (!d->gcnt) FL_HIP(hipMalloc(&d->gcnt, sizeof(int) * Den::kGnCounters));

@@ -79,11 +79,15 @@ __device__ __forceinline__ void row_stats_from_partials(const float* __restrict_
   rstd = 1.0f / sqrtf(var + eps);
 }
 
-// Byte offset of 16-B chunk `c` of LDS tile row `r`: rows of KCH chunks, chunk index XOR (r & 7).
-// For KCH = 8 the ds_read_b128 fragment pattern (lane&15 -> row, lane>>4 -> chunk) is conflict-free.
+// Byte offset of 16-B chunk `c` of LDS tile row `r` (128-B rows, two per 256-B bank line).  A 16-lane
+// ds_read_b128 group reads rows r0..r0+15 at one chunk; its 16-B slot is (r & 1) * 8 + (c ^ ((r >> 1) & 7)),
+// distinct for all 16 rows -> conflict-free.  (XOR with r & 7 put rows r and r + 8 in the same slot: a
+// 2-way conflict on every fragment read, SQ_LDS_BANK_CONFLICT.)  The commit writes (two rows x 8 chunks
+// per 16 lanes) stay conflict-free.
 template <int KCH>
 __device__ __forceinline__ int lds_off(int r, int c) {
-  return r * (KCH * 16) + ((c ^ (r & (KCH - 1) & 7)) << 4);
+  static_assert(KCH == 8, "128-B rows");
+  return r * (KCH * 16) + ((c ^ ((r >> 1) & 7)) << 4);
 }
 
 // NSTAGE = 2: LDS double buffer, loads issued one K-step ahead.

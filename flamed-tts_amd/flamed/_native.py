@@ -121,3 +121,13 @@ class Workspace:
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != torch.device(device):
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
         return self.buf
+
+
+def tensor_version(t: torch.Tensor) -> int:
+    """In-place version counter of a weight tensor, used to detect weight updates between calls.
+    Inference tensors (created under torch.inference_mode) have no counter; they are reported as -1
+    and identified by their data pointer alone."""
+    try:
+        return t._version
+    except RuntimeError:
+        return -1

@@ -335,7 +335,7 @@ class FacDecoderHIP:
 
     def _ensure(self, dev):
         params = fac_weight_list(self.dec)
-        sig = tuple((p.data_ptr(), p._version) for p in params) + (str(dev),)
+        sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(dev),)
         if sig == self._sig:
             return
         L = nat.lib()
@@ -417,7 +417,7 @@ class EncoderHIP:
 
     def _ensure(self, dev):
         params = enc_weight_list(self.enc)
-        sig = tuple((p.data_ptr(), p._version) for p in params) + (str(dev),)
+        sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(dev),)
         if sig == self._sig:
             return
         L = nat.lib()

@@ -337,7 +337,7 @@ class DenoiserHIP:
 
     def _ensure(self, device):
         params = denoiser_weight_list(self.den)
-        sig = tuple((p.data_ptr(), p._version) for p in params) + (str(device),)
+        sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(device),)
         if sig == self._sig and self.handle is not None:
             return
         L = nat.lib()

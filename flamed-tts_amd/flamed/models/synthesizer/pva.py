@@ -236,7 +236,7 @@ class PvaHIP:
     def _ensure(self, dev):
         gens = (self.pva.duration_generator, self.pva.sil_generator)
         params = [w for g in gens for w in g.hip_weights()]
-        sig = tuple((p.data_ptr(), p._version) for p in params) + (str(dev),)
+        sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(dev),)
         if sig == self._sig:
             return
         L = nat.lib()

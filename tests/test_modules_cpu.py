@@ -133,3 +133,14 @@ def test_conv1d_gemm_matches_conv1d():
         out = conv1d_gemm(x, w, b, s, p, d)
         assert out.shape == ref.shape
         assert torch.allclose(out, ref, atol=1e-5, rtol=1e-5)
+
+
+def test_tensor_version_handles_inference_tensors():
+    from flamed import _native as nat
+    t = torch.zeros(3)
+    v0 = nat.tensor_version(t)
+    t.add_(1)
+    assert nat.tensor_version(t) == v0 + 1
+    with torch.inference_mode():
+        u = torch.zeros(3)
+    assert nat.tensor_version(u) == -1

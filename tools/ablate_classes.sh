@@ -5,7 +5,7 @@ set -euo pipefail
 TAG=$1; shift
 mkdir -p gpurun_out/$TAG
 for c in -1 0 1 2 3 4 5 6 7 8; do
-  timeout -k 10 240 python bench.py --no-cpu-baseline --kernel-iters 1 --dup-class $c "$@" > gpurun_out/$TAG/d$c.json 2> gpurun_out/$TAG/d$c.err
+  timeout -k 10 240 python bench.py --no-cpu-baseline --no-secondary --kernel-iters 1 --dup-class $c "$@" > gpurun_out/$TAG/d$c.json 2> gpurun_out/$TAG/d$c.err
 done
 python - gpurun_out/$TAG "$@" <<'PY'
 import json, sys

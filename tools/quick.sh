@@ -14,9 +14,11 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 ks = " ".join(f"{k['name'][:10]}={k['us']}" for k in d["kernels"])
 print(f"B={d['config']['batch_per_gpu']} ms/solve={d['ms_per_step']:.2f} frames/s={d['value']:.0f} | {ks}")
+if d.get("secondary"):
+    print("  secondary:", json.dumps(d["secondary"]))
 PY
 }
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/$TAG/b1.json 2> gpurun_out/$TAG/b1.err
 summ gpurun_out/$TAG/b1.json
-timeout -k 10 300 python bench.py --no-cpu-baseline --batch 64 --steps 3 --warmup 1 > gpurun_out/$TAG/b64.json 2> gpurun_out/$TAG/b64.err
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --batch 64 --steps 3 --warmup 1 > gpurun_out/$TAG/b64.json 2> gpurun_out/$TAG/b64.err
 summ gpurun_out/$TAG/b64.json

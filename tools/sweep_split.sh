@@ -7,7 +7,7 @@ VARIANTS=$1; shift
 mkdir -p gpurun_out/$TAG
 for v in $VARIANTS; do
   t=${v%%:*}; m=${v##*:}
-  timeout -k 10 240 python bench.py --no-cpu-baseline --splitk-target $t --splitk-max $m "$@" > gpurun_out/$TAG/b_${t}_${m}.json 2> gpurun_out/$TAG/b_${t}_${m}.err
+  timeout -k 10 240 python bench.py --no-cpu-baseline --no-secondary --splitk-target $t --splitk-max $m "$@" > gpurun_out/$TAG/b_${t}_${m}.json 2> gpurun_out/$TAG/b_${t}_${m}.err
   python - gpurun_out/$TAG/b_${t}_${m}.json "$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

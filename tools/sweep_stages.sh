@@ -4,7 +4,7 @@ set -euo pipefail
 TAG=$1; shift
 mkdir -p gpurun_out/$TAG
 for v in 3 5 7; do
-  timeout -k 10 240 python bench.py --no-cpu-baseline --small-stages $v "$@" > gpurun_out/$TAG/s$v.json 2> gpurun_out/$TAG/s$v.err
+  timeout -k 10 240 python bench.py --no-cpu-baseline --no-secondary --small-stages $v "$@" > gpurun_out/$TAG/s$v.json 2> gpurun_out/$TAG/s$v.err
   python - gpurun_out/$TAG/s$v.json $v <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
