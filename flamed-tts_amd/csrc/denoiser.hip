@@ -12,6 +12,7 @@
 // AdaLN (depends only on t and the speaker) is precomputed for every (step, utterance) at once.
 #include "flamed_hip.h"
 #include "gemm.hpp"
+#include "gemm_dma.hpp"
 
 #include <string>
 #include <vector>
@@ -26,6 +27,27 @@ static int g_tune_split_max = 4;
 // Ablation (flamed_tune "dup_class"): launch every kernel of this class twice per step, so the solve
 // time delta is the class's in-graph cost.  -1 = off.
 static int g_dup_class = -1;
+// Bumped by every flamed_tune call: a captured solve graph built under other settings is re-captured.
+static int g_tune_epoch = 0;
+// flamed_tune "dma": 1 routes small-M bf16 GEMMs whose A operand is bf16 through the LDS-DMA pipeline
+// (gemm_dma.hpp), 2 also those with fp32 (transforming) A loaders, 0 (default) = gemm_kernel only.
+// In-graph per-launch costs at B = 1 (profiles/r01_dma_ab.txt): no gain for 1, a loss for 2.
+static int g_use_dma = 0;
+static int g_noctr = 0;  // diagnostic: kernels ignore the device step counter (wrong modulation rows)
+
+// Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
+template <typename DT, class AL, class EP>
+static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
+                    hipStream_t st) {
+  if constexpr (std::is_same<DT, bf16>::value) {
+    // measured (B = 1, T = 400, stamps + in-graph dup timing): the DMA ring shortens the K loop of
+    // the bf16-A GEMMs; for fp32-A loaders its LDS->LDS transform pass costs more LDS bandwidth than
+    // the ring saves, and at mid M its ~150 KB of LDS drops residency to one block per CU
+    if (c == kCfgSmall && (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)))
+      return launch_gemm_dma<32, 64>(al, W, ldw, ep, M, N, K, st);
+  }
+  return wide_a ? launch_gemm_auto<DT>(c, kWideA, al, W, ldw, ep, M, N, K, st) : launch_gemm_auto<DT>(c, al, W, ldw, ep, M, N, K, st);
+}
 // Diagnostic stamps (FL_STAMPS builds): kernel class whose launches point fl_stamp_buf at g_stamp_dev.
 static int g_stamp_class = -1;
 static unsigned long long* g_stamp_dev = nullptr;
@@ -77,6 +99,28 @@ struct LoadLNMod {
   const float* __restrict__ lnb;
   int kdim;  // K: columns staged per vector
   static constexpr int EPC = DTraits<DT>::EPC;
+  static constexpr int kSrcBytes = 4;
+  __device__ const char* src_row(int m) const { return reinterpret_cast<const char*>(x + (size_t)m * ld); }
+  // DMA-path transform: row statistics and the vector slot are per-thread constants of the K loop;
+  // per K-step only alpha/beta (two float4 pairs from LDS) change.
+  struct XRow { float mean, rstd; int voff, m; bool use; };
+  __device__ XRow xrow(int m, const float* st, const float*, bool use, int bm) const {
+    const int slot = use ? m / mod.div - bm / mod.div : 0;
+    return XRow{st[2 * (m - bm)], st[2 * (m - bm) + 1], 2 * slot * kdim, m, use};
+  }
+  template <typename D, typename R>
+  __device__ u32x4 xform(const XRow& xr, const R& r, int k, const float* st, const float* vec, int bm) const {
+    if (!xr.use) return finish_v<D>(r, xr.m, k, st, vec, false, bm);
+    const float* va = vec + xr.voff + k;
+    const float* vb = va + kdim;
+    const float4 a0 = ld4(va), a1 = ld4(va + 4), b0 = ld4(vb), b1 = ld4(vb + 4);
+    const float al[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float be[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float o[EPC];
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) o[j] = ((r.v[j] - xr.mean) * xr.rstd) * al[j] + be[j];
+    return pack_chunk<D>(o);
+  }
   static constexpr int kVec = 4;  // 2 slots x (alpha, beta)
   struct Raw { float v[EPC]; };
   static constexpr int stat_rows(int BM) { return BM; }
@@ -538,6 +582,27 @@ struct LoadGN {
   const float* __restrict__ gnb;
   int T;
   static constexpr int EPC = DTraits<DT>::EPC;
+  static constexpr int kSrcBytes = 4;
+  __device__ const char* src_row(int m) const { return reinterpret_cast<const char*>(D + (size_t)m * H); }
+  struct XRow { int voff, m; bool use; };
+  __device__ XRow xrow(int m, const float*, const float*, bool use, int bm) const {
+    return XRow{use ? 2 * (m / T - bm / T) * H : 0, m, use};
+  }
+  template <typename Dt, typename R>
+  __device__ u32x4 xform(const XRow& xr, const R& r, int k, const float* st, const float* vec, int bm) const {
+    if (!xr.use) return finish_v<Dt>(r, xr.m, k, st, vec, false, bm);
+    const float* mu = vec + xr.voff + k;
+    const float* sc = mu + H;
+    const float* bb = vec + 4 * H + k;
+    const float4 m0 = ld4(mu), m1 = ld4(mu + 4), s0 = ld4(sc), s1 = ld4(sc + 4), c0 = ld4(bb), c1 = ld4(bb + 4);
+    const float mv[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+    const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    float o[EPC];
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) o[j] = (r.v[j] - mv[j]) * sv[j] + cv[j];
+    return pack_chunk<Dt>(o);
+  }
   static constexpr int kVec = 5;  // 2 slots x (mean, scale) + bias
   struct Raw { float v[EPC]; };
   static constexpr int stat_rows(int) { return 0; }
@@ -693,7 +758,7 @@ struct Den {
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
-  int g_B = -1, g_T = -1, g_nfe = -1;
+  int g_B = -1, g_T = -1, g_nfe = -1, g_epoch = -1;
   const void *g_xt = nullptr, *g_mods = nullptr, *g_ws = nullptr;
   int* ctr = nullptr;  // device Euler step counter for graph replay
   int* scnt = nullptr;  // split-K tile counters (zeroed at load; every launch leaves them zero)
@@ -942,7 +1007,7 @@ template <typename DT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
                          const DenWs& w, int* ctr, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
-  const StepOff so{ctr, (long long)B * MS};
+  const StepOff so{g_noctr ? nullptr : ctr, (long long)B * MS};
   SplitCtx sctx;
   sctx.slab = w.SL; sctx.slab_floats = w.SLn; sctx.cnt = d->scnt; sctx.cnt_n = Den::kSplitCounters;
   sctx.target = g_tune_split_target; sctx.max_split = g_tune_split_max;
@@ -956,7 +1021,7 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (g_stamp_class >= 0) stamp_select(cls, st); TRY(x); if (g_dup_class == (cls)) TRY(x); kt_mark(cls, st); } while (0)
-  K_(0, (launch_gemm_auto<DT>(cfg, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
+  K_(0, (den_gemm<DT>(cfg, false, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
@@ -964,14 +1029,14 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
     K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
     K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
-    K_(3, (launch_gemm_auto<DT>(cfg, kWideA, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
+    K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
                                         EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
-    K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+    K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
                                         EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
                                         M, H, H, st)));
-    K_(5, (launch_gemm_auto<DT>(cfg, kWideA, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
+    K_(5, (den_gemm<DT>(cfg, true, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
                                         EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
-    K_(6, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
+    K_(6, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
                                         EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
@@ -980,11 +1045,11 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   const DenBlockW& F = d->fin;
   K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
   K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
-  K_(3, (launch_gemm_auto<DT>(cfg, kWideA, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
-  K_(4, (launch_gemm_auto<DT>(cfg, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
+  K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                       EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
                                       M, H, H, st)));
-  K_(7, (launch_gemm_auto<DT>(cfg, kWideA, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
+  K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
                                       EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
   {
     size_t n = (size_t)M * C;
@@ -1067,7 +1132,8 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   const int G = graph_chunk(nfe);
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // the graph bakes in dt = 1/nfe, so nfe is part of the key
-  const bool hit = d->gexec && d->g_B == B && d->g_T == T && d->g_nfe == nfe && d->g_xt == xt && d->g_mods == mods && d->g_ws == ws;
+  const bool hit = d->gexec && d->g_B == B && d->g_T == T && d->g_nfe == nfe && d->g_xt == xt && d->g_mods == mods && d->g_ws == ws &&
+                   d->g_epoch == g_tune_epoch;
   if (!hit) {
     if (d->gexec) { FL_HIP(hipGraphExecDestroy(d->gexec)); d->gexec = nullptr; }
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
@@ -1081,7 +1147,7 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     hipError_t ie = hipGraphInstantiate(&d->gexec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     FL_HIP(ie);
-    d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
+    d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_epoch = g_tune_epoch; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
   }
   FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
   for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
@@ -1105,14 +1171,76 @@ FLAMED_API int flamed_stamp_buffer(void* buf) {
 
 FLAMED_API int flamed_tune(const char* key, int value) {
   FL_REQUIRE(key, "flamed_tune: null key");
+  ++g_tune_epoch;
   const std::string k(key);
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "noctr") { g_noctr = value; return kOk; }
+  if (k == "dma") { FL_REQUIRE(value >= 0 && value <= 2, "flamed_tune: dma in {0, 1, 2}"); g_use_dma = value; return kOk; }
   if (k == "small_stages") { FL_REQUIRE(value == 3 || value == 5 || value == 7, "flamed_tune: small_stages must be 3, 5 or 7"); g_small_stages = value; return kOk; }
   if (k == "dup_class") { FL_REQUIRE(value >= -1 && value < FLAMED_DEN_KERNEL_CLASSES, "flamed_tune: dup_class in [-1, %d)", FLAMED_DEN_KERNEL_CLASSES); g_dup_class = value; return kOk; }
-  if (k == "splitk_max") { FL_REQUIRE(value == 1 || value == 2 || value == 4 || value == 8 || value == 16, "flamed_tune: splitk_max must be a power of two <= 16"); g_tune_split_max = value; return kOk; }
+  if (k == "splitk_max") { FL_REQUIRE(value == 1 || value == 2 || value == kMaxSplit, "flamed_tune: splitk_max must be 1, 2 or 4"); g_tune_split_max = value; return kOk; }
   set_error("flamed_tune: unknown key '%s'", key);
   return kBadArg;
+}
+
+// In-graph per-launch cost of every kernel class: a graph of `steps` Euler steps (dt = 0) is timed
+// as captured and again with one class launched twice per occurrence (flamed_tune dup_class); the
+// difference over the number of duplicated launches is what one launch of the class costs inside a
+// replayed step (dispatch included, event overhead excluded).  ms_out[c] per launch, ms_out[kClasses]
+// = one whole step.
+FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
+                                             size_t ws_bytes, int reps, float* ms_out, hipStream_t st) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && d->dev && xt && mods && ws && ms_out && reps > 0, "flamed_den_time_kernels_graph: bad args");
+  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
+    set_error("flamed_den_time_kernels_graph: workspace too small");
+    return kNoWorkspace;
+  }
+  constexpr int kSteps = 4;
+  if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  FL_HIP(hipEventCreate(&e0));
+  FL_HIP(hipEventCreate(&e1));
+  const int saved_dup = g_dup_class;
+  auto timed = [&](int dup, float* ms) -> int {
+    g_dup_class = dup;
+    FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
+    int rc = kOk;
+    for (int i = 0; i < kSteps && rc == kOk; ++i) rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+    g_dup_class = saved_dup;
+    if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+    FL_HIP(e);
+    hipGraphExec_t ex;
+    hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    FL_HIP(ie);
+    FL_HIP(hipGraphLaunch(ex, st));
+    FL_HIP(hipGraphLaunch(ex, st));
+    FL_HIP(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; ++r) FL_HIP(hipGraphLaunch(ex, st));
+    FL_HIP(hipEventRecord(e1, st));
+    FL_HIP(hipEventSynchronize(e1));
+    FL_HIP(hipEventElapsedTime(ms, e0, e1));
+    *ms /= (float)(reps * kSteps);
+    (void)hipGraphExecDestroy(ex);
+    return kOk;
+  };
+  float base = 0.f;
+  int rc = timed(-1, &base);
+  const int NB = d->NB;
+  const int per_step[FLAMED_DEN_KERNEL_CLASSES] = {1, NB + 1, 0, NB + 1, NB + 1, NB, NB, 1, 1};
+  for (int c = 0; c < FLAMED_DEN_KERNEL_CLASSES && rc == kOk; ++c) {
+    float t = base;
+    if (per_step[c] > 0 && (c != 2 || d->gcnt == nullptr)) rc = timed(c, &t);
+    ms_out[c] = per_step[c] > 0 ? (t - base) / (float)per_step[c] : 0.f;
+  }
+  ms_out[FLAMED_DEN_KERNEL_CLASSES] = base;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
 }
 
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,

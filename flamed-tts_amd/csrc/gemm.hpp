@@ -49,8 +49,9 @@ struct GemmSmem {
 // counter (agent-scope release before, acquire after — cdna_hip_programming.md §5 "Projection GEMM
 // at M = 256" item 2); the last arriver sums all `n` slabs in slice order (deterministic), resets the
 // counter and runs the fused epilogue.  n == 1: no split.
+constexpr int kMaxSplit = 4;
 struct SplitK {
-  int n;
+  int n;  // 1..kMaxSplit
   float* slab;  // tiles x n x BM x BN floats
   int* cnt;     // tiles counters, zero between launches
 };
@@ -306,38 +307,50 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
 
   FL_STAMP(2);
   // ---------------- split-K: slab hand-off, the last arriver reduces ----------------
+  // Write-through form (cdna_hip_programming.md §6 Guideline 16, R1 + sc1 consume): every slab store
+  // is a 16-B sc1 buffer store, every storing wave drains (vmcnt 0) before the block barrier, one lane
+  // takes a relaxed agent-scope ticket; the last arriver reads ALL slabs with sc1 loads.  No release
+  // fence (buffer_wbl2 writes back the XCD L2's dirty lines: ~6 us after a kernel that dirtied it) and
+  // no acquire (sc1 loads bypass this CU's L1).
   if (sk.n > 1) {
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
     float* slabs = sk.slab + (size_t)tile * sk.n * (BM * BN);
-    float* mine = slabs + (size_t)blockIdx.z * (BM * BN);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, sk.n * BM * BN * 4, 0x00020000);
+    const int mine = blockIdx.z * (BM * BN * 4);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) *reinterpret_cast<f32x4*>(mine + ((i * FN + j) * kGemmThreads + tid) * 4) = acc[i][j];
+      for (int j = 0; j < FN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                               mine + ((i * FN + j) * kGemmThreads + tid) * 16, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int t = __hip_atomic_fetch_add(sk.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == sk.n - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sk.cnt[tile] = 0;  // ready for the next launch
-      }
+      if (last) __hip_atomic_store(sk.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
       *s_flag = last;
     }
     __syncthreads();
     if (!*s_flag) return;  // block-uniform
-    // load every slab (own included: no per-element register/load select), then sum in slice order
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keeps the sc1 loads below the ticket
+    // load all kMaxSplit slab slots unconditionally (no per-element register/load select, guide §5
+    // item 4(c)): slots >= n lie past the descriptor's range and read as zero; sum in slice order
+    u32x4 q[FM][FN][kMaxSplit];
+#pragma unroll
+    for (int z = 0; z < kMaxSplit; ++z)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          q[i][j][z] = __builtin_amdgcn_raw_buffer_load_b128(rs, z * (BM * BN * 4) + ((i * FN + j) * kGemmThreads + tid) * 16, 0, 16);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const float* p = slabs + ((i * FN + j) * kGemmThreads + tid) * 4;
-        f32x4 sum = *reinterpret_cast<const f32x4*>(p);
-        for (int z = 1; z < sk.n; ++z) sum += *reinterpret_cast<const f32x4*>(p + (size_t)z * (BM * BN));
+        f32x4 sum = __builtin_bit_cast(f32x4, q[i][j][0]);
+#pragma unroll
+        for (int z = 1; z < kMaxSplit; ++z) sum += __builtin_bit_cast(f32x4, q[i][j][z]);
         acc[i][j] = sum;
       }
   }
@@ -429,6 +442,9 @@ struct LoadPlain {
   const DT* __restrict__ p;
   int ld;
   struct Raw { u32x4 v; };
+  static constexpr int kSrcBytes = sizeof(DT);  // DMA path: raw source rows, no transform when == 2
+  __device__ const char* src_row(int m) const { return reinterpret_cast<const char*>(p + (size_t)m * ld); }
+  struct XRow {};  // unused: bf16 rows are consumed in place
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
   __device__ Raw issue(int m, int k) const { return Raw{*reinterpret_cast<const u32x4*>(p + (size_t)m * ld + k)}; }
@@ -441,6 +457,12 @@ struct LoadF32 {
   const float* __restrict__ p;
   int ld;
   struct Raw { float v[DTraits<DT>::EPC]; };
+  static constexpr int kSrcBytes = 4;
+  __device__ const char* src_row(int m) const { return reinterpret_cast<const char*>(p + (size_t)m * ld); }
+  // DMA-path transform (gemm_dma.hpp): per-thread row context hoisted out of the K loop
+  struct XRow {};
+  __device__ XRow xrow(int, const float*, const float*, bool, int) const { return {}; }
+  template <typename D> __device__ u32x4 xform(const XRow&, const Raw& r, int, const float*, const float*, int) const { return pack_chunk<D>(r.v); }
   static constexpr int stat_rows(int) { return 0; }
   __device__ void prologue(int, int, int, float*) const {}
   __device__ Raw issue(int m, int k) const {

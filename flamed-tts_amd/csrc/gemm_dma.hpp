@@ -1,0 +1,357 @@
+// LDS-DMA pipelined bf16 GEMM for the latency-bound small/mid-M regime (denoiser at B*T < 8192 rows).
+//
+// Why a second main loop: the register-staged ring of gemm_kernel is serialised by hipcc — the
+// staging VGPRs of the next K-steps are reused as ds_read destinations and control-flow joins flush
+// the wait counters, so the emitted loop waits `s_waitcnt vmcnt(0)` every K-step (read in the .s of
+// the 32x64 3-stage instantiation) and only one K-step of operand traffic is ever in flight.  Here
+// every global operand byte travels by `global_load_lds_dwordx4` straight into an NS-deep LDS ring
+// (no VGPR destinations, so nothing for the compiler to wait on), completion is tracked with an
+// explicit counted `s_waitcnt vmcnt(ahead * G)` and raw `s_barrier`s (cdna_hip_programming.md §5
+// "Pipelining across barriers"), and NS-1 K-steps stay in flight.
+//
+// Operand images (128-B bf16 rows, XOR-swizzled exactly as lds_off<8>): glds writes a wave's 64 lanes
+// lane-linearly, so the swizzle is applied to each lane's SOURCE chunk (an involution) and the
+// fragment reads use lds_off (guide §5.4 rule 21).  An A loader whose source is fp32 (LayerNorm /
+// GroupNorm / conversion prologues, kSrcBytes == 4) has its raw 256-B rows staged linearly; one
+// LDS->LDS pass per K-step applies the loader's own finish/finish_v transform into a double-buffered
+// bf16 image.  The fused prologue (row statistics, per-column vectors) and epilogue policies are the
+// gemm_kernel ones, unchanged.
+#pragma once
+#include "gemm.hpp"
+
+namespace fl {
+
+// One wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane `g` to LDS [lds, lds + 1024).  Written
+// as inline asm (M0 saved and restored inside the statement, guide §5.7): hipcc does not see the DMA,
+// so it neither drains it before every ds_read (it cannot prove the reads do not alias the DMA target
+// and emits vmcnt(0) — read in the .s of the builtin form) nor at barriers; completion is ours to count.
+__device__ __forceinline__ void glds16(const void* g, char* lds) {
+  const unsigned l = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(lds)));
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(l)
+               : "memory");
+}
+
+// s_waitcnt vmcnt(n * G) for a runtime n in [0, NMAX] (the count is an instruction immediate).
+template <int G, int NMAX>
+__device__ __forceinline__ void wait_vm(int n) {
+  static_assert(NMAX * G <= 63, "vmcnt immediate is 6 bits");
+#define FL_WV(i) \
+  case i:        \
+    if constexpr (i <= NMAX) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(i * G) : "memory"); \
+    break;
+  switch (n) {
+    FL_WV(0) FL_WV(1) FL_WV(2) FL_WV(3) FL_WV(4) FL_WV(5) FL_WV(6) FL_WV(7) FL_WV(8) FL_WV(9)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+#undef FL_WV
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int BM, int BN, int NS, class AL, class EP>
+struct DmaSmem {
+  static constexpr int AE = AL::kSrcBytes;                 // 2 (bf16 A, used in place) or 4 (fp32, transformed)
+  static constexpr bool XF = AE == 4;
+  static constexpr int A_RAW = BM * 64 * AE;               // one K-step of A source rows
+  static constexpr int W_ST = BN * 128;                    // one K-step of W rows (bf16)
+  static constexpr int STAGE = A_RAW + W_ST;
+  static constexpr int ABF = XF ? BM * 128 : 0;            // transformed bf16 A image (x2, alternating)
+  static constexpr int ring = NS * STAGE;
+  static constexpr int red = BM * 2 * 4;
+  static constexpr int body = ring + 2 * ABF > red ? ring + 2 * ABF : red;
+  static constexpr int a_stats = AL::stat_rows(BM) * 2 * 4;
+  static constexpr int e_stats = EP::stat_rows(BM) * 2 * 4;
+  static constexpr int e_vec = kevec_of<EP>::value * BN * 4;
+  static constexpr int bytes = (body + a_stats + e_stats + e_vec + 15) / 16 * 16;  // + kVec*K*4 (runtime)
+  // glds instructions per thread per K-step
+  static constexpr int GW = BN / 32;                       // W: BN rows x 8 chunks / 64 lanes / 4 waves
+  static constexpr int GA = XF ? BM / 16 : BM / 32;        // A: BM rows x (16 | 8) chunks / 64 / 4
+  static constexpr int G = GW + GA;
+};
+
+template <int BM, int BN, int NS, class AL, class EP>
+__global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf16* __restrict__ W, int ldw, EP ep,
+                                                                 int M, int N, int K) {
+  using SM = DmaSmem<BM, BN, NS, AL, EP>;
+  constexpr bool XF = SM::XF;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int BKE = 64;
+  static_assert(BM % 32 == 0 && BN % 32 == 0 && NS >= 3 && NS - 2 <= 9, "dma gemm tile");
+  static_assert(!XF || BM * 8 % kGemmThreads == 0, "transform pass: whole chunks per thread");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* a_stats = reinterpret_cast<float*>(smem + SM::body);
+  float* e_stats = a_stats + AL::stat_rows(BM) * 2;
+  float* e_vec = e_stats + EP::stat_rows(BM) * 2;
+  float* a_vec = e_vec + kevec_of<EP>::value * BN;
+  constexpr bool AV = kvec_of<AL>::value > 0;
+  constexpr bool EV = kevec_of<EP>::value > 0;
+
+  FL_STAMP(0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int bn = blockIdx.x * BN;
+  const int bm = blockIdx.y * BM;
+  const int nsteps = K / BKE;
+
+  // ---- per-lane DMA sources (K-step 0); a K-step advances every source by 128 (bf16) / 256 (fp32) B
+  const char* wsrc[SM::GW];
+#pragma unroll
+  for (int j = 0; j < SM::GW; ++j) {
+    const int r = (wave * SM::GW + j) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    wsrc[j] = reinterpret_cast<const char*>(W + (size_t)(bn + r) * ldw) + c * 16;
+  }
+  const char* asrc[SM::GA];
+#pragma unroll
+  for (int j = 0; j < SM::GA; ++j) {
+    if constexpr (XF) {  // 4 rows x 16 linear chunks per instruction
+      const int r = (wave * SM::GA + j) * 4 + (lane >> 4);
+      const int m = bm + r < M ? bm + r : M - 1;
+      asrc[j] = al.src_row(m) + (lane & 15) * 16;
+    } else {             // 8 rows x 8 swizzled chunks per instruction
+      const int r = (wave * SM::GA + j) * 8 + (lane >> 3);
+      const int m = bm + r < M ? bm + r : M - 1;
+      asrc[j] = al.src_row(m) + ((lane & 7) ^ ((r >> 1) & 7)) * 16;
+    }
+  }
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    char* st = smem + (s % NS) * SM::STAGE;
+#pragma unroll
+    for (int j = 0; j < SM::GA; ++j)
+      glds16(asrc[j] + (size_t)s * (64 * SM::AE), st + (wave * SM::GA + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < SM::GW; ++j) glds16(wsrc[j] + (size_t)s * 128, st + SM::A_RAW + (wave * SM::GW + j) * 1024);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- kPreIssue K-steps go out before the fused prologue (whose loads then overlap them, and whose
+  // waits — in-order vmcnt — drain only those), the rest of the NS-1 deep ring right after it
+  constexpr int kPreIssue = 2;
+  const int ring_n = nsteps < NS - 1 ? nsteps : NS - 1;
+  const int pre_n = ring_n < kPreIssue ? ring_n : kPreIssue;
+  for (int s = 0; s < pre_n; ++s) issue(s);
+
+  constexpr bool PRE = kpre_of<EP>::value;
+  float pre[FM][FN][4];
+  const int fr = lane & 15, fq = lane >> 4;
+  bool a_uv = false, e_uv = false;
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int m = bm + wr * WTM + i * 16 + fq * 4 + r;
+          pre[i][j][r] = ep.pre(m < M ? m : M - 1, bn + wc * WTN + j * 16 + fr);
+        }
+  }
+  if constexpr (AV) a_uv = al.prologue_v(bm, BM, M, K, a_stats, a_vec);
+  else al.prologue(bm, BM, M, a_stats);
+  if constexpr (EV) e_uv = ep.prologue_v(bm, bn, BM, BN, M, e_stats, e_vec);
+  else ep.prologue(bm, BM, M, e_stats);
+  FL_STAMP(1);
+  for (int s = pre_n; s < ring_n; ++s) issue(s);
+
+  // transform pass (fp32-source loaders): raw K-step s -> bf16 image Abf[s & 1].  A thread transforms
+  // the same rows at every K-step, so its row context (statistics, vector slot) is built once here.
+  constexpr int PR = XF ? BM * 8 / kGemmThreads : 1;
+  typename AL::XRow xr[PR];  // filled after the first barrier (the prologue's LDS writes)
+  auto transform = [&](int s) __attribute__((always_inline)) {
+    if constexpr (XF) {
+      const char* st = smem + (s % NS) * SM::STAGE;
+      char* abf = smem + SM::ring + (s & 1) * SM::ABF;
+#pragma unroll
+      for (int p = 0; p < BM * 8 / kGemmThreads; ++p) {
+        const int q = tid + p * kGemmThreads;
+        const int r = q >> 3, c = q & 7;
+        const float* row = reinterpret_cast<const float*>(st + r * 256);
+        // odd rows read their two 16-B halves in the other order: the 16 lanes of a ds_read_b128
+        // group (two rows) then hit 16 distinct slots of the 256-B bank line
+        const int h0 = (r & 1), h1 = h0 ^ 1;
+        const float4 x0 = *reinterpret_cast<const float4*>(row + c * 8 + h0 * 4);
+        const float4 x1 = *reinterpret_cast<const float4*>(row + c * 8 + h1 * 4);
+        const float4 lo = h0 ? x1 : x0, hi = h0 ? x0 : x1;
+        typename AL::Raw raw;
+        raw.v[0] = lo.x; raw.v[1] = lo.y; raw.v[2] = lo.z; raw.v[3] = lo.w;
+        raw.v[4] = hi.x; raw.v[5] = hi.y; raw.v[6] = hi.z; raw.v[7] = hi.w;
+        const u32x4 o = al.template xform<bf16>(xr[p], raw, s * BKE + c * 8, a_stats, a_vec, bm);
+        *reinterpret_cast<u32x4*>(abf + lds_off<8>(r, c)) = o;
+      }
+    }
+  };
+  auto mfma_step = [&](const char* ta, const char* tb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const u32x4*>(ta + lds_off<8>(wr * WTM + i * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const u32x4*>(tb + lds_off<8>(wc * WTN + j * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i]), __builtin_bit_cast(bf16x8, b[j]),
+                                                              acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (XF) {
+    // ---- main loop, transform one K-step ahead: at step s the A image of s is complete (transformed
+    // during step s-1), so one barrier per step orders {transform s+1 -> Abf[(s+1)&1]} against
+    // {MFMA s <- Abf[s&1]} and the DMA reissue into the slot step s-1 used.
+    wait_vm<SM::G, NS - 2>(ring_n - 1);  // K-step 0 landed (ring_n - 1 younger K-steps in flight)
+    lds_barrier();
+#pragma unroll
+    for (int p = 0; p < PR; ++p) {
+      const int r = (tid + p * kGemmThreads) >> 3;
+      const int m = bm + r < M ? bm + r : M - 1;
+      xr[p] = al.xrow(m, a_stats, a_vec, a_uv, bm);
+    }
+    transform(0);
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) {
+        const int ahead = (nsteps - 2 - s) < (NS - 3) ? (nsteps - 2 - s) : (NS - 3);
+        wait_vm<SM::G, NS - 2>(ahead);  // K-step s+1 landed
+      }
+      lds_barrier();
+      if (s + NS - 1 < nsteps) issue(s + NS - 1);  // into slot (s-1) % NS: transformed at s-2, W read at s-1
+      if (s + 1 < nsteps) transform(s + 1);
+      mfma_step(smem + SM::ring + (s & 1) * SM::ABF, smem + (s % NS) * SM::STAGE + SM::A_RAW);
+    }
+  } else {
+    // ---- main loop: wait for K-step s (counted), barrier, reissue the slot of s-1, MFMA in place
+    for (int s = 0; s < nsteps; ++s) {
+      const int ahead = (nsteps - 1 - s) < (NS - 2) ? (nsteps - 1 - s) : (NS - 2);
+      wait_vm<SM::G, NS - 2>(ahead);
+      lds_barrier();
+      if (s + NS - 1 < nsteps) issue(s + NS - 1);  // into the slot K-step s-1 used (all waves are past it)
+      const char* st = smem + (s % NS) * SM::STAGE;
+      mfma_step(st, st + SM::A_RAW);
+    }
+  }
+  lds_barrier();  // every wave's fragment reads are done before the epilogue reuses the ring
+  FL_STAMP(2);
+
+  // ---- epilogue (gemm_kernel's, verbatim in effect)
+  auto& val = acc;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int m = bm + wr * WTM + i * 16 + fq * 4 + r;
+        int n = bn + wc * WTN + j * 16 + fr;
+        int mc = m < M ? m : M - 1;
+        if constexpr (PRE) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn, pre[i][j][r]);
+        else if constexpr (EV) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn);
+        else val[i][j][r] = ep.value(mc, n, acc[i][j][r], e_stats, bm);
+      }
+  FL_STAMP(3);
+  if constexpr (EP::kRowStats) {
+    float* red = reinterpret_cast<float*>(smem);
+    float mean[FM][4];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) sum += val[i][j][r];
+        sum = wave_sum16(sum);
+        if (fr == 0) red[(wr * WTM + i * 16 + fq * 4 + r) * 2 + wc] = sum;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int rl = wr * WTM + i * 16 + fq * 4 + r;
+        mean[i][r] = (red[rl * 2] + red[rl * 2 + 1]) * (1.0f / BN);
+      }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          float d = val[i][j][r] - mean[i][r];
+          sum += d * d;
+        }
+        sum = wave_sum16(sum);
+        if (fr == 0) red[(wr * WTM + i * 16 + fq * 4 + r) * 2 + wc] = sum;
+      }
+    __syncthreads();
+    if (wc == 0 && fr == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int rl = wr * WTM + i * 16 + fq * 4 + r;
+          int m = bm + rl;
+          if (m < M) ep.store_stats(m, blockIdx.x, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int m = bm + wr * WTM + i * 16 + fq * 4 + r;
+        int n = bn + wc * WTN + j * 16 + fr;
+        if (m < M) ep.store(m, n, val[i][j][r]);
+      }
+  FL_STAMP(4);
+}
+
+// Deepest ring that fits 160 KB next to the prologue/epilogue LDS (at most NSMAX stages).
+template <int BM, int BN, int NS, class AL, class EP>
+inline int launch_gemm_dma_ns(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  using SM = DmaSmem<BM, BN, NS, AL, EP>;
+  const size_t bytes = SM::bytes + (size_t)kvec_of<AL>::value * K * 4;
+  if constexpr (NS > 3) {
+    if (bytes > 160 * 1024) return launch_gemm_dma_ns<BM, BN, NS - 1>(al, W, ldw, ep, M, N, K, st);
+  }
+  FL_REQUIRE(bytes <= 160 * 1024, "gemm_dma: LDS request %zu B too large (K=%d)", bytes, K);
+  auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP>;
+  if (bytes > 64 * 1024) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(N / BN, (M + BM - 1) / BM), dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+template <int BM, int BN, class AL, class EP>
+inline int launch_gemm_dma(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  FL_REQUIRE(M > 0 && N % BN == 0 && K % 64 == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
+  return launch_gemm_dma_ns<BM, BN, 8>(al, W, ldw, ep, M, N, K, st);
+}
+
+}  // namespace fl

@@ -35,6 +35,7 @@ SIGNATURES = {
     "flamed_den_step": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, c_size_t, P]),
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_den_time_kernels": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
+    "flamed_den_time_kernels_graph": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),
     "flamed_stamp_buffer": (c_int, [P]),
     "flamed_probe_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),

@@ -100,12 +100,24 @@ enum { FLAMED_DEN_KERNEL_CLASSES = 9 };
 FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                        size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);
 
+/* Diagnostic: in-graph device time per launch (ms) of each kernel class: a captured graph of 4
+ * dt = 0 Euler steps is replayed `reps` times as is and once per class with that class's launches
+ * doubled (flamed_tune "dup_class"); ms_out[c] = (t_dup - t_base) / launches of c, and
+ * ms_out[FLAMED_DEN_KERNEL_CLASSES] = t_base per step.  ms_out holds FLAMED_DEN_KERNEL_CLASSES + 1
+ * floats.  Class 2 reads 0 when the GroupNorm finalize is fused into class 1. */
+FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
+                                             size_t ws_bytes, int reps, float* ms_out, hipStream_t stream);
+
 /* Tuning knobs (process-wide; diagnostic / benchmarking).  Keys:
  *   "splitk_target" — bf16 small-M GEMMs (M < 2048 rows) split K over workgroups until about this
  *                     many workgroups are launched (default 1 = off: slower at B = 1 on gfx950);
- *   "splitk_max"    — maximum number of K slices (power of two <= 16, default 4).
+ *   "splitk_max"    — maximum number of K slices (1, 2 or 4; default 4).
  *   "small_stages"  — pipeline of the small-M GEMM tile (M < 2048 rows): 3 (LDS ring, 2 K-steps in
  *                     flight), 5 or 7 (4 or 6 K-steps of register prefetch);
+ *   "dma"           — 1: small-M bf16 GEMMs whose A operand is bf16 run on the LDS-DMA pipeline
+ *                     (gemm_dma.hpp); 2: also those with fp32 (LayerNorm/GroupNorm) A operands;
+ *                     0 (default): the register-staged main loop only;
+ *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.
  * Split-K sums the slices in a fixed order (deterministic).  Returns 1001 for an unknown key. */

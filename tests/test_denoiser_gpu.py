@@ -104,3 +104,35 @@ def test_unsupported_dims_raise():
     den = SimpleMLPAdaLN(16, 64, 16, 32, 2, 31, 1, 15, 1, None).to(DEV).eval()
     with torch.inference_mode(), pytest.raises(RuntimeError, match="unsupported dims"):
         den(torch.zeros(1, 8, 16, device=DEV), torch.zeros(1, 1, device=DEV), torch.zeros(1, 32, device=DEV))
+
+
+@pytest.mark.parametrize("target,mx", [(512, 2), (1024, 4)])
+def test_split_k_solve_bf16(target, mx, pg_bf16):
+    """Small-M split-K (write-through slab hand-off, last arriver reduces) gives the unsplit result
+    up to fp32 summation order, and stays within the bf16 tolerance of the oracle."""
+    from flamed import _native as nat
+    pg, sd = pg_bf16
+    hip = pg.denoiser.hip()
+    g = torch.Generator().manual_seed(11)
+    B, T, nfe = 1, 200, 4
+    x0 = torch.randn(B, T, 256, generator=g)
+    spk = torch.randn(B, 256, generator=g)
+    ts = torch.linspace(0, 1, nfe + 1)
+    L = nat.lib()
+    with torch.inference_mode():
+        base = hip.solve(x0.to(DEV), ts.to(DEV), spk.to(DEV), nfe).cpu()
+        try:
+            nat.check(L.flamed_tune(b"splitk_target", target), "tune")
+            nat.check(L.flamed_tune(b"splitk_max", mx), "tune")
+            pg.denoiser.hip_graph = False
+            a = hip.solve(x0.to(DEV), ts.to(DEV), spk.to(DEV), nfe).cpu()
+            pg.denoiser.hip_graph = True
+            b = hip.solve(x0.to(DEV), ts.to(DEV), spk.to(DEV), nfe).cpu()
+            c = hip.solve(x0.to(DEV), ts.to(DEV), spk.to(DEV), nfe).cpu()
+        finally:
+            nat.check(L.flamed_tune(b"splitk_target", 1), "tune")
+            nat.check(L.flamed_tune(b"splitk_max", 4), "tune")
+    assert torch.equal(a, b) and torch.equal(b, c)  # deterministic reduction, graph == eager
+    assert rel_l2(a, base) < 5e-3  # bf16 re-rounding of U after a different fp32 summation order
+    ref = orc.euler_solve(sd, x0, spk, nfe)
+    assert rel_l2(a, ref) < 2e-2

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--clock-ghz", type=float, default=2.4)
+    ap.add_argument("--dma", type=int, default=1)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from flamed.models.synthesizer.prob_generator import ProbGenerator
@@ -48,6 +49,7 @@ def main():
     spk = torch.randn(B, 256, generator=g).to(dev)
     ts = torch.linspace(0, 1, 129, device=dev)
     L = nat.lib()
+    nat.check(L.flamed_tune(b"dma", a.dma), "tune")
     with torch.inference_mode():
         hip.solve(xt, ts, spk, 128)  # loads the weights into the handle
         torch.cuda.synchronize()
