@@ -21,6 +21,10 @@ namespace fl {
 
 thread_local SplitCtx* g_split = nullptr;
 int g_small_stages = 3;
+// Below kTinyRows rows (flamed_tune "bn32" 1, default) the denoiser GEMMs use 32 x 32 tiles: measured
+// at B = 1 (profiles/r01_dma_ab.txt) 34.6 vs 37.5 ms/solve at T = 131, but 41.9 vs 40.5 at T = 400.
+int g_bn32 = 1;
+constexpr int kTinyRows = 320;
 // Tuning knobs (flamed_tune): split-K workgroup target and maximum split for small-M GEMMs.
 static int g_tune_split_target = 1;  // split-K off by default: measured slower at B=1 (profiles/r01_splitk_sweep.txt)
 static int g_tune_split_max = 4;
@@ -32,13 +36,19 @@ static int g_tune_epoch = 0;
 // flamed_tune "dma": 1 routes small-M bf16 GEMMs whose A operand is bf16 through the LDS-DMA pipeline
 // (gemm_dma.hpp), 2 also those with fp32 (transforming) A loaders, 0 (default) = gemm_kernel only.
 // In-graph per-launch costs at B = 1 (profiles/r01_dma_ab.txt): no gain for 1, a loss for 2.
-static int g_use_dma = 0;
+static int g_use_dma = 1;
 static int g_noctr = 0;  // diagnostic: kernels ignore the device step counter (wrong modulation rows)
 
 // Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
 template <typename DT, class AL, class EP>
 static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
                     hipStream_t st) {
+  if (c == kCfgTiny) {  // row partials are 32 columns wide (cfg_bn): every GEMM of the step uses BN = 32
+    if constexpr (std::is_same<DT, bf16>::value) {
+      if (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)) return launch_gemm_dma<32, 32>(al, W, ldw, ep, M, N, K, st);
+    }
+    return launch_gemm_cfg<32, 32, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  }
   if constexpr (std::is_same<DT, bf16>::value) {
     // measured (B = 1, T = 400, stamps + in-graph dup timing): the DMA ring shortens the K loop of
     // the bf16-A GEMMs; for fp32-A loaders its LDS->LDS transform pass costs more LDS bandwidth than
@@ -793,7 +803,7 @@ static size_t den_slab_floats(const Den* d, int B, int T) {
 static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t M = (size_t)B * T;
   size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
-  size_t NTmax = d->H / 64;
+  size_t NTmax = d->H / 32;  // LN row partials per row: H / BN, BN >= 32
   size_t TS = (T + 63) / 64;
   const size_t sl = den_slab_floats(d, B, T);
   size_t sizes[9] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
@@ -1014,7 +1024,7 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   SplitScope split_scope(w.SLn ? &sctx : nullptr);
   // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
   int* gcnt = (d->gcnt && (size_t)B * (H / kDwCG) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;
-  const GemmCfg cfg = pick_cfg(M);
+  const GemmCfg cfg = (g_bn32 && M < kTinyRows) ? kCfgTiny : pick_cfg(M);
   const int BN = cfg_bn(cfg);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
@@ -1175,6 +1185,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   const std::string k(key);
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "bn32") { g_bn32 = value != 0; return kOk; }
   if (k == "noctr") { g_noctr = value; return kOk; }
   if (k == "dma") { FL_REQUIRE(value >= 0 && value <= 2, "flamed_tune: dma in {0, 1, 2}"); g_use_dma = value; return kOk; }
   if (k == "small_stages") { FL_REQUIRE(value == 3 || value == 5 || value == 7, "flamed_tune: small_stages must be 3, 5 or 7"); g_small_stages = value; return kOk; }

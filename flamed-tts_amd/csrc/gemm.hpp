@@ -56,21 +56,20 @@ struct SplitK {
   int* cnt;     // tiles counters, zero between launches
 };
 
-// LayerNorm row statistics from producer partials: S[m][NT] = (tile mean, tile M2) over `tw` columns.
-__device__ __forceinline__ void row_stats_from_partials(const float* __restrict__ S, int m, int NT, int tw,
-                                                        float eps, float& mean, float& rstd) {
-  const float2* p = reinterpret_cast<const float2*>(S) + (size_t)m * NT;
-  // NT <= 16 partials: load them all before reducing (independent loads in flight together)
-  float2 q[16];
+// LayerNorm row statistics from producer partials: S[m][NT] = (tile mean, tile M2) over `tw` columns,
+// NT <= 32.  All partials are loaded before reducing (independent loads in flight together).
+template <int MAXNT>
+__device__ __forceinline__ void row_stats_n(const float2* __restrict__ p, int NT, int tw, float eps, float& mean, float& rstd) {
+  float2 q[MAXNT];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) q[i] = i < NT ? p[i] : make_float2(0.f, 0.f);
+  for (int i = 0; i < MAXNT; ++i) q[i] = i < NT ? p[i] : make_float2(0.f, 0.f);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) s += q[i].x;
+  for (int i = 0; i < MAXNT; ++i) s += q[i].x;
   mean = s / (float)NT;
   float m2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < MAXNT; ++i) {
     if (i < NT) {
       float d = q[i].x - mean;
       m2 += q[i].y + (float)tw * d * d;
@@ -78,6 +77,17 @@ __device__ __forceinline__ void row_stats_from_partials(const float* __restrict_
   }
   float var = m2 / (float)(NT * tw);
   rstd = 1.0f / sqrtf(var + eps);
+}
+// The 32-partial form (BN = 32 tiles) stays out of line: inlined next to the 16-partial form it cost
+// ~6 us per consuming GEMM at B = 1 even when never executed (register allocation of the prologue).
+__device__ __noinline__ void row_stats_32(const float2* __restrict__ p, int NT, int tw, float eps, float& mean, float& rstd) {
+  row_stats_n<32>(p, NT, tw, eps, mean, rstd);
+}
+__device__ __forceinline__ void row_stats_from_partials(const float* __restrict__ S, int m, int NT, int tw,
+                                                        float eps, float& mean, float& rstd) {
+  const float2* p = reinterpret_cast<const float2*>(S) + (size_t)m * NT;
+  if (NT <= 16) row_stats_n<16>(p, NT, tw, eps, mean, rstd);
+  else row_stats_32(p, NT, tw, eps, mean, rstd);
 }
 
 // Byte offset of 16-B chunk `c` of LDS tile row `r` (128-B rows, two per 256-B bank line).  A 16-lane
@@ -629,6 +639,7 @@ extern thread_local SplitCtx* g_split;
 // Pipeline depth of the small-M (32 x 64) config: 3 = LDS ring of 3 / 2 K-steps in flight,
 // 5 / 7 = 4 / 6 K-steps of register prefetch (flamed_tune "small_stages").
 extern int g_small_stages;
+
 struct SplitScope {
   SplitCtx* prev;
   explicit SplitScope(SplitCtx* c) : prev(g_split) { g_split = c; }
@@ -673,9 +684,10 @@ inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int
 
 // Tile selection by shape.  `BNf` fixes the N tile when the epilogue's row partials need a known
 // width (0 = free choice).
-enum GemmCfg { kCfgSmall = 0, kCfgMid = 1, kCfgLarge = 2 };
+enum GemmCfg { kCfgSmall = 0, kCfgMid = 1, kCfgLarge = 2, kCfgTiny = 3 /* denoiser only: 32 x 32 tiles */ };
 inline GemmCfg pick_cfg(int M) { return M < 2048 ? kCfgSmall : (M < 8192 ? kCfgMid : kCfgLarge); }
-inline int cfg_bn(GemmCfg) { return 64; }
+// Tiny-M tiles are 32 columns wide: half the weight panel per workgroup, twice the workgroups.
+inline int cfg_bn(GemmCfg c) { return c == kCfgTiny ? 32 : 64; }
 
 template <typename DT, class AL, class EP>
 inline int launch_gemm_auto(GemmCfg c, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {

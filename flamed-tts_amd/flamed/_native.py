@@ -40,6 +40,7 @@ SIGNATURES = {
     "flamed_stamp_buffer": (c_int, [P]),
     "flamed_probe_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_empty": (c_int, [c_int, c_int, ctypes.POINTER(c_float), P]),
+    "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
     "flamed_dur_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(P)]),
     "flamed_dur_destroy": (c_int, [P]),
     "flamed_dur_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),

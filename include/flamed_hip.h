@@ -114,9 +114,11 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "splitk_max"    — maximum number of K slices (1, 2 or 4; default 4).
  *   "small_stages"  — pipeline of the small-M GEMM tile (M < 2048 rows): 3 (LDS ring, 2 K-steps in
  *                     flight), 5 or 7 (4 or 6 K-steps of register prefetch);
- *   "dma"           — 1: small-M bf16 GEMMs whose A operand is bf16 run on the LDS-DMA pipeline
- *                     (gemm_dma.hpp); 2: also those with fp32 (LayerNorm/GroupNorm) A operands;
- *                     0 (default): the register-staged main loop only;
+ *   "dma"           — 1 (default): small-M bf16 GEMMs whose A operand is bf16 run on the LDS-DMA
+ *                     pipeline (gemm_dma.hpp); 2: also those with fp32 (LayerNorm/GroupNorm) A
+ *                     operands; 0: the register-staged main loop only;
+ *   "bn32"          — 1 (default): denoiser GEMMs over fewer than 320 rows use 32 x 32 tiles (LN row
+ *                     partials 32 columns wide); 0: 32 x 64 as above 320 rows;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.
@@ -137,6 +139,9 @@ FLAMED_API int flamed_stamp_buffer(void* buf);
  * flamed_probe_empty: an empty kernel of `blocks` x 256 threads (the per-node floor). */
 FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int wbufs, const void* A, const void* W,
                                  void* C, float* us_out, hipStream_t stream);
+/* flamed_probe_stream: per-CU ingest — `blocks` workgroups each stream their own `kb` KB slice of src
+ * (mode 1: LDS-DMA ring, mode 0: register loads).  src must hold blocks x kb KB. */
+FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const void* src, float* us_out, hipStream_t stream);
 FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t stream);
 
 /* ==================== PVA duration / silence generators + length regulator ====================

@@ -10,7 +10,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "flamed-tts_amd"))
 from flamed import _native as nat  # noqa: E402
 
-VARIANTS = {0: "32x64s3", 1: "64x64s3", 2: "32x64s2", 6: "32x64r4", 7: "32x64r6", 8: "64x64r4", 5: "128x64s3",
+VARIANTS = {0: "32x64s3", 9: "32x32s3", 10: "32x64dma", 11: "32x32dma", 1: "64x64s3", 6: "32x64r4", 5: "128x64s3",
             3: "128x128s3"}
 
 
@@ -22,7 +22,7 @@ def main():
     nat.check(L.flamed_probe_empty(256, 64, ctypes.byref(us), st), "empty")
     print(f"empty kernel: {us.value:6.2f} us/launch")
     N = 1024
-    for M in (400, 1600, 25600):
+    for M in ([int(a) for a in sys.argv[1:]] or (131, 400, 1600, 25600)):
         for K in ((1024,) if M != 400 else (256, 1024)):
             A = torch.randn(M, K, device=dev).to(torch.bfloat16)
             nb = 24
@@ -32,7 +32,7 @@ def main():
             for wb in (1, nb):
                 row = []
                 for v, name in VARIANTS.items():
-                    if v == 3 and M < 1600:
+                    if (v == 3 and M < 1600) or (v in (9, 10, 11) and M > 4000):
                         continue
                     reps = 48 if M < 4000 else 24
                     rc = L.flamed_probe_gemm(v, M, N, K, reps, wb, nat.ptr(A), nat.ptr(W), nat.ptr(C), ctypes.byref(us), st)
