@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--splitk-max", type=int, default=None, help="flamed_tune splitk_max")
     ap.add_argument("--dup-class", type=int, default=None, help="ablation: flamed_tune dup_class")
     ap.add_argument("--small-stages", type=int, default=None, help="flamed_tune small_stages (3, 5, 7)")
+    ap.add_argument("--big", type=int, default=None, help="flamed_tune big (large-M bf16 path)")
+    ap.add_argument("--big-ns", type=int, default=None, help="flamed_tune big_ns (2 or 3)")
     ap.add_argument("--bn32", type=int, default=None, help="flamed_tune bn32 (32-wide small-M GEMM tiles)")
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
@@ -183,7 +185,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")

@@ -39,25 +39,6 @@ static int g_tune_epoch = 0;
 static int g_use_dma = 1;
 static int g_noctr = 0;  // diagnostic: kernels ignore the device step counter (wrong modulation rows)
 
-// Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
-template <typename DT, class AL, class EP>
-static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
-                    hipStream_t st) {
-  if (c == kCfgTiny) {  // row partials are 32 columns wide (cfg_bn): every GEMM of the step uses BN = 32
-    if constexpr (std::is_same<DT, bf16>::value) {
-      if (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)) return launch_gemm_dma<32, 32>(al, W, ldw, ep, M, N, K, st);
-    }
-    return launch_gemm_cfg<32, 32, 3, DT>(al, W, ldw, ep, M, N, K, st);
-  }
-  if constexpr (std::is_same<DT, bf16>::value) {
-    // measured (B = 1, T = 400, stamps + in-graph dup timing): the DMA ring shortens the K loop of
-    // the bf16-A GEMMs; for fp32-A loaders its LDS->LDS transform pass costs more LDS bandwidth than
-    // the ring saves, and at mid M its ~150 KB of LDS drops residency to one block per CU
-    if (c == kCfgSmall && (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)))
-      return launch_gemm_dma<32, 64>(al, W, ldw, ep, M, N, K, st);
-  }
-  return wide_a ? launch_gemm_auto<DT>(c, kWideA, al, W, ldw, ep, M, N, K, st) : launch_gemm_auto<DT>(c, al, W, ldw, ep, M, N, K, st);
-}
 // Diagnostic stamps (FL_STAMPS builds): kernel class whose launches point fl_stamp_buf at g_stamp_dev.
 static int g_stamp_class = -1;
 static unsigned long long* g_stamp_dev = nullptr;
@@ -746,6 +727,142 @@ __global__ void stack_taps_kernel(const float* __restrict__ src, DT* __restrict_
   store_val<DT>(dst + ((size_t)k * N + n) * Cin + c, src[i]);
 }
 
+// ------------------------------ large-M bf16 path ------------------------------
+// At B*T >= 8192 rows the GEMMs are MFMA-bound and an A loader that transforms fp32 rows inside the
+// GEMM re-does that work for every column tile.  There each transforming A operand is written once as
+// bf16 rows (A16) by a streaming pass — LayerNorm + AdaLN modulate, GroupNorm apply or a plain cast,
+// the same arithmetic as the fused loaders — and the GEMM runs on 128 x 128 LDS-DMA tiles with
+// XCD-aware placement (gemm_dma.hpp).  flamed_tune "big" 0 keeps the fused register-staged GEMMs.
+int g_big = 1;
+int g_big_ns = 2;  // LDS ring depth of the 128 x 128 tiles (2: two workgroups per CU, 635 TF plain at M = 25600; 3: one, 418 TF)
+thread_local bf16* g_a16 = nullptr;
+
+__global__ void cast_bf16x8_kernel(const float* __restrict__ src, int ld, bf16* __restrict__ dst, int M, int K) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K8 = K / 8;
+  if (i >= (size_t)M * K8) return;
+  const int m = i / K8, c = i - (size_t)m * K8;
+  const float* p = src + (size_t)m * ld + c * 8;
+  const float4 a = ld4(p), b = ld4(p + 4);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  *reinterpret_cast<u32x4*>(dst + (size_t)m * K + c * 8) = pack_chunk<bf16>(v);
+}
+
+// A16 = GroupNorm(D) (LoadGN's arithmetic: (x - mean) * (rstd * gn_w) + gn_b)
+__global__ void gn_apply_bf16_kernel(LoadGN<bf16> al, bf16* __restrict__ dst, int M) {
+  const int H = al.H, K8 = H / 8;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)M * K8) return;
+  const int m = i / K8, k = (int)(i - (size_t)m * K8) * 8;
+  const float* x = al.D + (size_t)m * H + k;
+  const float* g = al.gns + ((size_t)(m / al.T) * H + k) * 2;
+  const float4 x0 = ld4(x), x1 = ld4(x + 4);
+  const float4 g0 = ld4(g), g1 = ld4(g + 4), g2 = ld4(g + 8), g3 = ld4(g + 12);
+  const float4 w0 = ld4(al.gnw + k), w1 = ld4(al.gnw + k + 4), b0 = ld4(al.gnb + k), b1 = ld4(al.gnb + k + 4);
+  const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  const float mu[8] = {g0.x, g0.z, g1.x, g1.z, g2.x, g2.z, g3.x, g3.z};
+  const float rs[8] = {g0.y, g0.w, g1.y, g1.w, g2.y, g2.w, g3.y, g3.w};
+  const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (xv[j] - mu[j]) * (rs[j] * wv[j]) + bv[j];
+  *reinterpret_cast<u32x4*>(dst + (size_t)m * H + k) = pack_chunk<bf16>(o);
+}
+
+// A16 = LayerNorm(X) (+affine) * (1 + scale) + shift (LoadLNMod's arithmetic); 2 rows per workgroup,
+// the row statistics combined once per row from the producer's partials.
+template <bool AFF>
+__global__ __launch_bounds__(256) void lnmod_apply_bf16_kernel(LoadLNMod<bf16, AFF> al, bf16* __restrict__ dst, int M) {
+  __shared__ float st[2][2];
+  const int r = threadIdx.x >> 7, lt = threadIdx.x & 127;
+  const int m = blockIdx.x * 2 + r;
+  if (lt == 0 && m < M) row_stats_from_partials(al.S, m, al.NT, al.tw, al.eps, st[r][0], st[r][1]);
+  __syncthreads();
+  if (m >= M) return;
+  const float mean = st[r][0], rstd = st[r][1];
+  const ModRef md = al.mod.at();
+  const size_t mo = (size_t)(m / md.div) * md.ms;
+  const int K = al.kdim;
+  for (int k = lt * 8; k < K; k += 128 * 8) {
+    const float* x = al.x + (size_t)m * al.ld + k;
+    const float4 x0 = ld4(x), x1 = ld4(x + 4);
+    const float4 c0 = ld4(md.sc + mo + k), c1 = ld4(md.sc + mo + k + 4), h0 = ld4(md.sh + mo + k), h1 = ld4(md.sh + mo + k + 4);
+    float4 w0 = make_float4(1.f, 1.f, 1.f, 1.f), w1 = w0, b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+    if (AFF) { w0 = ld4(al.lnw + k); w1 = ld4(al.lnw + k + 4); b0 = ld4(al.lnb + k); b1 = ld4(al.lnb + k + 4); }
+    const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s1 = 1.0f + sc[j];
+      o[j] = ((xv[j] - mean) * rstd) * (wv[j] * s1) + (bv[j] * s1 + sh[j]);
+    }
+    *reinterpret_cast<u32x4*>(dst + (size_t)m * K + k) = pack_chunk<bf16>(o);
+  }
+}
+
+static int big_prep(const LoadF32<bf16>& al, int M, int K, bf16* a16, hipStream_t st) {
+  const size_t n = (size_t)M * (K / 8);
+  hipLaunchKernelGGL(cast_bf16x8_kernel, dim3((n + 255) / 256), dim3(256), 0, st, al.p, al.ld, a16, M, K);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+static int big_prep(const LoadGN<bf16>& al, int M, int K, bf16* a16, hipStream_t st) {
+  FL_REQUIRE(K == al.H && K % 8 == 0, "big_prep(GN): K=%d", K);
+  const size_t n = (size_t)M * (K / 8);
+  hipLaunchKernelGGL(gn_apply_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, al, a16, M);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+template <bool AFF>
+static int big_prep(const LoadLNMod<bf16, AFF>& al, int M, int K, bf16* a16, hipStream_t st) {
+  FL_REQUIRE(K == al.kdim && K % 8 == 0, "big_prep(LN): K=%d", K);
+  hipLaunchKernelGGL(lnmod_apply_bf16_kernel<AFF>, dim3((M + 1) / 2), dim3(256), 0, st, al, a16, M);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+template <class EP>
+static int launch_big(const LoadPlain<bf16>& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  if (g_big_ns == 2) return launch_gemm_dma_fixed<128, 128, 2, true>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm_dma_fixed<128, 128, 3, true>(al, W, ldw, ep, M, N, K, st);
+}
+
+// Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
+template <typename DT, class AL, class EP>
+static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
+                    hipStream_t st) {
+  if constexpr (std::is_same<DT, bf16>::value) {
+    if (c == kCfgLarge && g_big) {
+      if constexpr (AL::kSrcBytes == 2) {
+        return launch_big(al, W, ldw, ep, M, N, K, st);
+      } else {
+        FL_REQUIRE(g_a16, "den_gemm: large-M A16 workspace missing");
+        int rc = big_prep(al, M, K, g_a16, st);
+        if (rc) return rc;
+        return launch_big(LoadPlain<bf16>{g_a16, K}, W, ldw, ep, M, N, K, st);
+      }
+    }
+  }
+  if (c == kCfgTiny) {  // row partials are 32 columns wide (cfg_bn): every GEMM of the step uses BN = 32
+    if constexpr (std::is_same<DT, bf16>::value) {
+      if (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)) return launch_gemm_dma<32, 32>(al, W, ldw, ep, M, N, K, st);
+    }
+    return launch_gemm_cfg<32, 32, 3, DT>(al, W, ldw, ep, M, N, K, st);
+  }
+  if constexpr (std::is_same<DT, bf16>::value) {
+    // measured (B = 1, T = 400, stamps + in-graph dup timing): the DMA ring shortens the K loop of
+    // the bf16-A GEMMs; for fp32-A loaders its LDS->LDS transform pass costs more LDS bandwidth than
+    // the ring saves, and at mid M its ~150 KB of LDS drops residency to one block per CU
+    if (c == kCfgSmall && (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)))
+      return launch_gemm_dma<32, 64>(al, W, ldw, ep, M, N, K, st);
+  }
+  return wide_a ? launch_gemm_auto<DT>(c, kWideA, al, W, ldw, ep, M, N, K, st) : launch_gemm_auto<DT>(c, al, W, ldw, ep, M, N, K, st);
+}
+
 // ------------------------------ handle ------------------------------
 
 struct DenBlockW {
@@ -790,6 +907,7 @@ struct DenWs {
   float* Y;    // conv_out tap-stacked GEMM output, M x 3C
   float* SL;   // split-K slabs (small-M GEMMs), SLn floats
   size_t SLn;
+  bf16* A16;   // large-M bf16 path: normalised A operand rows, M x H (null otherwise)
 };
 
 // split-K slab capacity: 32 x 64 tiles of the widest GEMM (max(H, 3C) columns) x 4 slices, small M only
@@ -806,11 +924,12 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t NTmax = d->H / 32;  // LN row partials per row: H / BN, BN >= 32
   size_t TS = (T + 63) / 64;
   const size_t sl = den_slab_floats(d, B, T);
-  size_t sizes[9] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
-                     8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl};
+  const size_t a16 = (d->dt == FLAMED_BF16 && M >= 8192) ? 2 * M * d->H : 0;  // pick_cfg's large-M range
+  size_t sizes[10] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
+                      8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16};
   size_t off = 0;
-  void* ptrs[9];
-  for (int i = 0; i < 9; ++i) {
+  void* ptrs[10];
+  for (int i = 0; i < 10; ++i) {
     ptrs[i] = base ? (char*)base + off : nullptr;
     off += align256(sizes[i]);
   }
@@ -818,6 +937,7 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
     w->X = (float*)ptrs[0]; w->S0 = (float*)ptrs[1]; w->S1 = (float*)ptrs[2]; w->D = (float*)ptrs[3];
     w->U = ptrs[4]; w->GP = (float*)ptrs[5]; w->GNS = (float*)ptrs[6]; w->Y = (float*)ptrs[7];
     w->SL = (float*)ptrs[8]; w->SLn = sl;
+    w->A16 = a16 ? (bf16*)ptrs[9] : nullptr;
   }
   return off;
 }
@@ -1025,7 +1145,14 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
   int* gcnt = (d->gcnt && (size_t)B * (H / kDwCG) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;
   const GemmCfg cfg = (g_bn32 && M < kTinyRows) ? kCfgTiny : pick_cfg(M);
-  const int BN = cfg_bn(cfg);
+  const bool big = std::is_same<DT, bf16>::value && cfg == kCfgLarge && g_big;
+  FL_REQUIRE(!big || w.A16, "den_step: large-M workspace without the A16 buffer");
+  const int BN = big ? 128 : cfg_bn(cfg);  // LN row-partial width = the N tile of the stats epilogues
+  struct A16Scope {
+    bf16* prev;
+    explicit A16Scope(bf16* p) : prev(g_a16) { g_a16 = p; }
+    ~A16Scope() { g_a16 = prev; }
+  } a16_scope(w.A16);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
   int rc;
@@ -1185,6 +1312,8 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   const std::string k(key);
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "big") { g_big = value != 0; return kOk; }
+  if (k == "big_ns") { FL_REQUIRE(value == 2 || value == 3, "flamed_tune: big_ns in {2, 3}"); g_big_ns = value; return kOk; }
   if (k == "bn32") { g_bn32 = value != 0; return kOk; }
   if (k == "noctr") { g_noctr = value; return kOk; }
   if (k == "dma") { FL_REQUIRE(value >= 0 && value <= 2, "flamed_tune: dma in {0, 1, 2}"); g_use_dma = value; return kOk; }

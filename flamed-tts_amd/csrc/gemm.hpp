@@ -500,7 +500,10 @@ struct EpiBiasAct {
   __device__ void prologue(int, int, int, float*) const {}
   __device__ float value(int, int n, float acc, const float*, int) const {
     float v = acc + (bias ? bias[n] : 0.f);
-    if constexpr (ACT == 1) v = gelu_erf(v);
+    if constexpr (ACT == 1) {
+      if constexpr (std::is_same<OT, bf16>::value) v = gelu_fast(v);  // bf16 output: 4.7e-7 erf error is invisible
+      else v = gelu_erf(v);                                            // fp32 parity mode: ocml erff
+    }
     if constexpr (ACT == 2) v = silu(v);
     if constexpr (ACT == 3) v = fmaxf(v, 0.f);
     return v;

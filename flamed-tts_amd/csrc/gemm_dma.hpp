@@ -76,7 +76,10 @@ struct DmaSmem {
   static constexpr int G = GW + GA;
 };
 
-template <int BM, int BN, int NS, class AL, class EP>
+// XCD = true: workgroup ids are remapped so the ~nwg/8 tiles one XCD receives (dispatch round-robins
+// ids over the 8 XCDs) are consecutive in row-major tile order — a row panel of A is then fetched by
+// one XCD's L2 instead of all eight (large M, where A is the big operand; guide §5 T1, bijective form).
+template <int BM, int BN, int NS, class AL, class EP, bool XCD = false>
 __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf16* __restrict__ W, int ldw, EP ep,
                                                                  int M, int N, int K) {
   using SM = DmaSmem<BM, BN, NS, AL, EP>;
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int BKE = 64;
-  static_assert(BM % 32 == 0 && BN % 32 == 0 && NS >= 3 && NS - 2 <= 9, "dma gemm tile");
+  static_assert(BM % 32 == 0 && BN % 32 == 0 && NS >= (SM::XF ? 3 : 2) && NS - 2 <= 9, "dma gemm tile");
   static_assert(!XF || BM * 8 % kGemmThreads == 0, "transform pass: whole chunks per thread");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -100,8 +103,16 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const int bn = blockIdx.x * BN;
-  const int bm = blockIdx.y * BM;
+  int tx = blockIdx.x, ty = blockIdx.y;
+  if constexpr (XCD) {
+    const int gx = gridDim.x, nwg = gx * gridDim.y, id = blockIdx.y * gx + blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (id >> 3);
+    ty = wg / gx;
+    tx = wg - ty * gx;
+  }
+  const int bn = tx * BN;
+  const int bm = ty * BM;
   const int nsteps = K / BKE;
 
   // ---- per-lane DMA sources (K-step 0); a K-step advances every source by 128 (bf16) / 256 (fp32) B
@@ -148,10 +159,14 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   for (int s = 0; s < pre_n; ++s) issue(s);
 
   constexpr bool PRE = kpre_of<EP>::value;
+  // Small tiles fetch the residual (X) before the K loop; at 128 x 128 that costs 64 VGPRs and drops the
+  // kernel to one workgroup per CU (B = 64: conv_3 222 -> 234 us, mlp.2 183 -> 204 us), so it waits.
+  constexpr bool PRE_EARLY = PRE && FM * FN <= 4;
   float pre[FM][FN][4];
   const int fr = lane & 15, fq = lane >> 4;
   bool a_uv = false, e_uv = false;
-  if constexpr (PRE) {
+  auto fetch_pre = [&]() __attribute__((always_inline)) {
+    if constexpr (PRE) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -161,7 +176,9 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
           int m = bm + wr * WTM + i * 16 + fq * 4 + r;
           pre[i][j][r] = ep.pre(m < M ? m : M - 1, bn + wc * WTN + j * 16 + fr);
         }
-  }
+    }
+  };
+  if constexpr (PRE_EARLY) fetch_pre();
   if constexpr (AV) a_uv = al.prologue_v(bm, BM, M, K, a_stats, a_vec);
   else al.prologue(bm, BM, M, a_stats);
   if constexpr (EV) e_uv = ep.prologue_v(bm, bn, BM, BN, M, e_stats, e_vec);
@@ -249,6 +266,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   }
   lds_barrier();  // every wave's fragment reads are done before the epilogue reuses the ring
   FL_STAMP(2);
+  if constexpr (PRE && !PRE_EARLY) fetch_pre();
 
   // ---- epilogue (gemm_kernel's, verbatim in effect)
   auto& val = acc;
@@ -309,7 +327,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
         for (int r = 0; r < 4; ++r) {
           int rl = wr * WTM + i * 16 + fq * 4 + r;
           int m = bm + rl;
-          if (m < M) ep.store_stats(m, blockIdx.x, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
+          if (m < M) ep.store_stats(m, tx, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
         }
     }
   }
@@ -336,6 +354,26 @@ inline int launch_gemm_dma_ns(const AL& al, const bf16* W, int ldw, const EP& ep
   }
   FL_REQUIRE(bytes <= 160 * 1024, "gemm_dma: LDS request %zu B too large (K=%d)", bytes, K);
   auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP>;
+  if (bytes > 64 * 1024) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(N / BN, (M + BM - 1) / BM), dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+// Fixed ring depth, optional XCD-aware placement (large-M tiles).
+template <int BM, int BN, int NS, bool XCD, class AL, class EP>
+inline int launch_gemm_dma_fixed(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  FL_REQUIRE(M > 0 && N % BN == 0 && K % 64 == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
+  using SM = DmaSmem<BM, BN, NS, AL, EP>;
+  const size_t bytes = SM::bytes + (size_t)kvec_of<AL>::value * K * 4;
+  FL_REQUIRE(bytes <= 160 * 1024, "gemm_dma: LDS request %zu B too large (K=%d)", bytes, K);
+  auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP, XCD>;
   if (bytes > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {

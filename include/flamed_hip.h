@@ -119,6 +119,10 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     operands; 0: the register-staged main loop only;
  *   "bn32"          — 1 (default): denoiser GEMMs over fewer than 320 rows use 32 x 32 tiles (LN row
  *                     partials 32 columns wide); 0: 32 x 64 as above 320 rows;
+ *   "big"           — 1 (default): bf16 denoiser steps over >= 8192 rows write each transforming A
+ *                     operand once as bf16 rows and run 128 x 128 LDS-DMA GEMM tiles with XCD-aware
+ *                     placement; 0: fused register-staged GEMMs;
+ *   "big_ns"        — LDS ring depth of those tiles: 2 (default, two workgroups per CU) or 3;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.

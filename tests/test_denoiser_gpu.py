@@ -136,3 +136,27 @@ def test_split_k_solve_bf16(target, mx, pg_bf16):
     assert rel_l2(a, base) < 5e-3  # bf16 re-rounding of U after a different fp32 summation order
     ref = orc.euler_solve(sd, x0, spk, nfe)
     assert rel_l2(a, ref) < 2e-2
+
+
+@pytest.mark.parametrize("per_frame_t", [False, True])
+def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
+    """Large-M bf16 path (B*T >= 8192 rows): LN/GN/cast passes to bf16 rows + 128x128 LDS-DMA GEMM tiles
+    with XCD-aware placement, vs the oracle (bf16 tolerance); also the fused register-staged path
+    (flamed_tune big 0) on the same input."""
+    from flamed import _native as nat
+    pg, sd = pg_bf16
+    g = torch.Generator().manual_seed(21)
+    B, T = 17, 500
+    x = torch.randn(B, T, 256, generator=g)
+    c = torch.randn(B, 256, generator=g)
+    t = torch.rand(B, T, generator=g) if per_frame_t else torch.tensor([[0.6]])
+    ref = orc.denoiser_forward(sd, x, t, c)
+    L = nat.lib()
+    v_big = _vel(pg, x, t, c)
+    try:
+        nat.check(L.flamed_tune(b"big", 0), "tune")
+        v_fused = _vel(pg, x, t, c)
+    finally:
+        nat.check(L.flamed_tune(b"big", 1), "tune")
+    assert rel_l2(v_big, ref) < 2e-2
+    assert rel_l2(v_fused, ref) < 2e-2

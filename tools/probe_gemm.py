@@ -11,7 +11,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from flamed import _native as nat  # noqa: E402
 
 VARIANTS = {0: "32x64s3", 9: "32x32s3", 10: "32x64dma", 11: "32x32dma", 1: "64x64s3", 6: "32x64r4", 5: "128x64s3",
-            3: "128x128s3"}
+            3: "128x128s3", 12: "128x128dma3x", 13: "128x128dma2x", 16: "128x128dma3", 14: "256x128dma3x",
+            15: "256x128dma2x", 17: "256x128dma4x"}
+BIG = (3, 5, 12, 13, 14, 15, 16, 17)
 
 
 def main():
@@ -32,7 +34,7 @@ def main():
             for wb in (1, nb):
                 row = []
                 for v, name in VARIANTS.items():
-                    if (v == 3 and M < 1600) or (v in (9, 10, 11) and M > 4000):
+                    if (v in BIG and M < 1600) or (v not in BIG and M > 4000):
                         continue
                     reps = 48 if M < 4000 else 24
                     rc = L.flamed_probe_gemm(v, M, N, K, reps, wb, nat.ptr(A), nat.ptr(W), nat.ptr(C), ctypes.byref(us), st)
@@ -41,7 +43,7 @@ def main():
                         continue
                     tf = 2 * M * N * K / (us.value * 1e-6) / 1e12
                     row.append(f"{name}={us.value:6.2f}({tf:4.0f}TF)")
-                    if M <= 1600:  # correctness of this variant (launch 0 reads buffer 0)
+                    if M <= 1600 or v in BIG:  # correctness of this variant (launch 0 reads buffer 0)
                         nat.check(L.flamed_probe_gemm(v, M, N, K, 1, 1, nat.ptr(A), nat.ptr(W), nat.ptr(C),
                                                       ctypes.byref(us), st), "chk")
                         torch.cuda.synchronize()
