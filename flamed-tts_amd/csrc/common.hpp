@@ -110,6 +110,18 @@ template <> __device__ __forceinline__ u32x4 pack_chunk<bf16>(const float* v) {
 }
 
 template <typename DT> __device__ __forceinline__ void store_val(DT* p, float v) { *p = (DT)v; }
+// four consecutive values (16-B fp32 / 8-B bf16 store; p aligned accordingly)
+template <typename DT> __device__ __forceinline__ void store_val4(DT* p, const float* v);
+template <> __device__ __forceinline__ void store_val4<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> __device__ __forceinline__ void store_val4<bf16>(bf16* p, const float* v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = (bf16)v[j];
+  *reinterpret_cast<uint2*>(p) = __builtin_bit_cast(uint2, b);
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 

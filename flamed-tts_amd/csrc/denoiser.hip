@@ -232,7 +232,7 @@ struct EpiConvNeXtResid {
   int NTout;
   static constexpr bool kRowStats = true;
   static constexpr bool kPre = true;  // X[m][n] prefetched before the main loop
-  static constexpr int kEVec = 8;
+  static constexpr int kEVec = 8;  // fields x kEVecStride floats in LDS
   static constexpr int stat_rows(int BM) { return BM; }
   __device__ float pre(int m, int n) const { return X[(size_t)m * ld + n]; }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
@@ -261,29 +261,31 @@ struct EpiConvNeXtResid {
       m = m < M ? m : M - 1;
       row_stats_from_partials(Sin, m, NTin, twin, eps, st[2 * r], st[2 * r + 1]);
     }
+    constexpr int S = kEVecStride;  // field-major (structure of arrays): a row's lanes read consecutive columns
     if (idx < cnt) {
-      vec[c * 8 + slot * 3 + 0] = w * sc1;
-      vec[c * 8 + slot * 3 + 1] = b * sc1 + shv;
-      vec[c * 8 + slot * 3 + 2] = gv;
-      if (slot == 0) vec[c * 8 + 6] = b3v;
+      vec[(slot * 3 + 0) * S + c] = w * sc1;
+      vec[(slot * 3 + 1) * S + c] = b * sc1 + shv;
+      vec[(slot * 3 + 2) * S + c] = gv;
+      if (slot == 0) vec[6 * S + c] = b3v;
     }
     for (int q = idx + blockDim.x; q < cnt; q += blockDim.x) {  // BN > blockDim / 2 (not used by the tile configs)
       const int sl = q / BN, cc = q - sl * BN, n = bn + cc;
       const size_t mo = (size_t)(r0 + sl) * md.ms + n;
       const float s1 = 1.0f + md.sc[mo];
-      vec[cc * 8 + sl * 3 + 0] = (AFF ? lnw[n] : 1.0f) * s1;
-      vec[cc * 8 + sl * 3 + 1] = (AFF ? lnb[n] : 0.0f) * s1 + md.sh[mo];
-      vec[cc * 8 + sl * 3 + 2] = gate[so + mo];
-      if (sl == 0) vec[cc * 8 + 6] = b3[n];
+      vec[(sl * 3 + 0) * S + cc] = (AFF ? lnw[n] : 1.0f) * s1;
+      vec[(sl * 3 + 1) * S + cc] = (AFF ? lnb[n] : 0.0f) * s1 + md.sh[mo];
+      vec[(sl * 3 + 2) * S + cc] = gate[so + mo];
+      if (sl == 0) vec[6 * S + cc] = b3[n];
     }
     return ok;
   }
   __device__ float value_v(int m, int n, float acc, const float* st, const float* vec, bool use, int bm, int bn, float x) const {
     float xh = (x - st[2 * (m - bm)]) * st[2 * (m - bm) + 1];
     if (use) {
-      const float* v = vec + (n - bn) * 8 + (m / mod.div - bm / mod.div) * 3;
-      float h = xh * v[0] + v[1];
-      return x + v[2] * (h + (acc + vec[(n - bn) * 8 + 6]));
+      constexpr int S = kEVecStride;
+      const float* v = vec + (m / mod.div - bm / mod.div) * 3 * S + (n - bn);
+      float h = xh * v[0] + v[S];
+      return x + v[2 * S] * (h + (acc + vec[6 * S + (n - bn)]));
     }
     const long long so = mod.so.get();
     const ModRef md = mod.at();
@@ -294,6 +296,7 @@ struct EpiConvNeXtResid {
     return x + gate[so + mo] * (h + (acc + b3[n]));
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(X + (size_t)m * ld + n, v); }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(Sout)[(size_t)m * NTout + nt] = make_float2(mean, m2);
   }
@@ -318,21 +321,21 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
     const int r0 = bm / div, r1 = last / div;
     if (r1 - r0 > 1) return false;
     const float* g = gate + so.get();
-    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {
+    for (int idx = threadIdx.x; idx < (r1 - r0 + 1) * BN; idx += blockDim.x) {  // field-major, as EpiConvNeXtResid
       int slot = idx / BN, c = idx - slot * BN, n = bn + c;
-      vec[c * 4 + slot] = g[(size_t)(r0 + slot) * ms + n];
-      if (slot == 0) vec[c * 4 + 2] = b[n];
+      vec[slot * kEVecStride + c] = g[(size_t)(r0 + slot) * ms + n];
+      if (slot == 0) vec[2 * kEVecStride + c] = b[n];
     }
     return true;
   }
   __device__ float value_v(int m, int n, float acc, const float*, const float* vec, bool use, int bm, int bn, float x) const {
     if (use) {
-      const float* v = vec + (n - bn) * 4;
-      return x + v[m / div - bm / div] * (acc + v[2]);
+      return x + vec[(m / div - bm / div) * kEVecStride + (n - bn)] * (acc + vec[2 * kEVecStride + (n - bn)]);
     }
     return x + gate[so.get() + (size_t)(m / div) * ms + n] * (acc + b[n]);
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(X + (size_t)m * ld + n, v); }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(Sout)[(size_t)m * NTout + nt] = make_float2(mean, m2);
   }

@@ -23,6 +23,9 @@ constexpr int kGemmThreads = 256;
 // kEVec floats per output column of its tile.  Detected by these traits (0 when absent).
 template <class T, class = void> struct kvec_of { static constexpr int value = 0; };
 template <class T> struct kvec_of<T, std::void_t<decltype(T::kVec)>> { static constexpr int value = T::kVec; };
+// Per-column epilogue vectors are stored field-major with this column stride (>= every N tile that
+// stages them), so the lanes of a row read consecutive floats (conflict-free, vectorisable).
+constexpr int kEVecStride = 128;
 template <class T, class = void> struct kevec_of { static constexpr int value = 0; };
 template <class T> struct kevec_of<T, std::void_t<decltype(T::kEVec)>> { static constexpr int value = T::kEVec; };
 // Epilogues with kPre read one global value per output element (e.g. the residual X); the kernel
@@ -37,7 +40,8 @@ struct GemmSmem {
   static constexpr int tiles = NSTAGE * (BM + BN) * ROWB;
   static constexpr int a_stats = AL::stat_rows(BM) * 2 * 4;
   static constexpr int e_stats = EP::stat_rows(BM) * 2 * 4;
-  static constexpr int e_vec = kevec_of<EP>::value * BN * 4;
+  static constexpr int e_vec = kevec_of<EP>::value * kEVecStride * 4;
+  static_assert(kevec_of<EP>::value == 0 || BN <= kEVecStride, "per-column vectors: BN <= kEVecStride");
   static constexpr int red = BM * 2 * 4;
   static constexpr int base = (tiles > red ? tiles : red) + 16;  // + 16 B: split-K "last arriver" flag
   static constexpr int flag = base - 16;
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
   int* s_flag = reinterpret_cast<int*>(smem + SM::flag);
   float* e_stats = a_stats + AL::stat_rows(BM) * 2;
   float* e_vec = e_stats + EP::stat_rows(BM) * 2;
-  float* a_vec = e_vec + kevec_of<EP>::value * BN;
+  float* a_vec = e_vec + kevec_of<EP>::value * kEVecStride;
   constexpr bool AV = kvec_of<AL>::value > 0;
   constexpr bool EV = kevec_of<EP>::value > 0;
 
@@ -509,6 +513,7 @@ struct EpiBiasAct {
     return v;
   }
   __device__ void store(int m, int n, float v) const { store_val<OT>(out + (size_t)m * ldo + n, v); }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<OT>(out + (size_t)m * ldo + n, v); }
   __device__ void store_stats(int, int, float, float) const {}
 };
 
@@ -529,6 +534,7 @@ struct EpiBiasStatsT {
     return RELU ? fmaxf(v, 0.f) : v;
   }
   __device__ void store(int m, int n, float v) const { out[(size_t)m * ldo + n] = v; }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(out + (size_t)m * ldo + n, v); }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(S)[(size_t)m * NT + nt] = make_float2(mean, m2);
   }

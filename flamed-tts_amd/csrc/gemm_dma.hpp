@@ -19,6 +19,8 @@
 #pragma once
 #include "gemm.hpp"
 
+#include <utility>
+
 namespace fl {
 
 // One wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane `g` to LDS [lds, lds + 1024).  Written
@@ -55,6 +57,22 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// Four consecutive outputs of one row: the epilogue's own store4 when it has one, else four stores.
+template <class T, class = void> struct has_store4 { static constexpr bool value = false; };
+template <class T>
+struct has_store4<T, std::void_t<decltype(std::declval<const T&>().store4(0, 0, (const float*)nullptr))>> {
+  static constexpr bool value = true;
+};
+template <class EP>
+__device__ __forceinline__ void store4(const EP& ep, int m, int n, const float* v) {
+  if constexpr (has_store4<EP>::value) {
+    ep.store4(m, n, v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ep.store(m, n + e, v[e]);
+  }
+}
+
 template <int BM, int BN, int NS, class AL, class EP>
 struct DmaSmem {
   static constexpr int AE = AL::kSrcBytes;                 // 2 (bf16 A, used in place) or 4 (fp32, transformed)
@@ -65,10 +83,16 @@ struct DmaSmem {
   static constexpr int ABF = XF ? BM * 128 : 0;            // transformed bf16 A image (x2, alternating)
   static constexpr int ring = NS * STAGE;
   static constexpr int red = BM * 2 * 4;
-  static constexpr int body = ring + 2 * ABF > red ? ring + 2 * ABF : red;
+  // big tiles (more than 4 MFMA fragments per wave) run the row-vectorised epilogue through an fp32
+  // image of the whole output tile in LDS
+  static constexpr bool VEPI = (BM / 32) * (BN / 32) > 4;
+  static constexpr int ctile = VEPI ? BM * BN * 4 : 0;
+  static constexpr int body0 = ring + 2 * ABF > red ? ring + 2 * ABF : red;
+  static constexpr int body = body0 > ctile ? body0 : ctile;
   static constexpr int a_stats = AL::stat_rows(BM) * 2 * 4;
   static constexpr int e_stats = EP::stat_rows(BM) * 2 * 4;
-  static constexpr int e_vec = kevec_of<EP>::value * BN * 4;
+  static constexpr int e_vec = kevec_of<EP>::value * kEVecStride * 4;
+  static_assert(kevec_of<EP>::value == 0 || BN <= kEVecStride, "per-column vectors: BN <= kEVecStride");
   static constexpr int bytes = (body + a_stats + e_stats + e_vec + 15) / 16 * 16;  // + kVec*K*4 (runtime)
   // glds instructions per thread per K-step
   static constexpr int GW = BN / 32;                       // W: BN rows x 8 chunks / 64 lanes / 4 waves
@@ -94,7 +118,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   float* a_stats = reinterpret_cast<float*>(smem + SM::body);
   float* e_stats = a_stats + AL::stat_rows(BM) * 2;
   float* e_vec = e_stats + EP::stat_rows(BM) * 2;
-  float* a_vec = e_vec + kevec_of<EP>::value * BN;
+  float* a_vec = e_vec + kevec_of<EP>::value * kEVecStride;
   constexpr bool AV = kvec_of<AL>::value > 0;
   constexpr bool EV = kevec_of<EP>::value > 0;
 
@@ -266,81 +290,142 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   }
   lds_barrier();  // every wave's fragment reads are done before the epilogue reuses the ring
   FL_STAMP(2);
-  if constexpr (PRE && !PRE_EARLY) fetch_pre();
+  if constexpr (PRE && !PRE_EARLY && !SM::VEPI) fetch_pre();
 
-  // ---- epilogue (gemm_kernel's, verbatim in effect)
-  auto& val = acc;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int m = bm + wr * WTM + i * 16 + fq * 4 + r;
-        int n = bn + wc * WTN + j * 16 + fr;
-        int mc = m < M ? m : M - 1;
-        if constexpr (PRE) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn, pre[i][j][r]);
-        else if constexpr (EV) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn);
-        else val[i][j][r] = ep.value(mc, n, acc[i][j][r], e_stats, bm);
-      }
-  FL_STAMP(3);
-  if constexpr (EP::kRowStats) {
-    float* red = reinterpret_cast<float*>(smem);
-    float mean[FM][4];
+  if constexpr (SM::VEPI) {
+    // ---- row-vectorised epilogue: accumulators -> fp32 tile image in LDS (16-float column blocks
+    // XOR-swizzled by row & 3, so a fragment write's four rows hit distinct banks), then each thread
+    // handles 16 x (one row, 4 consecutive columns): 16-B residual loads / stores, row statistics over
+    // a half-wave per row.
+    float* ct = reinterpret_cast<float*>(smem);
+    auto cidx = [](int row, int col) __attribute__((always_inline)) { return row * BN + (col ^ ((row & 3) << 4)); };
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sum = 0.f;
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) sum += val[i][j][r];
-        sum = wave_sum16(sum);
-        if (fr == 0) red[(wr * WTM + i * 16 + fq * 4 + r) * 2 + wc] = sum;
-      }
+        for (int r = 0; r < 4; ++r) ct[cidx(wr * WTM + i * 16 + fq * 4 + r, wc * WTN + j * 16 + fr)] = acc[i][j][r];
     __syncthreads();
+    FL_STAMP(3);
+    constexpr int C4 = BN / 4, IT = BM * C4 / kGemmThreads, RPI = kGemmThreads / C4;  // rows per iteration
+    static_assert(C4 == 32, "row-vectorised epilogue: a row is one half-wave of float4 columns");
+    float v[IT][4];
+    float xr[IT][4];
+    if constexpr (PRE) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int it = 0; it < IT; ++it) {
+        const int row = it * RPI + (tid >> 5), c = (tid & 31) * 4;
+        const int m = bm + row < M ? bm + row : M - 1;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int rl = wr * WTM + i * 16 + fq * 4 + r;
-        mean[i][r] = (red[rl * 2] + red[rl * 2 + 1]) * (1.0f / BN);
+        for (int e = 0; e < 4; ++e) xr[it][e] = ep.pre(m, bn + c + e);
       }
-    __syncthreads();
+    }
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+    for (int it = 0; it < IT; ++it) {
+      const int row = it * RPI + (tid >> 5), c = (tid & 31) * 4;
+      const int m = bm + row < M ? bm + row : M - 1;
+      const float4 a4 = *reinterpret_cast<const float4*>(ct + cidx(row, c));
+      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+      float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sum = 0.f;
+      for (int e = 0; e < 4; ++e) {
+        const int n = bn + c + e;
+        if constexpr (PRE) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bn, xr[it][e]);
+        else if constexpr (EV) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bn);
+        else v[e] = ep.value(m, n, av[e], e_stats, bm);
+      }
+      if constexpr (EP::kRowStats) {
+        float sum = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          float d = val[i][j][r] - mean[i][r];
-          sum += d * d;
+        for (int o = 1; o < 32; o <<= 1) sum += __shfl_xor(sum, o);
+        const float mean = sum * (1.0f / BN);
+        float q = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[e] - mean;
+          q += d * d;
         }
-        sum = wave_sum16(sum);
-        if (fr == 0) red[(wr * WTM + i * 16 + fq * 4 + r) * 2 + wc] = sum;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o);
+        if ((tid & 31) == 0 && bm + row < M) ep.store_stats(bm + row, tx, mean, q);
       }
-    __syncthreads();
-    if (wc == 0 && fr == 0) {
-#pragma unroll
+      if (bm + row < M) store4(ep, bm + row, bn + c, v);
+    }
+  } else {
+    // ---- epilogue (gemm_kernel's, verbatim in effect)
+    auto& val = acc;
+  #pragma unroll
+    for (int i = 0; i < FM; ++i)
+  #pragma unroll
+      for (int j = 0; j < FN; ++j)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int m = bm + wr * WTM + i * 16 + fq * 4 + r;
+          int n = bn + wc * WTN + j * 16 + fr;
+          int mc = m < M ? m : M - 1;
+          if constexpr (PRE) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn, pre[i][j][r]);
+          else if constexpr (EV) val[i][j][r] = ep.value_v(mc, n, acc[i][j][r], e_stats, e_vec, e_uv, bm, bn);
+          else val[i][j][r] = ep.value(mc, n, acc[i][j][r], e_stats, bm);
+        }
+    FL_STAMP(3);
+    if constexpr (EP::kRowStats) {
+      float* red = reinterpret_cast<float*>(smem);
+      float mean[FM][4];
+  #pragma unroll
       for (int i = 0; i < FM; ++i)
-#pragma unroll
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sum = 0.f;
+  #pragma unroll
+          for (int j = 0; j < FN; ++j) sum += val[i][j][r];
+          sum = wave_sum16(sum);
+          if (fr == 0) red[(wr * WTM + i * 16 + fq * 4 + r) * 2 + wc] = sum;
+        }
+      __syncthreads();
+  #pragma unroll
+      for (int i = 0; i < FM; ++i)
+  #pragma unroll
         for (int r = 0; r < 4; ++r) {
           int rl = wr * WTM + i * 16 + fq * 4 + r;
-          int m = bm + rl;
-          if (m < M) ep.store_stats(m, tx, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
+          mean[i][r] = (red[rl * 2] + red[rl * 2 + 1]) * (1.0f / BN);
         }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int m = bm + wr * WTM + i * 16 + fq * 4 + r;
-        int n = bn + wc * WTN + j * 16 + fr;
-        if (m < M) ep.store(m, n, val[i][j][r]);
+      __syncthreads();
+  #pragma unroll
+      for (int i = 0; i < FM; ++i)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sum = 0.f;
+  #pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            float d = val[i][j][r] - mean[i][r];
+            sum += d * d;
+          }
+          sum = wave_sum16(sum);
+          if (fr == 0) red[(wr * WTM + i * 16 + fq * 4 + r) * 2 + wc] = sum;
+        }
+      __syncthreads();
+      if (wc == 0 && fr == 0) {
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int rl = wr * WTM + i * 16 + fq * 4 + r;
+            int m = bm + rl;
+            if (m < M) ep.store_stats(m, tx, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
+          }
       }
+    }
+  #pragma unroll
+    for (int i = 0; i < FM; ++i)
+  #pragma unroll
+      for (int j = 0; j < FN; ++j)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int m = bm + wr * WTM + i * 16 + fq * 4 + r;
+          int n = bn + wc * WTN + j * 16 + fr;
+          if (m < M) ep.store(m, n, val[i][j][r]);
+        }
+  }
   FL_STAMP(4);
 }
 
