@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--small-stages", type=int, default=None, help="flamed_tune small_stages (3, 5, 7)")
     ap.add_argument("--big", type=int, default=None, help="flamed_tune big (large-M bf16 path)")
     ap.add_argument("--big-ns", type=int, default=None, help="flamed_tune big_ns (2 or 3)")
+    ap.add_argument("--dw-tc", type=int, default=None, help="flamed_tune dw_tc (large-M depthwise T-chunk)")
     ap.add_argument("--bn32", type=int, default=None, help="flamed_tune bn32 (32-wide small-M GEMM tiles)")
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
@@ -168,6 +169,57 @@ def secondary_measurements(dev, nfe):
     return out
 
 
+def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
+    """BASELINE configs[2] on the same handle: B = 64 utterances x 400 frames, nfe-step graph solve (one
+    timed solve after a warm one), with the in-graph per-class costs and the roofline of the dominant
+    kernel class."""
+    import ctypes
+    from flamed import _native as nat
+    hip = pg.denoiser.hip()
+    g = torch.Generator().manual_seed(args.seed + 1)
+    x0 = (torch.randn(B, T, C, generator=g) * 0.3 + torch.randn(B, T, C, generator=g)).to(dev)
+    spk = torch.randn(B, C, generator=g).to(dev)
+    ts = torch.linspace(0, 1, nfe + 1, device=dev)
+    with torch.inference_mode():
+        hip.solve(x0, ts, spk, nfe)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hip.solve(x0, ts, spk, nfe)
+        torch.cuda.synchronize()
+        sec = time.perf_counter() - t0
+        L = nat.lib()
+        mods = hip.adaln(ts[:1], spk, torch.zeros(B, dtype=torch.int32, device=dev), torch.arange(B, dtype=torch.int32, device=dev))
+        ws = nat.Workspace().get(L.flamed_den_workspace_size(hip.handle, B, T), dev)
+        ms = (ctypes.c_float * (N_CLASSES + 1))()
+        xs = x0.clone()
+        nat.check(L.flamed_den_time_kernels_graph(hip.handle, nat.ptr(xs), nat.ptr(mods), B, T, nat.ptr(ws), ws.numel(), 4, ms,
+                                                  nat.stream_ptr(dev)), "flamed_den_time_kernels_graph")
+        torch.cuda.synchronize()
+    es = 2 if args.dtype == "bf16" else 4
+    ks = []
+    for cls in range(N_CLASSES):
+        if cls == 2 and ms[cls] <= 0.0:
+            continue
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
+        t = max(ms[cls], 1e-6) * 1e-3
+        ks.append({"name": KERNEL_NAMES[cls], "us": round(ms[cls] * 1e3, 2), "per_step": per_step,
+                   "GBps": round(nbytes / t / 1e9, 1), "TFLOPs": round(flops / t / 1e12, 2)})
+    dom = max(ks, key=lambda k: k["us"] * k["per_step"])
+    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es)
+    ridge = MFMA_PEAK_TFS[args.dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if flops / nbytes > ridge:
+        roof = {"bound": "mfma", "achieved": dom["TFLOPs"], "peak": MFMA_PEAK_TFS[args.dtype], "unit": "TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof.update({"frac": round(roof["achieved"] / roof["peak"], 4), "kernel": dom["name"], "launch_us": dom["us"],
+                 "tflops": dom["TFLOPs"], "gbps": dom["GBps"]})
+    return {"workload": f"BASELINE configs[2]: {B} utterances x {T} frames, nsteps-denoiser={nfe}, hipGraph solve",
+            "value": round(B * T / sec, 2), "unit": "latent frames/s", "ms_per_solve": round(sec * 1e3, 3),
+            "rtf_denoiser": round(sec / (B * T * 200 / 16000.0), 6), "step_us_graph": round(ms[N_CLASSES] * 1e3, 2),
+            "roofline": roof,
+            "kernels": ks}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -185,7 +237,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")
@@ -303,6 +355,10 @@ def main():
             secondary = secondary_measurements(dev, nfe)
         except Exception as e:  # reported, never fatal for the headline line
             secondary = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            secondary["throughput_mode"] = throughput_mode(pg, dev, nfe, args, H, C, NB)
+        except Exception as e:
+            secondary["throughput_mode"] = {"error": f"{type(e).__name__}: {e}"}
 
     audio_s = T * 200 / 16000.0
     value = world * B * T / sec

@@ -365,15 +365,18 @@ struct EpiEuler {  // xt = xt + dt * (acc + b)   (prob_generator.py:445)
 // whole T axis (:89) are finished by gn_finalize; the normalisation itself is applied in the conv_2
 // GEMM's A-operand loader (LoadGN).
 constexpr int kDwCG = 64, kDwTC = 64;
+// T-chunk of the depthwise-conv workgroups at large M (B*T >= 8192): half the workgroups, half the halo
+// re-read (30 of 128 rows instead of 30 of 64); flamed_tune "dw_tc" 64 | 128.
+int g_dw_tc_big = 64;  // 128 measured slower at B = 64 (97 vs 82 us per launch, profiles/r01_b64_bigpath.txt)
 
-template <bool AFF, int KS>
+template <bool AFF, int KS, int TC>
 __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restrict__ X, int H, const float* __restrict__ S,
                                                            int NT, int tw, float eps_ln, ModRef mod,
                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                            const float* __restrict__ dww, const float* __restrict__ dwb,
                                                            float* __restrict__ D, float* __restrict__ GP, int T, int TS,
                                                            int* __restrict__ gcnt, float* __restrict__ GNS) {
-  constexpr int HALO = KS / 2, SR = kDwTC + 2 * HALO, RG = 256 / kDwCG, RPT = kDwTC / RG, WIN = RPT + KS - 1;
+  constexpr int HALO = KS / 2, SR = TC + 2 * HALO, RG = 256 / kDwCG, RPT = TC / RG, WIN = RPT + KS - 1;
   constexpr int C4 = kDwCG / 4;                      // float4 chunks per staged row
   constexpr int NX = (SR * C4 + 255) / 256;          // float4 loads per thread for the X tile
   FL_STAMP(0);
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   __shared__ float va[kDwCG], vb[kDwCG];
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * kDwCG, ts = blockIdx.y, b = blockIdx.z;
-  const int t0 = ts * kDwTC;
+  const int t0 = ts * TC;
   const int cl = tid % kDwCG, rg = tid / kDwCG, c = c0 + cl;
   mod = mod.at();
   // every independent global load is issued up front: X tile (float4), conv taps, LN stats, alpha/beta
@@ -552,10 +555,15 @@ static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, in
                                const float* lnb, const float* dww, const float* dwb, float* D, float* GP, float* GNS,
                                int B, int T, hipStream_t st, int part, int* gcnt) {
   FL_REQUIRE(H % kDwCG == 0 && H % 256 == 0, "dwconv: H=%d must be a multiple of 256", H);
-  const int TS = (T + kDwTC - 1) / kDwTC;
+  const int TC = ((size_t)B * T >= 8192 && g_dw_tc_big == 128) ? 128 : kDwTC;
+  const int TS = (T + TC - 1) / TC;
   if (part != 2) {
-    hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
-                       mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+    if (TC == 128)
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, 128>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
+                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+    else
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
+                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     FL_LAUNCH_CHECK();
   }
   if (part != 1 && !gcnt) {
@@ -1315,6 +1323,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   const std::string k(key);
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
   if (k == "big") { g_big = value != 0; return kOk; }
   if (k == "big_ns") { FL_REQUIRE(value == 2 || value == 3, "flamed_tune: big_ns in {2, 3}"); g_big_ns = value; return kOk; }
   if (k == "bn32") { g_bn32 = value != 0; return kOk; }

@@ -123,6 +123,7 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     operand once as bf16 rows and run 128 x 128 LDS-DMA GEMM tiles with XCD-aware
  *                     placement; 0: fused register-staged GEMMs;
  *   "big_ns"        — LDS ring depth of those tiles: 2 (default, two workgroups per CU) or 3;
+ *   "dw_tc"         — frames per depthwise-conv workgroup at >= 8192 rows: 64 (default) or 128;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.
