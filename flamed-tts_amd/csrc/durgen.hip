@@ -135,28 +135,30 @@ struct DurNet {
 
 struct PvaGraph {
   hipGraphExec_t exec = nullptr;
-  hipStream_t cap = nullptr;
+  hipStream_t cap = nullptr, cap2 = nullptr;  // the two nets' chains are captured as parallel branches
+  hipEvent_t fork = nullptr, join = nullptr;
   std::vector<const void*> key;
-  int* ctr = nullptr;  // device Euler step counter
+  int* ctr = nullptr;  // device Euler step counters: [0] duration chain, [1] silence chain
 };
 static PvaGraph g_pva;  // one cached graph per process (durgen is tiny; recaptured on any change)
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct PvaWs {
-  float *Fd, *TH, *TEMBd, *TEMBs, *Pd, *Ps, *R1, *S1, *R2;
+  float *Fd, *TH, *TEMBd, *TEMBs, *Pd, *Ps, *R1, *S1, *R2, *R1s, *S1s, *R2s;  // R*/S* per net (chains run concurrently)
 };
 static size_t pva_ws_layout(const DurNet* n, int B, int L, int nfe, void* base, PvaWs* w) {
   size_t M = (size_t)B * L;
-  size_t sizes[9] = {4ull * nfe * n->D, 4ull * nfe * 4 * n->D, 4ull * nfe * n->D, 4ull * nfe * n->D, 4 * M * n->D,
-                     4 * M * n->D, 4 * M * n->F, 8 * M * (n->F / 64), 4 * M * n->F};
+  size_t sizes[12] = {4ull * nfe * n->D, 4ull * nfe * 4 * n->D, 4ull * nfe * n->D, 4ull * nfe * n->D, 4 * M * n->D,
+                      4 * M * n->D, 4 * M * n->F, 8 * M * (n->F / 64), 4 * M * n->F, 4 * M * n->F, 8 * M * (n->F / 64),
+                      4 * M * n->F};
   size_t off = 0;
-  float* p[9];
-  for (int i = 0; i < 9; ++i) {
+  float* p[12];
+  for (int i = 0; i < 12; ++i) {
     p[i] = base ? (float*)((char*)base + off) : nullptr;
     off += a256(sizes[i]);
   }
-  if (w) *w = PvaWs{p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8]};
+  if (w) *w = PvaWs{p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], p[8], p[9], p[10], p[11]};
   return off;
 }
 
@@ -172,8 +174,11 @@ static int net_prepare(DurNet* n, const float* enc, int M, const float* ts, int 
   return kOk;
 }
 
+struct NetBufs {
+  float *R1, *S1, *R2;
+};
 static int net_step(DurNet* n, const float* P, const float* temb, float* xt, const uint8_t* mask, int B, int L, float dt,
-                    const PvaWs& w, hipStream_t st, const int* ctr = nullptr, int* ctr_inc = nullptr) {
+                    const NetBufs& w, hipStream_t st, const int* ctr = nullptr, int* ctr_inc = nullptr) {
   const int M = B * L, D = n->D, F = n->F;
   const int NT = F / 64;
   int rc;
@@ -332,17 +337,21 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   const int M = B * L, D = nd->D;
   // delta_t = 1 / nfe as a python float, applied in fp32 (pva.py:99,106,109)
   const float dt = (float)(1.0 / (double)nfe);
+  const NetBufs bd{w.R1, w.S1, w.R2}, bs{w.R1s, w.S1s, w.R2s};
   int rc;
   if ((rc = net_prepare(nd, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBd, w.Pd, st))) return rc;
   if ((rc = net_prepare(ns, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBs, w.Ps, st))) return rc;
   if (!use_graph) {
     for (int i = 0; i < nfe; ++i) {  // dur then sil on every step (pva.py:104-109)
-      if ((rc = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, w, st))) return rc;
-      if ((rc = net_step(ns, w.Ps, w.TEMBs + (size_t)i * D, sil_t, mask, B, L, dt, w, st))) return rc;
+      if ((rc = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, bd, st))) return rc;
+      if ((rc = net_step(ns, w.Ps, w.TEMBs + (size_t)i * D, sil_t, mask, B, L, dt, bs, st))) return rc;
     }
     return kOk;
   }
-  // graph of G steps replayed nfe/G times; the step's time-embedding row comes from a device counter
+  // graph of G steps replayed nfe/G times; the step's time-embedding row comes from a device counter.
+  // The duration and silence flows are independent chains (each net reads only its own x_t and the
+  // encoder output, pva.py:104-109): they are captured as two parallel branches (fork/join events),
+  // each with its own counter and scratch, and run concurrently.
   int G = 1;
   for (int g = 16; g > 1; --g)
     if (nfe % g == 0) { G = g; break; }
@@ -352,11 +361,21 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   if (!g_pva.exec || g_pva.key != key) {
     if (g_pva.exec) { FL_HIP(hipGraphExecDestroy(g_pva.exec)); g_pva.exec = nullptr; }
     if (!g_pva.cap) FL_HIP(hipStreamCreateWithFlags(&g_pva.cap, hipStreamNonBlocking));
+    if (!g_pva.cap2) FL_HIP(hipStreamCreateWithFlags(&g_pva.cap2, hipStreamNonBlocking));
+    if (!g_pva.fork) FL_HIP(hipEventCreateWithFlags(&g_pva.fork, hipEventDisableTiming));
+    if (!g_pva.join) FL_HIP(hipEventCreateWithFlags(&g_pva.join, hipEventDisableTiming));
     FL_HIP(hipStreamBeginCapture(g_pva.cap, hipStreamCaptureModeRelaxed));
     int r = kOk;
-    for (int i = 0; i < G && r == kOk; ++i) {
-      r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, w, g_pva.cap, g_pva.ctr, nullptr);
-      if (r == kOk) r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, w, g_pva.cap, g_pva.ctr, g_pva.ctr);
+    hipError_t fe = hipEventRecord(g_pva.fork, g_pva.cap);
+    if (fe == hipSuccess) fe = hipStreamWaitEvent(g_pva.cap2, g_pva.fork, 0);
+    if (fe != hipSuccess) r = kHip;
+    for (int i = 0; i < G && r == kOk; ++i) r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, bd, g_pva.cap, g_pva.ctr, g_pva.ctr);
+    for (int i = 0; i < G && r == kOk; ++i)
+      r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, bs, g_pva.cap2, g_pva.ctr + 1, g_pva.ctr + 1);
+    if (r == kOk) {
+      fe = hipEventRecord(g_pva.join, g_pva.cap2);
+      if (fe == hipSuccess) fe = hipStreamWaitEvent(g_pva.cap, g_pva.join, 0);
+      if (fe != hipSuccess) r = kHip;
     }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(g_pva.cap, &g);
@@ -367,7 +386,7 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
     FL_HIP(ie);
     g_pva.key = key;
   }
-  FL_HIP(hipMemsetAsync(g_pva.ctr, 0, sizeof(int), st));
+  FL_HIP(hipMemsetAsync(g_pva.ctr, 0, 2 * sizeof(int), st));
   for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(g_pva.exec, st));
   return kOk;
 }
