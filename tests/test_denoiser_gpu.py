@@ -160,3 +160,31 @@ def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
         nat.check(L.flamed_tune(b"big", 1), "tune")
     assert rel_l2(v_big, ref) < 2e-2
     assert rel_l2(v_fused, ref) < 2e-2
+
+
+@pytest.mark.parametrize("knobs,B,T", [
+    ({"dma": 0, "bn32": 0}, 1, 200), ({"dma": 1, "bn32": 0}, 1, 200), ({"dma": 2, "bn32": 0}, 1, 200),
+    ({"dma": 0, "bn32": 1}, 1, 200), ({"dma": 2, "bn32": 1}, 1, 200), ({"dma": 1, "bn32": 1}, 3, 1000),
+    ({"big_ns": 3}, 17, 500), ({"big": 1, "dw_tc": 128}, 17, 500),
+])
+def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
+    """Every GEMM main-loop / tile / pipeline variant behind flamed_tune computes the same velocity (vs the
+    oracle, bf16 tolerance): register-staged vs LDS-DMA, 32- vs 64-wide small tiles, mid-M, large-M ring
+    depth and depthwise T-chunk."""
+    from flamed import _native as nat
+    pg, sd = pg_bf16
+    g = torch.Generator().manual_seed(B * 7 + T)
+    x = torch.randn(B, T, 256, generator=g)
+    c = torch.randn(B, 256, generator=g)
+    t = torch.tensor([[0.35]])
+    ref = orc.denoiser_forward(sd, x, t, c)
+    L = nat.lib()
+    defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64}
+    try:
+        for k, v in knobs.items():
+            nat.check(L.flamed_tune(k.encode(), v), "tune")
+        v_hip = _vel(pg, x, t, c)
+    finally:
+        for k in knobs:
+            nat.check(L.flamed_tune(k.encode(), defaults[k]), "tune")
+    assert rel_l2(v_hip, ref) < 2e-2
