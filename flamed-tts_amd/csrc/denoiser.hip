@@ -745,6 +745,8 @@ __global__ void stack_taps_kernel(const float* __restrict__ src, DT* __restrict_
 // the same arithmetic as the fused loaders — and the GEMM runs on 128 x 128 LDS-DMA tiles with
 // XCD-aware placement (gemm_dma.hpp).  flamed_tune "big" 0 keeps the fused register-staged GEMMs.
 int g_big = 1;
+int g_big_min_rows = 1536;  // flamed_tune "big_rows": smallest B*T on the large-M path (B=4/8/16 at T=400:
+                            // 93.6/113.4/188.5 -> 80.1/91.2/116.0 ms per solve; B=3 even)
 int g_big_ns = 2;  // LDS ring depth of the 128 x 128 tiles (2: two workgroups per CU, 635 TF plain at M = 25600; 3: one, 418 TF)
 thread_local bf16* g_a16 = nullptr;
 
@@ -935,7 +937,7 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t NTmax = d->H / 32;  // LN row partials per row: H / BN, BN >= 32
   size_t TS = (T + 63) / 64;
   const size_t sl = den_slab_floats(d, B, T);
-  const size_t a16 = (d->dt == FLAMED_BF16 && M >= 8192) ? 2 * M * d->H : 0;  // pick_cfg's large-M range
+  const size_t a16 = (d->dt == FLAMED_BF16 && M >= (size_t)g_big_min_rows) ? 2 * M * d->H : 0;  // large-M path range
   size_t sizes[10] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
                       8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16};
   size_t off = 0;
@@ -1155,7 +1157,8 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   SplitScope split_scope(w.SLn ? &sctx : nullptr);
   // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
   int* gcnt = (d->gcnt && (size_t)B * (H / kDwCG) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;
-  const GemmCfg cfg = (g_bn32 && M < kTinyRows) ? kCfgTiny : pick_cfg(M);
+  const GemmCfg cfg = (g_bn32 && M < kTinyRows) ? kCfgTiny
+                      : (std::is_same<DT, bf16>::value && g_big && M >= g_big_min_rows) ? kCfgLarge : pick_cfg(M);
   const bool big = std::is_same<DT, bf16>::value && cfg == kCfgLarge && g_big;
   FL_REQUIRE(!big || w.A16, "den_step: large-M workspace without the A16 buffer");
   const int BN = big ? 128 : cfg_bn(cfg);  // LN row-partial width = the N tile of the stats epilogues
@@ -1324,6 +1327,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
   if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
+  if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }
   if (k == "big") { g_big = value != 0; return kOk; }
   if (k == "big_ns") { FL_REQUIRE(value == 2 || value == 3, "flamed_tune: big_ns in {2, 3}"); g_big_ns = value; return kOk; }
   if (k == "bn32") { g_bn32 = value != 0; return kOk; }

@@ -119,9 +119,10 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     operands; 0: the register-staged main loop only;
  *   "bn32"          — 1 (default): denoiser GEMMs over fewer than 320 rows use 32 x 32 tiles (LN row
  *                     partials 32 columns wide); 0: 32 x 64 as above 320 rows;
- *   "big"           — 1 (default): bf16 denoiser steps over >= 8192 rows write each transforming A
+ *   "big"           — 1 (default): bf16 denoiser steps over >= big_rows rows write each transforming A
  *                     operand once as bf16 rows and run 128 x 128 LDS-DMA GEMM tiles with XCD-aware
  *                     placement; 0: fused register-staged GEMMs;
+ *   "big_rows"      — smallest B*T on that path (default 1536, >= 1024);
  *   "big_ns"        — LDS ring depth of those tiles: 2 (default, two workgroups per CU) or 3;
  *   "dw_tc"         — frames per depthwise-conv workgroup at >= 8192 rows: 64 (default) or 128;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
