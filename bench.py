@@ -170,6 +170,28 @@ def secondary_measurements(dev, nfe):
     return out
 
 
+def long_form(pg, dev, args, C, T=2400, nfe=256):
+    """BASELINE configs[4] shape at bf16: 30 s utterances (2400 frames), nsteps-denoiser=256, B = 1 and 16
+    (the fp8 projections of that config are not built)."""
+    hip = pg.denoiser.hip()
+    out = {"frames": T, "nfe": nfe, "dtype": args.dtype, "note": "bf16 GEMM operands (fp8 not built)"}
+    ts = torch.linspace(0, 1, nfe + 1, device=dev)
+    for B in (1, 16):
+        g = torch.Generator().manual_seed(args.seed + 2)
+        x0 = (torch.randn(B, T, C, generator=g) * 0.3 + torch.randn(B, T, C, generator=g)).to(dev)
+        spk = torch.randn(B, C, generator=g).to(dev)
+        with torch.inference_mode():
+            hip.solve(x0, ts, spk, nfe)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            hip.solve(x0, ts, spk, nfe)
+            torch.cuda.synchronize()
+            sec = time.perf_counter() - t0
+        out[f"B{B}"] = {"ms_per_solve": round(sec * 1e3, 3), "latent_frames_per_s": round(B * T / sec, 1),
+                        "rtf_denoiser": round(sec / (B * T * 200 / 16000.0), 6)}
+    return out
+
+
 def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
     """BASELINE configs[2] on the same handle: B = 64 utterances x 400 frames, nfe-step graph solve (one
     timed solve after a warm one), with the in-graph per-class costs and the roofline of the dominant
@@ -360,6 +382,10 @@ def main():
             secondary["throughput_mode"] = throughput_mode(pg, dev, nfe, args, H, C, NB)
         except Exception as e:
             secondary["throughput_mode"] = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            secondary["long_form"] = long_form(pg, dev, args, C)
+        except Exception as e:
+            secondary["long_form"] = {"error": f"{type(e).__name__}: {e}"}
 
     audio_s = T * 200 / 16000.0
     value = world * B * T / sec
