@@ -73,12 +73,25 @@ __device__ __forceinline__ void store4(const EP& ep, int m, int n, const float* 
   }
 }
 
-template <int BM, int BN, int NS, class AL, class EP>
+// Byte offset of 16-B chunk c of row r in a K-step image with CPR chunks per row (CPR = 8: lds_off;
+// CPR = 4, 64-B rows: slot (r & 3) * 4 + (c ^ ((r >> 2) & 3)) of the 256-B bank line, distinct for the
+// 16 rows a ds_read_b128 lane group reads at one chunk).
+template <int CPR>
+__device__ __forceinline__ int lds_offk(int r, int c) {
+  if constexpr (CPR == 8) return lds_off<8>(r, c);
+  else return r * 64 + ((c ^ ((r >> 2) & 3)) << 4);
+}
+template <int CPR>
+__device__ __forceinline__ int lds_swz(int r) { return CPR == 8 ? ((r >> 1) & 7) : ((r >> 2) & 3); }
+
+template <int BM, int BN, int NS, class AL, class EP, int KB = 64>
 struct DmaSmem {
   static constexpr int AE = AL::kSrcBytes;                 // 2 (bf16 A, used in place) or 4 (fp32, transformed)
   static constexpr bool XF = AE == 4;
-  static constexpr int A_RAW = BM * 64 * AE;               // one K-step of A source rows
-  static constexpr int W_ST = BN * 128;                    // one K-step of W rows (bf16)
+  static_assert(KB == 64 || (KB == 32 && !XF), "K-step: 64, or 32 for bf16 A");
+  static constexpr int CPR = KB / 8;                       // 16-B chunks per bf16 row of one K-step
+  static constexpr int A_RAW = BM * KB * AE;               // one K-step of A source rows
+  static constexpr int W_ST = BN * KB * 2;                 // one K-step of W rows (bf16)
   static constexpr int STAGE = A_RAW + W_ST;
   static constexpr int ABF = XF ? BM * 128 : 0;            // transformed bf16 A image (x2, alternating)
   static constexpr int ring = NS * STAGE;
@@ -95,22 +108,23 @@ struct DmaSmem {
   static_assert(kevec_of<EP>::value == 0 || BN <= kEVecStride, "per-column vectors: BN <= kEVecStride");
   static constexpr int bytes = (body + a_stats + e_stats + e_vec + 15) / 16 * 16;  // + kVec*K*4 (runtime)
   // glds instructions per thread per K-step
-  static constexpr int GW = BN / 32;                       // W: BN rows x 8 chunks / 64 lanes / 4 waves
-  static constexpr int GA = XF ? BM / 16 : BM / 32;        // A: BM rows x (16 | 8) chunks / 64 / 4
+  static constexpr int GW = BN * CPR / 256;                // W: BN rows x CPR chunks / 64 lanes / 4 waves
+  static constexpr int GA = XF ? BM / 16 : BM * CPR / 256; // A: BM rows x (16 | CPR) chunks / 64 / 4
   static constexpr int G = GW + GA;
 };
 
 // XCD = true: workgroup ids are remapped so the ~nwg/8 tiles one XCD receives (dispatch round-robins
 // ids over the 8 XCDs) are consecutive in row-major tile order — a row panel of A is then fetched by
 // one XCD's L2 instead of all eight (large M, where A is the big operand; guide §5 T1, bijective form).
-template <int BM, int BN, int NS, class AL, class EP, bool XCD = false>
+template <int BM, int BN, int NS, class AL, class EP, bool XCD = false, int KB = 64>
 __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf16* __restrict__ W, int ldw, EP ep,
                                                                  int M, int N, int K) {
-  using SM = DmaSmem<BM, BN, NS, AL, EP>;
+  using SM = DmaSmem<BM, BN, NS, AL, EP, KB>;
+  constexpr int CPR = SM::CPR, RPI = 64 / CPR;  // rows per DMA wave-instruction
   constexpr bool XF = SM::XF;
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int BKE = 64;
+  constexpr int BKE = KB;
   static_assert(BM % 32 == 0 && BN % 32 == 0 && NS >= (SM::XF ? 3 : 2) && NS - 2 <= 9, "dma gemm tile");
   static_assert(!XF || BM * 8 % kGemmThreads == 0, "transform pass: whole chunks per thread");
 
@@ -143,8 +157,8 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   const char* wsrc[SM::GW];
 #pragma unroll
   for (int j = 0; j < SM::GW; ++j) {
-    const int r = (wave * SM::GW + j) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int r = (wave * SM::GW + j) * RPI + lane / CPR;
+    const int c = (lane % CPR) ^ lds_swz<CPR>(r);
     wsrc[j] = reinterpret_cast<const char*>(W + (size_t)(bn + r) * ldw) + c * 16;
   }
   const char* asrc[SM::GA];
@@ -155,18 +169,18 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
       const int m = bm + r < M ? bm + r : M - 1;
       asrc[j] = al.src_row(m) + (lane & 15) * 16;
     } else {             // 8 rows x 8 swizzled chunks per instruction
-      const int r = (wave * SM::GA + j) * 8 + (lane >> 3);
+      const int r = (wave * SM::GA + j) * RPI + lane / CPR;
       const int m = bm + r < M ? bm + r : M - 1;
-      asrc[j] = al.src_row(m) + ((lane & 7) ^ ((r >> 1) & 7)) * 16;
+      asrc[j] = al.src_row(m) + ((lane % CPR) ^ lds_swz<CPR>(r)) * 16;
     }
   }
   auto issue = [&](int s) __attribute__((always_inline)) {
     char* st = smem + (s % NS) * SM::STAGE;
 #pragma unroll
     for (int j = 0; j < SM::GA; ++j)
-      glds16(asrc[j] + (size_t)s * (64 * SM::AE), st + (wave * SM::GA + j) * 1024);
+      glds16(asrc[j] + (size_t)s * (KB * SM::AE), st + (wave * SM::GA + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < SM::GW; ++j) glds16(wsrc[j] + (size_t)s * 128, st + SM::A_RAW + (wave * SM::GW + j) * 1024);
+    for (int j = 0; j < SM::GW; ++j) glds16(wsrc[j] + (size_t)s * (KB * 2), st + SM::A_RAW + (wave * SM::GW + j) * 1024);
   };
 
   f32x4 acc[FM][FN];
@@ -239,12 +253,12 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   };
   auto mfma_step = [&](const char* ta, const char* tb) __attribute__((always_inline)) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KB / 32; ++kk) {
       u32x4 a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const u32x4*>(ta + lds_off<8>(wr * WTM + i * 16 + fr, kk * 4 + fq));
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const u32x4*>(ta + lds_offk<CPR>(wr * WTM + i * 16 + fr, kk * 4 + fq));
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const u32x4*>(tb + lds_off<8>(wc * WTN + j * 16 + fr, kk * 4 + fq));
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const u32x4*>(tb + lds_offk<CPR>(wc * WTN + j * 16 + fr, kk * 4 + fq));
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -452,13 +466,13 @@ inline int launch_gemm_dma_ns(const AL& al, const bf16* W, int ldw, const EP& ep
 }
 
 // Fixed ring depth, optional XCD-aware placement (large-M tiles).
-template <int BM, int BN, int NS, bool XCD, class AL, class EP>
+template <int BM, int BN, int NS, bool XCD, class AL, class EP, int KB = 64>
 inline int launch_gemm_dma_fixed(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
-  FL_REQUIRE(M > 0 && N % BN == 0 && K % 64 == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
-  using SM = DmaSmem<BM, BN, NS, AL, EP>;
+  FL_REQUIRE(M > 0 && N % BN == 0 && K % KB == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
+  using SM = DmaSmem<BM, BN, NS, AL, EP, KB>;
   const size_t bytes = SM::bytes + (size_t)kvec_of<AL>::value * K * 4;
   FL_REQUIRE(bytes <= 160 * 1024, "gemm_dma: LDS request %zu B too large (K=%d)", bytes, K);
-  auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP, XCD>;
+  auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP, XCD, KB>;
   if (bytes > 64 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
