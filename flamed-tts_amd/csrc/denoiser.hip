@@ -367,27 +367,29 @@ struct EpiEuler {  // xt = xt + dt * (acc + b)   (prob_generator.py:445)
 constexpr int kDwCG = 64, kDwTC = 64;
 // T-chunk of the depthwise-conv workgroups at large M (B*T >= 8192): half the workgroups, half the halo
 // re-read (30 of 128 rows instead of 30 of 64); flamed_tune "dw_tc" 64 | 128.
+int g_dw_cg32_rows = 1536;  // flamed_tune "dw_cg32": below this many rows, narrow depthwise workgroups
+int g_dw_cg_small = 32;     // flamed_tune "dw_cg": their channel width (32 or 16)
 int g_dw_tc_big = 64;  // 128 measured slower at B = 64 (97 vs 82 us per launch, profiles/r01_b64_bigpath.txt)
 
-template <bool AFF, int KS, int TC>
+template <bool AFF, int KS, int TC, int CG = kDwCG>
 __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restrict__ X, int H, const float* __restrict__ S,
                                                            int NT, int tw, float eps_ln, ModRef mod,
                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                            const float* __restrict__ dww, const float* __restrict__ dwb,
                                                            float* __restrict__ D, float* __restrict__ GP, int T, int TS,
                                                            int* __restrict__ gcnt, float* __restrict__ GNS) {
-  constexpr int HALO = KS / 2, SR = TC + 2 * HALO, RG = 256 / kDwCG, RPT = TC / RG, WIN = RPT + KS - 1;
-  constexpr int C4 = kDwCG / 4;                      // float4 chunks per staged row
+  constexpr int HALO = KS / 2, SR = TC + 2 * HALO, RG = 256 / CG, RPT = TC / RG, WIN = RPT + KS - 1;
+  constexpr int C4 = CG / 4;                      // float4 chunks per staged row
   constexpr int NX = (SR * C4 + 255) / 256;          // float4 loads per thread for the X tile
   FL_STAMP(0);
-  __shared__ float hs[SR * kDwCG];
+  __shared__ float hs[SR * CG];
   __shared__ float rs[SR * 2];
-  __shared__ float red[RG * kDwCG * 3 + 1];  // + "last arriver" flag
-  __shared__ float va[kDwCG], vb[kDwCG];
+  __shared__ float red[RG * CG * 3 + 1];  // + "last arriver" flag
+  __shared__ float va[CG], vb[CG];
   const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * kDwCG, ts = blockIdx.y, b = blockIdx.z;
+  const int c0 = blockIdx.x * CG, ts = blockIdx.y, b = blockIdx.z;
   const int t0 = ts * TC;
-  const int cl = tid % kDwCG, rg = tid / kDwCG, c = c0 + cl;
+  const int cl = tid % CG, rg = tid / CG, c = c0 + cl;
   mod = mod.at();
   // every independent global load is issued up front: X tile (float4), conv taps, LN stats, alpha/beta
   float4 xv[NX];
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   const float bias = dwb[c];
   // one modulation row for the whole utterance (sampling path): stage alpha/beta once
   const bool uni = ((size_t)b * T) / mod.div == ((size_t)b * T + T - 1) / mod.div;
-  if (uni && tid < kDwCG) {
+  if (uni && tid < CG) {
     size_t mo = (((size_t)b * T) / mod.div) * mod.ms + c0 + tid;
     float sc1 = 1.0f + mod.sc[mo];
     float lw = AFF ? lnw[c0 + tid] : 1.0f, lb = AFF ? lnb[c0 + tid] : 0.0f;
@@ -442,13 +444,13 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
         }
       }
     }
-    *reinterpret_cast<float4*>(hs + r * kDwCG + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(hs + r * CG + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
   FL_STAMP(2);
   float win[WIN];
 #pragma unroll
-  for (int j = 0; j < WIN; ++j) win[j] = hs[(rg * RPT + j) * kDwCG + cl];
+  for (int j = 0; j < WIN; ++j) win[j] = hs[(rg * RPT + j) * CG + cl];
   float vals[RPT];
   float cn = 0.f, cs = 0.f;
 #pragma unroll
@@ -471,15 +473,15 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
       float d = vals[q] - cm;
       c2 += d * d;
     }
-  red[(rg * kDwCG + cl) * 3 + 0] = cn;
-  red[(rg * kDwCG + cl) * 3 + 1] = cm;
-  red[(rg * kDwCG + cl) * 3 + 2] = c2;
+  red[(rg * CG + cl) * 3 + 0] = cn;
+  red[(rg * CG + cl) * 3 + 1] = cm;
+  red[(rg * CG + cl) * 3 + 2] = c2;
   FL_STAMP(3);
   __syncthreads();
-  if (tid < kDwCG) {
+  if (tid < CG) {
     float n = 0.f, mu = 0.f, m2 = 0.f;
 #pragma unroll
-    for (int g = 0; g < RG; ++g) chan_combine(n, mu, m2, red[(g * kDwCG + tid) * 3], red[(g * kDwCG + tid) * 3 + 1], red[(g * kDwCG + tid) * 3 + 2]);
+    for (int g = 0; g < RG; ++g) chan_combine(n, mu, m2, red[(g * CG + tid) * 3], red[(g * CG + tid) * 3 + 1], red[(g * CG + tid) * 3 + 2]);
     float* o = GP + (((size_t)b * TS + ts) * H + c0 + tid) * 3;
     if (gcnt) {  // handed to another workgroup: write-through (sc1) stores, no release fence needed
       __hip_atomic_store(o, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   // drained, one relaxed agent-scope ticket; the last arriver reads them with sc1 (agent atomic) loads.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int* flag = reinterpret_cast<int*>(red + RG * kDwCG * 3);
+  int* flag = reinterpret_cast<int*>(red + RG * CG * 3);
   if (tid == 0) {
     int* cnt = gcnt + (size_t)b * gridDim.x + blockIdx.x;
     const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
     *flag = last;
   }
   __syncthreads();
-  if (!*flag || tid >= kDwCG) return;
+  if (!*flag || tid >= CG) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
   float n = 0.f, mu = 0.f, m2 = 0.f;
   for (int t0c = 0; t0c < TS; t0c += 8) {
@@ -557,9 +559,17 @@ static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, in
   FL_REQUIRE(H % kDwCG == 0 && H % 256 == 0, "dwconv: H=%d must be a multiple of 256", H);
   const int TC = ((size_t)B * T >= 8192 && g_dw_tc_big == 128) ? 128 : kDwTC;
   const int TS = (T + TC - 1) / TC;
+  // fewer than g_dw_cg32_rows frames: 32-channel workgroups (twice the workgroups, half the serial work each)
+  const bool cg32 = (size_t)B * T < (size_t)g_dw_cg32_rows;
   if (part != 2) {
     if (TC == 128)
       hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, 128>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
+                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+    else if (cg32 && g_dw_cg_small == 16)
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 16>), dim3(H / 16, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
+                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+    else if (cg32)
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 32>), dim3(H / 32, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
                          mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     else
       hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
@@ -1156,7 +1166,7 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   sctx.target = g_tune_split_target; sctx.max_split = g_tune_split_max;
   SplitScope split_scope(w.SLn ? &sctx : nullptr);
   // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
-  int* gcnt = (d->gcnt && (size_t)B * (H / kDwCG) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;
+  int* gcnt = (d->gcnt && (size_t)B * (H / 16) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;  // >= 16-channel groups
   const GemmCfg cfg = (g_bn32 && M < kTinyRows) ? kCfgTiny
                       : (std::is_same<DT, bf16>::value && g_big && M >= g_big_min_rows) ? kCfgLarge : pick_cfg(M);
   const bool big = std::is_same<DT, bf16>::value && cfg == kCfgLarge && g_big;
@@ -1326,6 +1336,8 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   const std::string k(key);
   if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
+  if (k == "dw_cg") { FL_REQUIRE(value == 16 || value == 32, "flamed_tune: dw_cg in {16, 32}"); g_dw_cg_small = value; return kOk; }
+  if (k == "dw_cg32") { FL_REQUIRE(value >= 0, "flamed_tune: dw_cg32 >= 0"); g_dw_cg32_rows = value; return kOk; }
   if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
   if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }
   if (k == "big") { g_big = value != 0; return kOk; }
