@@ -38,6 +38,7 @@ static int probe_variant(int v, const bf16* A, const bf16* W, bf16* C, int M, in
     case 17: return launch_gemm_dma_fixed<256, 128, 4, true>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 18: return launch_gemm_dma_fixed<128, 128, 4, true, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 32>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 19: return launch_gemm_dma_fixed<128, 128, 3, true, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 32>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 21: return launch_gemm_dma_fixed<128, 128, 2, true, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 32>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 20: return launch_gemm_dma_fixed<256, 128, 4, true, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 32>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     default: set_error("probe: unknown variant %d", v); return kBadArg;
   }

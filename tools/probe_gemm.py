@@ -12,8 +12,8 @@ from flamed import _native as nat  # noqa: E402
 
 VARIANTS = {0: "32x64s3", 9: "32x32s3", 10: "32x64dma", 11: "32x32dma", 1: "64x64s3", 6: "32x64r4", 5: "128x64s3",
             3: "128x128s3", 12: "128x128dma3x", 13: "128x128dma2x", 16: "128x128dma3", 14: "256x128dma3x",
-            15: "256x128dma2x", 18: "128x128k32dma4x", 19: "128x128k32dma3x", 20: "256x128k32dma4x"}
-BIG = (3, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20)
+            15: "256x128dma2x", 18: "128x128k32dma4x", 19: "128x128k32dma3x", 21: "128x128k32dma2x", 20: "256x128k32dma4x"}
+BIG = (3, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21)
 
 
 def main():
