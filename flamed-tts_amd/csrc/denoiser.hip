@@ -21,6 +21,7 @@ namespace fl {
 
 thread_local SplitCtx* g_split = nullptr;
 int g_small_stages = 3;
+int g_xcd_strips = 0;
 // Below kTinyRows rows (flamed_tune "bn32" 1, default) the denoiser GEMMs use 32 x 32 tiles: measured
 // at B = 1 (profiles/r01_dma_ab.txt) 34.6 vs 37.5 ms/solve at T = 131, but 41.9 vs 40.5 at T = 400.
 int g_bn32 = 1;
@@ -1342,6 +1343,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }
   if (k == "big") { g_big = value != 0; return kOk; }
   if (k == "big_ns") { FL_REQUIRE(value == 2 || value == 3, "flamed_tune: big_ns in {2, 3}"); g_big_ns = value; return kOk; }
+  if (k == "xcd_strips") { FL_REQUIRE(value >= 0 && value <= 64, "flamed_tune: xcd_strips in [0, 64]"); g_xcd_strips = value; return kOk; }
   if (k == "bn32") { g_bn32 = value != 0; return kOk; }
   if (k == "noctr") { g_noctr = value; return kOk; }
   if (k == "dma") { FL_REQUIRE(value >= 0 && value <= 2, "flamed_tune: dma in {0, 1, 2}"); g_use_dma = value; return kOk; }

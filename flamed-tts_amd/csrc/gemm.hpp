@@ -58,7 +58,24 @@ struct SplitK {
   int n;  // 1..kMaxSplit
   float* slab;  // tiles x n x BM x BN floats
   int* cnt;     // tiles counters, zero between launches
+  int strips = 0;  // > 0: XCD-aware placement in column strips of this many tiles (xcd_tile)
 };
+
+// XCD-aware tile placement for small grids: dispatch round-robins workgroup ids over the 8 XCDs (each
+// with a private L2), so by default column tile x always lands on XCD x mod 8 and every A row panel
+// is fetched by all 8 L2s.  Here the id is first made consecutive per XCD (bijective, guide §5 T1),
+// then walked through column strips of `sw` tiles in row-major order inside each strip: an XCD gets a
+// compact block of about (gy / (8 * sw / gx)) rows x sw columns, so A panels are shared by gx / sw
+// XCDs and W panels by 8 * sw / gx.  Requires gx % sw == 0.
+__device__ __forceinline__ void xcd_tile(int sw, int& tx, int& ty) {
+  const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy, id = blockIdx.y * gx + blockIdx.x;
+  const int xcd = id & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (id >> 3);
+  const int per_strip = gy * sw;
+  const int strip = wg / per_strip, w = wg - strip * per_strip;
+  ty = w / sw;
+  tx = strip * sw + (w - ty * sw);
+}
 
 // LayerNorm row statistics from producer partials: S[m][NT] = (tile mean, tile M2) over `tw` columns,
 // NT <= 32.  All partials are loaded before reducing (independent loads in flight together).
@@ -136,8 +153,10 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int bn = blockIdx.x * BN;
-  const int bm = blockIdx.y * BM;
+  int tx = blockIdx.x, ty = blockIdx.y;
+  if (sk.strips > 0) xcd_tile(sk.strips, tx, ty);
+  const int bn = tx * BN;
+  const int bm = ty * BM;
 
   bool a_uv = false, e_uv = false;  // set by the prologue (per-column vectors staged in LDS)
   typename AL::Raw ra0[ACH], ra1[ACH];
@@ -327,7 +346,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
   // fence (buffer_wbl2 writes back the XCD L2's dirty lines: ~6 us after a kernel that dirtied it) and
   // no acquire (sc1 loads bypass this CU's L1).
   if (sk.n > 1) {
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tile = ty * gridDim.x + tx;
     float* slabs = sk.slab + (size_t)tile * sk.n * (BM * BN);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, sk.n * BM * BN * 4, 0x00020000);
     const int mine = blockIdx.z * (BM * BN * 4);
@@ -430,7 +449,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
         for (int r = 0; r < 4; ++r) {
           int rl = wr * WTM + i * 16 + fq * 4 + r;
           int m = bm + rl;
-          if (m < M) ep.store_stats(m, blockIdx.x, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
+          if (m < M) ep.store_stats(m, tx, mean[i][r], red[rl * 2] + red[rl * 2 + 1]);
         }
     }
   }
@@ -648,6 +667,8 @@ extern thread_local SplitCtx* g_split;
 // Pipeline depth of the small-M (32 x 64) config: 3 = LDS ring of 3 / 2 K-steps in flight,
 // 5 / 7 = 4 / 6 K-steps of register prefetch (flamed_tune "small_stages").
 extern int g_small_stages;
+// XCD strip width of small/mid-M tile placement (SplitK::strips; flamed_tune "xcd_strips", 0 = off).
+extern int g_xcd_strips;
 
 struct SplitScope {
   SplitCtx* prev;
@@ -658,14 +679,18 @@ struct SplitScope {
 template <int BM, int BN, typename DT>
 inline SplitK choose_split(int M, int N, int K) {
   constexpr int BKE = 8 * DTraits<DT>::EPC;
-  SplitK sk{1, nullptr, nullptr};
+  SplitK sk{1, nullptr, nullptr, 0};
+  {
+    const int gx = N / BN;
+    if (g_xcd_strips > 0 && gx % g_xcd_strips == 0 && M < 8192) sk.strips = g_xcd_strips;
+  }
   SplitCtx* c = g_split;
   if (!c || DTraits<DT>::kCode != 1) return sk;  // fp32 parity mode keeps one exact FMA chain
   const int tiles = (N / BN) * ((M + BM - 1) / BM);
   int n = 1;
   while (n * 2 <= c->max_split && tiles * n * 2 <= c->target && (K / BKE) % (n * 2) == 0 && K / (n * 2) >= 2 * BKE) n *= 2;
   if (n == 1 || tiles > c->cnt_n || (size_t)tiles * n * BM * BN > c->slab_floats) return sk;
-  return SplitK{n, c->slab, c->cnt};
+  return SplitK{n, c->slab, c->cnt, sk.strips};
 }
 
 template <int BM, int BN, int NSTAGE, typename DT, class AL, class EP>
