@@ -460,13 +460,20 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < KS; ++j) a += w[j] * win[q + j];
     vals[q] = a;
-    int t = t0 + rg * RPT + q;
-    if (t < T) {
-      D[((size_t)b * T + t) * H + c] = a;
+    if (t0 + rg * RPT + q < T) {
       cn += 1.f;
       cs += a;
     }
   }
+  // D is written after the chunk partials are published (below): with the GroupNorm hand-off its
+  // stores then drain alongside the ticket round trip instead of ahead of the partials' drain.
+  auto store_d = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int t = t0 + rg * RPT + q;
+      if (t < T) D[((size_t)b * T + t) * H + c] = vals[q];
+    }
+  };
   float cm = cn > 0.f ? cs / cn : 0.f, c2 = 0.f;
 #pragma unroll
   for (int q = 0; q < RPT; ++q)
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
   red[(rg * CG + cl) * 3 + 1] = cm;
   red[(rg * CG + cl) * 3 + 2] = c2;
   FL_STAMP(3);
-  __syncthreads();
+  lds_barrier();
   if (tid < CG) {
     float n = 0.f, mu = 0.f, m2 = 0.f;
 #pragma unroll
@@ -493,13 +500,17 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
     }
   }
   FL_STAMP(4);
-  if (!gcnt) return;
+  if (!gcnt) {
+    store_d();
+    return;
+  }
   // GroupNorm finalize fused: the last T-chunk block of this (utterance, channel group) combines the
   // TS chunk partials in chunk order (as gn_finalize_kernel) and writes GNS = (mean, rstd).
   // Hand-off (cdna_hip_programming.md §6 Guideline 16, sc1 form): partials stored write-through and
   // drained, one relaxed agent-scope ticket; the last arriver reads them with sc1 (agent atomic) loads.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  store_d();
   int* flag = reinterpret_cast<int*>(red + RG * CG * 3);
   if (tid == 0) {
     int* cnt = gcnt + (size_t)b * gridDim.x + blockIdx.x;

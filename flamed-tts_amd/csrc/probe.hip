@@ -16,8 +16,111 @@ static int probe_launch(const bf16* A, const bf16* W, bf16* C, int M, int N, int
   return launch_gemm_cfg<BM, BN, NS, bf16>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
 }
 
+// Wave-split-K tile (probe): NW waves share one BM x BN output tile, wave w owning K slice
+// [w*K/NW, (w+1)*K/NW).  MFMA operands are loaded straight from global memory into registers (lane
+// (fr, fq) of a 16x16x32 fragment reads the 16 B at row fr, k + 8 fq), every load of the slice is
+// issued before the first MFMA, and the NW partial tiles are summed through LDS.  No LDS staging of
+// operands and no barrier inside the K loop: the whole K chain is one memory round trip deep.
+template <int BM, int BN, int NW, int KS>
+__global__ __launch_bounds__(NW * 64) void gemm_wsk_probe_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
+                                                                 bf16* __restrict__ C, int M, int N, int K) {
+  constexpr int FM = BM / 16, FN = BN / 16, LDR = BN + 4;
+  __shared__ float red[NW * BM * LDR];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  const int bm = blockIdx.y * BM, bn = blockIdx.x * BN;
+  const int k0 = w * KS * 32 + fq * 8;
+  u32x4 a[KS][FM], b[KS][FN];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      int m = bm + i * 16 + fr;
+      m = m < M ? m : M - 1;
+      a[s][i] = *reinterpret_cast<const u32x4*>(A + (size_t)m * K + k0 + s * 32);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      b[s][j] = *reinterpret_cast<const u32x4*>(W + (size_t)(bn + j * 16 + fr) * K + k0 + s * 32);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep every load of the slice ahead of the first MFMA
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s][i]),
+                                                            __builtin_bit_cast(bf16x8, b[s][j]), acc[i][j], 0, 0, 0);
+  float* rw = red + w * BM * LDR;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rw[(i * 16 + fq * 4 + r) * LDR + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < BM * BN / 4; e += NW * 64) {
+    const int r = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const float4 p = *reinterpret_cast<const float4*>(red + q * BM * LDR + r * LDR + c4);
+      v[0] += p.x; v[1] += p.y; v[2] += p.z; v[3] += p.w;
+    }
+    if (bm + r < M) store_val4<bf16>(C + (size_t)(bm + r) * N + bn + c4, v);
+  }
+}
+
+template <int BM, int BN, int NW>
+static int probe_wsk(const bf16* A, const bf16* W, bf16* C, int M, int N, int K, hipStream_t st) {
+  FL_REQUIRE(K == 1024 && N % BN == 0, "probe wsk: K must be 1024, N %% %d", BN);
+  constexpr int KS = 1024 / 32 / NW;
+  hipLaunchKernelGGL((gemm_wsk_probe_kernel<BM, BN, NW, KS>), dim3(N / BN, (M + BM - 1) / BM), dim3(NW * 64), 0, st, A, W, C, M, N, K);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+// Split-K over workgroups with the register-staged template (slab hand-off, last arriver reduces):
+// a bigger tile cuts the total operand bytes pulled into the CUs, the split spreads them over more CUs.
+template <int BM, int BN, int SPLIT>
+static int probe_split(const bf16* A, const bf16* W, bf16* C, int M, int N, int K, hipStream_t st) {
+  static float* slab = nullptr;
+  static int* cnt = nullptr;
+  constexpr size_t kSlab = (size_t)16 << 20, kCnt = 1 << 16;
+  if (!slab) {
+    FL_HIP(hipMalloc(&slab, kSlab * 4));
+    FL_HIP(hipMalloc(&cnt, kCnt * 4));
+    FL_HIP(hipMemset(cnt, 0, kCnt * 4));
+    FL_HIP(hipDeviceSynchronize());
+  }
+  SplitCtx c;
+  c.slab = slab; c.slab_floats = kSlab; c.cnt = cnt; c.cnt_n = (int)kCnt;
+  c.target = 1 << 30; c.max_split = SPLIT;
+  SplitScope scope(&c);
+  return launch_gemm_cfg<BM, BN, 3, bf16>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+}
+
 static int probe_variant(int v, const bf16* A, const bf16* W, bf16* C, int M, int N, int K, hipStream_t st) {
   switch (v) {
+    case 30: return probe_split<64, 64, 2>(A, W, C, M, N, K, st);
+    case 31: return probe_split<64, 64, 4>(A, W, C, M, N, K, st);
+    case 32: return probe_split<128, 64, 2>(A, W, C, M, N, K, st);
+    case 33: return probe_split<128, 64, 4>(A, W, C, M, N, K, st);
+    case 34: return probe_split<32, 64, 2>(A, W, C, M, N, K, st);
+    case 35: return probe_split<32, 64, 4>(A, W, C, M, N, K, st);
+    case 22: return probe_wsk<32, 32, 4>(A, W, C, M, N, K, st);
+    case 23: return probe_wsk<32, 32, 8>(A, W, C, M, N, K, st);
+    case 24: return probe_wsk<32, 64, 8>(A, W, C, M, N, K, st);
+    case 25: return probe_wsk<64, 32, 8>(A, W, C, M, N, K, st);
+    case 26: return probe_wsk<64, 64, 8>(A, W, C, M, N, K, st);
+    case 27: return probe_wsk<16, 64, 8>(A, W, C, M, N, K, st);
+    case 28: return probe_wsk<32, 32, 16>(A, W, C, M, N, K, st);
+    case 29: return probe_wsk<16, 32, 8>(A, W, C, M, N, K, st);
     case 0: return probe_launch<32, 64, 3>(A, W, C, M, N, K, st);
     case 1: return probe_launch<64, 64, 3>(A, W, C, M, N, K, st);
     case 2: return probe_launch<32, 64, 2>(A, W, C, M, N, K, st);

@@ -125,6 +125,9 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "big_rows"      — smallest B*T on that path (default 1536, >= 1024);
  *   "big_ns"        — LDS ring depth of those tiles: 2 (default, two workgroups per CU) or 3;
  *   "dw_tc"         — frames per depthwise-conv workgroup at >= 8192 rows: 64 (default) or 128;
+ *   "dw_cg32"       — below this many rows (default 1536) the depthwise conv uses narrow channel
+ *                     groups of "dw_cg" channels (16 or 32; default 32);
+ *   "xcd_strips"    — XCD strip width of small/mid-M register-staged tile placement (0 = off);
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.

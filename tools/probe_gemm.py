@@ -12,8 +12,15 @@ from flamed import _native as nat  # noqa: E402
 
 VARIANTS = {0: "32x64s3", 9: "32x32s3", 10: "32x64dma", 11: "32x32dma", 1: "64x64s3", 6: "32x64r4", 5: "128x64s3",
             3: "128x128s3", 12: "128x128dma3x", 13: "128x128dma2x", 16: "128x128dma3", 14: "256x128dma3x",
-            15: "256x128dma2x", 18: "128x128k32dma4x", 19: "128x128k32dma3x", 21: "128x128k32dma2x", 20: "256x128k32dma4x"}
+            15: "256x128dma2x", 18: "128x128k32dma4x", 19: "128x128k32dma3x", 21: "128x128k32dma2x", 20: "256x128k32dma4x",
+            22: "wsk32x32w4", 23: "wsk32x32w8", 24: "wsk32x64w8", 25: "wsk64x32w8", 26: "wsk64x64w8",
+            27: "wsk16x64w8", 28: "wsk32x32w16", 29: "wsk16x32w8",
+            30: "64x64sk2", 31: "64x64sk4", 32: "128x64sk2", 33: "128x64sk4", 34: "32x64sk2", 35: "32x64sk4"}
+WSK = (22, 23, 24, 25, 26, 27, 28, 29)
 BIG = (3, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21)
+
+
+VSEL = [int(x) for x in os.environ.get("PROBE_VARIANTS", "").split(",") if x]
 
 
 def main():
@@ -34,7 +41,7 @@ def main():
             for wb in (1, nb):
                 row = []
                 for v, name in VARIANTS.items():
-                    if (v in BIG and M < 1600) or (v not in BIG and M > 4000):
+                    if (v in BIG and M < 1600) or (v not in BIG and M > 4000) or (v in WSK and K != 1024) or (VSEL and v not in VSEL):
                         continue
                     reps = 48 if M < 4000 else 24
                     rc = L.flamed_probe_gemm(v, M, N, K, reps, wb, nat.ptr(A), nat.ptr(W), nat.ptr(C), ctypes.byref(us), st)

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--clock-ghz", type=float, default=2.4)
     ap.add_argument("--dma", type=int, default=1)
+    ap.add_argument("--tune", nargs="*", default=[], help="extra flamed_tune key=value pairs")
+    ap.add_argument("--classes", default="", help="comma-separated kernel classes (default: all)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from flamed.models.synthesizer.prob_generator import ProbGenerator
@@ -50,6 +52,10 @@ def main():
     ts = torch.linspace(0, 1, 129, device=dev)
     L = nat.lib()
     nat.check(L.flamed_tune(b"dma", a.dma), "tune")
+    for kv in a.tune:
+        k, v = kv.split("=")
+        nat.check(L.flamed_tune(k.encode(), int(v)), "tune")
+    only = [int(x) for x in a.classes.split(",") if x]
     with torch.inference_mode():
         hip.solve(xt, ts, spk, 128)  # loads the weights into the handle
         torch.cuda.synchronize()
@@ -60,6 +66,8 @@ def main():
         nat.check(L.flamed_stamp_buffer(nat.ptr(buf)), "stamp_buffer")
         st = nat.stream_ptr(dev)
         for cls, (name, phases) in NAMES.items():
+            if only and cls not in only:
+                continue
             nat.check(L.flamed_tune(b"stamp_class", cls), "tune")
             for _ in range(2):
                 buf.zero_()
