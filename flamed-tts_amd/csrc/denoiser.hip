@@ -38,6 +38,9 @@ static int g_tune_epoch = 0;
 // (gemm_dma.hpp), 2 also those with fp32 (transforming) A loaders, 0 (default) = gemm_kernel only.
 // In-graph per-launch costs at B = 1 (profiles/r01_dma_ab.txt): no gain for 1, a loss for 2.
 static int g_use_dma = 1;
+// Ring depth of the small-M DMA tiles: at M = 400, K = 1024 with the step's weights streaming from
+// MALL (tools/probe_gemm.py, 24 weight buffers) 3 stages 6.48 us, 4: 6.70, 8: 7.14, 2: 8.36 per launch.
+int g_dma_ns = 3;
 static int g_noctr = 0;  // diagnostic: kernels ignore the device step counter (wrong modulation rows)
 
 // Diagnostic stamps (FL_STAMPS builds): kernel class whose launches point fl_stamp_buf at g_stamp_dev.
@@ -1350,6 +1353,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
   if (k == "dw_cg") { FL_REQUIRE(value == 16 || value == 32, "flamed_tune: dw_cg in {16, 32}"); g_dw_cg_small = value; return kOk; }
   if (k == "dw_cg32") { FL_REQUIRE(value >= 0, "flamed_tune: dw_cg32 >= 0"); g_dw_cg32_rows = value; return kOk; }
+  if (k == "dma_ns") { FL_REQUIRE(value == 3 || value == 4 || value == 6 || value == 8, "flamed_tune: dma_ns in {3, 4, 6, 8}"); g_dma_ns = value; return kOk; }
   if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
   if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }
   if (k == "big") { g_big = value != 0; return kOk; }

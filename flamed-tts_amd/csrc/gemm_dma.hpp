@@ -23,6 +23,9 @@
 
 namespace fl {
 
+// LDS ring depth of the small-M DMA tiles (launch_gemm_dma; flamed_tune "dma_ns": 3, 4, 6 or 8).
+extern int g_dma_ns;
+
 // One wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane `g` to LDS [lds, lds + 1024).  Written
 // as inline asm (M0 saved and restored inside the statement, guide §5.7): hipcc does not see the DMA,
 // so it neither drains it before every ds_read (it cannot prove the reads do not alias the DMA target
@@ -116,7 +119,7 @@ struct DmaSmem {
 // XCD = true: workgroup ids are remapped so the ~nwg/8 tiles one XCD receives (dispatch round-robins
 // ids over the 8 XCDs) are consecutive in row-major tile order — a row panel of A is then fetched by
 // one XCD's L2 instead of all eight (large M, where A is the big operand; guide §5 T1, bijective form).
-template <int BM, int BN, int NS, class AL, class EP, bool XCD = false, int KB = 64>
+template <int BM, int BN, int NS, class AL, class EP, int XCD = 0, int KB = 64>
 __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf16* __restrict__ W, int ldw, EP ep,
                                                                  int M, int N, int K) {
   using SM = DmaSmem<BM, BN, NS, AL, EP, KB>;
@@ -142,7 +145,14 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   int tx = blockIdx.x, ty = blockIdx.y;
-  if constexpr (XCD) {
+  if constexpr (XCD == 2) {
+    // column strips: XCD x (= dispatch id mod 8) owns tile columns [x*gx/8, (x+1)*gx/8), so each XCD's
+    // L2 pulls 1/8 of the weight panel (the larger operand at small M) and all of A (gx % 8 == 0)
+    const int gx = gridDim.x, id = blockIdx.y * gx + blockIdx.x, sw = gx >> 3;
+    const int xcd = id & 7, k = id >> 3;
+    ty = k / sw;
+    tx = xcd * sw + (k - ty * sw);
+  } else if constexpr (XCD == 1) {
     const int gx = gridDim.x, nwg = gx * gridDim.y, id = blockIdx.y * gx + blockIdx.x;
     const int xcd = id & 7, q = nwg >> 3, rr = nwg & 7;
     const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (id >> 3);
@@ -466,7 +476,7 @@ inline int launch_gemm_dma_ns(const AL& al, const bf16* W, int ldw, const EP& ep
 }
 
 // Fixed ring depth, optional XCD-aware placement (large-M tiles).
-template <int BM, int BN, int NS, bool XCD, class AL, class EP, int KB = 64>
+template <int BM, int BN, int NS, int XCD, class AL, class EP, int KB = 64>
 inline int launch_gemm_dma_fixed(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   FL_REQUIRE(M > 0 && N % BN == 0 && K % KB == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
   using SM = DmaSmem<BM, BN, NS, AL, EP, KB>;
@@ -488,7 +498,12 @@ inline int launch_gemm_dma_fixed(const AL& al, const bf16* W, int ldw, const EP&
 template <int BM, int BN, class AL, class EP>
 inline int launch_gemm_dma(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   FL_REQUIRE(M > 0 && N % BN == 0 && K % 64 == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
-  return launch_gemm_dma_ns<BM, BN, 8>(al, W, ldw, ep, M, N, K, st);
+  switch (g_dma_ns) {  // ring depth (flamed_tune "dma_ns"); deeper rings fall back while LDS does not fit
+    case 8: return launch_gemm_dma_ns<BM, BN, 8>(al, W, ldw, ep, M, N, K, st);
+    case 6: return launch_gemm_dma_ns<BM, BN, 6>(al, W, ldw, ep, M, N, K, st);
+    case 4: return launch_gemm_dma_ns<BM, BN, 4>(al, W, ldw, ep, M, N, K, st);
+    default: return launch_gemm_dma_ns<BM, BN, 3>(al, W, ldw, ep, M, N, K, st);
+  }
 }
 
 }  // namespace fl

@@ -107,6 +107,16 @@ static int probe_split(const bf16* A, const bf16* W, bf16* C, int M, int N, int 
 
 static int probe_variant(int v, const bf16* A, const bf16* W, bf16* C, int M, int N, int K, hipStream_t st) {
   switch (v) {
+    case 36: return launch_gemm_dma<64, 32>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 37: return launch_gemm_dma_fixed<32, 32, 4, false, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 40: return launch_gemm_dma_fixed<32, 32, 8, true, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 41: return launch_gemm_dma_fixed<64, 32, 4, false, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 42: return launch_gemm_dma_fixed<32, 32, 2, false, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 43: return launch_gemm_dma_fixed<32, 32, 8, 2, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 44: return launch_gemm_dma_fixed<32, 32, 4, 2, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 45: return launch_gemm_dma_fixed<32, 64, 4, 2, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 46: return launch_gemm_dma_fixed<32, 64, 4, 0, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 47: return launch_gemm_dma_fixed<32, 32, 3, 0, LoadPlain<bf16>, EpiBiasAct<bf16, 0>, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 30: return probe_split<64, 64, 2>(A, W, C, M, N, K, st);
     case 31: return probe_split<64, 64, 4>(A, W, C, M, N, K, st);
     case 32: return probe_split<128, 64, 2>(A, W, C, M, N, K, st);

@@ -117,6 +117,7 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "dma"           — 1 (default): small-M bf16 GEMMs whose A operand is bf16 run on the LDS-DMA
  *                     pipeline (gemm_dma.hpp); 2: also those with fp32 (LayerNorm/GroupNorm) A
  *                     operands; 0: the register-staged main loop only;
+ *   "dma_ns"        — LDS ring depth of those tiles: 3 (default), 4, 6 or 8;
  *   "bn32"          — 1 (default): denoiser GEMMs over fewer than 320 rows use 32 x 32 tiles (LN row
  *                     partials 32 columns wide); 0: 32 x 64 as above 320 rows;
  *   "big"           — 1 (default): bf16 denoiser steps over >= big_rows rows write each transforming A

@@ -166,7 +166,7 @@ def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
     ({"dma": 0, "bn32": 0}, 1, 200), ({"dma": 1, "bn32": 0}, 1, 200), ({"dma": 2, "bn32": 0}, 1, 200),
     ({"dma": 0, "bn32": 1}, 1, 200), ({"dma": 2, "bn32": 1}, 1, 200), ({"dma": 1, "bn32": 1}, 3, 1000),
     ({"big_ns": 3}, 17, 500), ({"big": 1, "dw_tc": 128}, 17, 500),
-    ({"dw_cg": 16}, 2, 300), ({"dw_cg32": 0}, 1, 131),
+    ({"dw_cg": 16}, 2, 300), ({"dw_cg32": 0}, 1, 131), ({"dma_ns": 8}, 1, 400), ({"dma_ns": 4, "dma": 2}, 1, 250),
 ])
 def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     """Every GEMM main-loop / tile / pipeline variant behind flamed_tune computes the same velocity (vs the
@@ -180,7 +180,7 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     t = torch.tensor([[0.35]])
     ref = orc.denoiser_forward(sd, x, t, c)
     L = nat.lib()
-    defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536}
+    defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536, "dma_ns": 3}
     try:
         for k, v in knobs.items():
             nat.check(L.flamed_tune(k.encode(), v), "tune")

@@ -15,7 +15,9 @@ VARIANTS = {0: "32x64s3", 9: "32x32s3", 10: "32x64dma", 11: "32x32dma", 1: "64x6
             15: "256x128dma2x", 18: "128x128k32dma4x", 19: "128x128k32dma3x", 21: "128x128k32dma2x", 20: "256x128k32dma4x",
             22: "wsk32x32w4", 23: "wsk32x32w8", 24: "wsk32x64w8", 25: "wsk64x32w8", 26: "wsk64x64w8",
             27: "wsk16x64w8", 28: "wsk32x32w16", 29: "wsk16x32w8",
-            30: "64x64sk2", 31: "64x64sk4", 32: "128x64sk2", 33: "128x64sk4", 34: "32x64sk2", 35: "32x64sk4"}
+            30: "64x64sk2", 31: "64x64sk4", 32: "128x64sk2", 33: "128x64sk4", 34: "32x64sk2", 35: "32x64sk4",
+            36: "64x32dma", 37: "32x32dma4", 38: "32x32k32dma8", 39: "32x32k32dma16", 40: "32x32dma8x", 41: "64x32dma4",
+            42: "32x32dma2", 43: "32x32dma8s", 44: "32x32dma4s", 45: "32x64dma4s", 46: "32x64dma4", 47: "32x32dma3"}
 WSK = (22, 23, 24, 25, 26, 27, 28, 29)
 BIG = (3, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21)
 
