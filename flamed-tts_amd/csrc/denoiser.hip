@@ -234,9 +234,14 @@ struct EpiConvNeXtResid {
   const float* __restrict__ lnb;
   float* __restrict__ Sout;
   int NTout;
+  // LayerNorm fold of the consumer (bf16 handles, else ya = null): ya = bf16(X_new * alpha_next),
+  // alpha_next = yw (1 + ysc) of the next LayerNorm + modulation (rows as `mod`)
+  bf16* __restrict__ ya = nullptr;
+  const float* __restrict__ yw = nullptr;
+  const float* __restrict__ ysc = nullptr;
   static constexpr bool kRowStats = true;
   static constexpr bool kPre = true;  // X[m][n] prefetched before the main loop
-  static constexpr int kEVec = 8;  // fields x kEVecStride floats in LDS
+  static constexpr int kEVec = 9;  // fields x kEVecStride floats in LDS
   static constexpr int stat_rows(int BM) { return BM; }
   __device__ float pre(int m, int n) const { return X[(size_t)m * ld + n]; }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
@@ -248,7 +253,7 @@ struct EpiConvNeXtResid {
     const ModRef md = mod.at();
     // this thread's staging values (one pass: cnt <= 2 * BN <= blockDim) load before the row statistics
     const int idx = threadIdx.x;
-    float sc1 = 0.f, shv = 0.f, gv = 0.f, w = 1.f, b = 0.f, b3v = 0.f;
+    float sc1 = 0.f, shv = 0.f, gv = 0.f, w = 1.f, b = 0.f, b3v = 0.f, al = 1.f;
     int slot = 0, c = 0;
     if (idx < cnt) {
       slot = idx / BN; c = idx - slot * BN;
@@ -259,6 +264,7 @@ struct EpiConvNeXtResid {
       gv = gate[so + mo];
       if (AFF) { w = lnw[n]; b = lnb[n]; }
       b3v = b3[n];
+      if (ya) al = (yw ? yw[n] : 1.0f) * (1.0f + ysc[so + mo]);
     }
     for (int r = threadIdx.x; r < BM; r += blockDim.x) {
       int m = bm + r;
@@ -271,6 +277,7 @@ struct EpiConvNeXtResid {
       vec[(slot * 3 + 1) * S + c] = b * sc1 + shv;
       vec[(slot * 3 + 2) * S + c] = gv;
       if (slot == 0) vec[6 * S + c] = b3v;
+      vec[(7 + slot) * S + c] = al;
     }
     for (int q = idx + blockDim.x; q < cnt; q += blockDim.x) {  // BN > blockDim / 2 (not used by the tile configs)
       const int sl = q / BN, cc = q - sl * BN, n = bn + cc;
@@ -280,6 +287,7 @@ struct EpiConvNeXtResid {
       vec[(sl * 3 + 1) * S + cc] = (AFF ? lnb[n] : 0.0f) * s1 + md.sh[mo];
       vec[(sl * 3 + 2) * S + cc] = gate[so + mo];
       if (sl == 0) vec[6 * S + cc] = b3[n];
+      vec[(7 + sl) * S + cc] = ya ? (yw ? yw[n] : 1.0f) * (1.0f + ysc[so + mo]) : 1.0f;
     }
     return ok;
   }
@@ -287,9 +295,12 @@ struct EpiConvNeXtResid {
     float xh = (x - st[2 * (m - bm)]) * st[2 * (m - bm) + 1];
     if (use) {
       constexpr int S = kEVecStride;
-      const float* v = vec + (m / mod.div - bm / mod.div) * 3 * S + (n - bn);
+      const int slot = m / mod.div - bm / mod.div;
+      const float* v = vec + slot * 3 * S + (n - bn);
       float h = xh * v[0] + v[S];
-      return x + v[2 * S] * (h + (acc + vec[6 * S + (n - bn)]));
+      const float r = x + v[2 * S] * (h + (acc + vec[6 * S + (n - bn)]));
+      if (ya) ya[(size_t)m * ld + n] = (bf16)(r * vec[(7 + slot) * S + (n - bn)]);
+      return r;
     }
     const long long so = mod.so.get();
     const ModRef md = mod.at();
@@ -297,7 +308,9 @@ struct EpiConvNeXtResid {
     float sc1 = 1.0f + md.sc[mo];
     float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
     float h = xh * (w * sc1) + (b * sc1 + md.sh[mo]);
-    return x + gate[so + mo] * (h + (acc + b3[n]));
+    const float r = x + gate[so + mo] * (h + (acc + b3[n]));
+    if (ya) ya[(size_t)m * ld + n] = (bf16)(r * ((yw ? yw[n] : 1.0f) * (1.0f + ysc[so + mo])));
+    return r;
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
   __device__ void store4(int m, int n, const float* v) const { store_val4<float>(X + (size_t)m * ld + n, v); }
@@ -343,6 +356,105 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(Sout)[(size_t)m * NTout + nt] = make_float2(mean, m2);
   }
+};
+
+// ---- LayerNorm fold (bf16 handles): a GEMM whose A operand is LN(x)*alpha + beta (mlp.0 :151-152,
+// conv_out :238-245), alpha = w (1 + scale), beta = b (1 + scale) + shift per column k, is computed as
+//   out[m][n] = rstd_m * (sum_k W[n][k] (x[m][k] alpha_k) - mean_m * wa[n]) + wb[n]
+// with wa = W alpha, wb = W beta (+ bias) precomputed for every modulation row by flamed_den_adaln
+// (LoadFold) and x*alpha written in bf16 by the producer's epilogue (EpiConvNeXtResid::ya) — so the
+// GEMM runs on a plain bf16 operand (LDS-DMA main loop) with no A-side transform, and the row
+// statistics enter only the epilogue.
+
+// A[r][k] = alpha (WHICH 0) or beta (WHICH 1) of modulation row r, from the mods table.
+template <int WHICH>
+struct LoadFold {
+  const float* __restrict__ sc;
+  const float* __restrict__ sh;
+  int ms;
+  const float* __restrict__ lw;  // LN weight / bias (null: elementwise_affine=False)
+  const float* __restrict__ lb;
+  struct Raw { float s[8]; float h[WHICH ? 8 : 1]; };
+  static constexpr int kSrcBytes = 4;
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ Raw issue(int m, int k) const {
+    Raw r;
+    const float* q = sc + (size_t)m * ms + k;
+    const float4 a = ld4(q), b = ld4(q + 4);
+    r.s[0] = a.x; r.s[1] = a.y; r.s[2] = a.z; r.s[3] = a.w; r.s[4] = b.x; r.s[5] = b.y; r.s[6] = b.z; r.s[7] = b.w;
+    if constexpr (WHICH == 1) {
+      const float* p = sh + (size_t)m * ms + k;
+      const float4 c = ld4(p), d = ld4(p + 4);
+      r.h[0] = c.x; r.h[1] = c.y; r.h[2] = c.z; r.h[3] = c.w; r.h[4] = d.x; r.h[5] = d.y; r.h[6] = d.z; r.h[7] = d.w;
+    }
+    return r;
+  }
+  template <typename D> __device__ u32x4 finish(const Raw& r, int, int k, const float*, int) const {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s1 = 1.0f + r.s[j];
+      if constexpr (WHICH == 0) v[j] = (lw ? lw[k + j] : 1.0f) * s1;
+      else v[j] = (lb ? lb[k + j] : 0.0f) * s1 + r.h[j];
+    }
+    return pack_chunk<D>(v);
+  }
+};
+
+// Consumer epilogue: out = act(rstd_m (acc - mean_m wa[n]) + wb[n]) with (mean, rstd) from the
+// producer's row partials and [wa, wb] of the (at most two) modulation rows of the tile staged in LDS.
+template <typename OT, int ACT>
+struct EpiLNFold {
+  OT* __restrict__ out;
+  int ldo;
+  const float* __restrict__ Sin;
+  int NTin, twin;
+  float eps;
+  const float* __restrict__ fold;  // wa at fold[row * ms + n], wb at fold[row * ms + N + n]
+  int N, ms, div;
+  StepOff so;
+  static constexpr bool kRowStats = false;
+  static constexpr int kEVec = 4;
+  static constexpr int stat_rows(int BM) { return BM; }
+  __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
+    const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
+    const int r0 = bm / div, r1 = last / div;
+    const bool ok = r1 - r0 <= 1;
+    const float* f = fold + so.get();
+    const int cnt = ok ? (r1 - r0 + 1) * BN : 0;
+    for (int idx = threadIdx.x; idx < cnt; idx += blockDim.x) {
+      const int slot = idx / BN, c = idx - slot * BN;
+      const size_t o = (size_t)(r0 + slot) * ms + bn + c;
+      vec[(2 * slot) * kEVecStride + c] = f[o];
+      vec[(2 * slot + 1) * kEVecStride + c] = f[o + N];
+    }
+    for (int r = threadIdx.x; r < BM; r += blockDim.x) {
+      int m = bm + r;
+      m = m < M ? m : M - 1;
+      row_stats_from_partials(Sin, m, NTin, twin, eps, st[2 * r], st[2 * r + 1]);
+    }
+    return ok;
+  }
+  __device__ float value_v(int m, int n, float acc, const float* st, const float* vec, bool use, int bm, int bn) const {
+    const float mean = st[2 * (m - bm)], rstd = st[2 * (m - bm) + 1];
+    float wa, wb;
+    if (use) {
+      const float* v = vec + 2 * (m / div - bm / div) * kEVecStride + (n - bn);
+      wa = v[0];
+      wb = v[kEVecStride];
+    } else {
+      const float* f = fold + so.get() + (size_t)(m / div) * ms + n;
+      wa = f[0];
+      wb = f[N];
+    }
+    float v = rstd * (acc - mean * wa) + wb;
+    if constexpr (ACT == 2) v = silu(v);
+    return v;
+  }
+  __device__ void store(int m, int n, float v) const { store_val<OT>(out + (size_t)m * ldo + n, v); }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<OT>(out + (size_t)m * ldo + n, v); }
+  __device__ void store_stats(int, int, float, float) const {}
 };
 
 struct EpiEuler {  // xt = xt + dt * (acc + b)   (prob_generator.py:445)
@@ -869,6 +981,10 @@ static int launch_big(const LoadPlain<bf16>& al, const bf16* W, int ldw, const E
   return launch_gemm_dma_fixed<128, 128, 3, true>(al, W, ldw, ep, M, N, K, st);
 }
 
+// flamed_tune "lnfold": 1 (default, bf16 handles) mlp.0 / conv_out run as plain bf16 GEMMs with the
+// LayerNorm folded into the epilogue (EpiLNFold); 0: LayerNorm + modulation in the A loader.
+static int g_lnfold = 1;
+
 // Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
 template <typename DT, class AL, class EP>
 static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
@@ -910,7 +1026,9 @@ struct DenBlockW {
 
 struct Den {
   int C, H, NB, KS, S, dt;  // dt: 0 f32, 1 bf16
-  int MS;                   // mods row stride = (6 NB + 5) H
+  int MS;                   // mods row stride: MS0 modulation floats + the LayerNorm-fold tables (bf16)
+  int MS0;                  // (6 NB + 5) H: shift/scale/gate vectors of every adaLN_modulation
+  int fold = 0;             // row holds fold tables [wa, wb] per LN-consuming GEMM (mlp.0 x NB, conv_out)
   char* dev = nullptr;      // packed weight arena
   size_t dev_bytes = 0;
   // fp32 AdaLN path
@@ -946,6 +1064,7 @@ struct DenWs {
   float* SL;   // split-K slabs (small-M GEMMs), SLn floats
   size_t SLn;
   bf16* A16;   // large-M bf16 path: normalised A operand rows, M x H (null otherwise)
+  bf16* XA;    // LayerNorm fold: X * alpha_next rows (bf16 handles), M x H
 };
 
 // split-K slab capacity: 32 x 64 tiles of the widest GEMM (max(H, 3C) columns) x 4 slices, small M only
@@ -963,11 +1082,12 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t TS = (T + 63) / 64;
   const size_t sl = den_slab_floats(d, B, T);
   const size_t a16 = (d->dt == FLAMED_BF16 && M >= (size_t)g_big_min_rows) ? 2 * M * d->H : 0;  // large-M path range
-  size_t sizes[10] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
-                      8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16};
+  const size_t xa = d->fold ? 2 * M * d->H : 0;
+  size_t sizes[11] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
+                      8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16, xa};
   size_t off = 0;
-  void* ptrs[10];
-  for (int i = 0; i < 10; ++i) {
+  void* ptrs[11];
+  for (int i = 0; i < 11; ++i) {
     ptrs[i] = base ? (char*)base + off : nullptr;
     off += align256(sizes[i]);
   }
@@ -976,6 +1096,7 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
     w->U = ptrs[4]; w->GP = (float*)ptrs[5]; w->GNS = (float*)ptrs[6]; w->Y = (float*)ptrs[7];
     w->SL = (float*)ptrs[8]; w->SLn = sl;
     w->A16 = a16 ? (bf16*)ptrs[9] : nullptr;
+    w->XA = xa ? (bf16*)ptrs[10] : nullptr;
   }
   return off;
 }
@@ -995,7 +1116,9 @@ FLAMED_API int flamed_den_create(int C, int H, int n_blocks, int kernel, int spk
   FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16, "flamed_den_create: dtype must be FLAMED_F32 or FLAMED_BF16");
   Den* d = new Den();
   d->C = C; d->H = H; d->NB = n_blocks; d->KS = kernel; d->S = spk_dim; d->dt = dtype;
-  d->MS = (6 * n_blocks + 5) * H;
+  d->MS0 = (6 * n_blocks + 5) * H;
+  d->fold = dtype == FLAMED_BF16;
+  d->MS = d->MS0 + (d->fold ? n_blocks * 2 * H + 2 * 3 * C : 0);
   *out = reinterpret_cast<flamed_den_t>(d);
   return kOk;
 }
@@ -1030,7 +1153,7 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
   size_t o_t0w = take(4ull * H * 256), o_t0b = take(4ull * H), o_t2w = take(4ull * H * H), o_t2b = take(4ull * H);
   size_t o_cw = take(4ull * H * S), o_cb = take(4ull * H);
-  size_t o_adaw = take(4ull * d->MS * H), o_adab = take(4ull * d->MS);
+  size_t o_adaw = take(4ull * d->MS0 * H), o_adab = take(4ull * d->MS0);
   size_t o_win = take(es * H * C);
   std::vector<size_t> o_blk(NB);
   for (int i = 0; i < NB; ++i) o_blk[i] = take(es * 4ull * H * H);
@@ -1109,6 +1232,11 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   return kOk;
 }
 
+FLAMED_API int flamed_den_mods_stride(flamed_den_t h) {
+  Den* d = reinterpret_cast<Den*>(h);
+  return d ? d->MS : 0;
+}
+
 FLAMED_API size_t flamed_den_adaln_workspace_size(flamed_den_t h, int n_t, int n_spk) {
   Den* d = reinterpret_cast<Den*>(h);
   if (!d) return 0;
@@ -1137,7 +1265,21 @@ FLAMED_API int flamed_den_adaln(flamed_den_t h, const float* t_vals, int n_t, co
   if ((rc = launch_gemm<float>(LoadF32<float>{F, 256}, d->t0w, 256, EpiBiasAct<float, 2>{d->t0b, T1, H}, n_t, H, 256, st))) return rc;
   if ((rc = launch_gemm<float>(LoadF32<float>{T1, H}, d->t2w, H, EpiBiasAct<float, 0>{d->t2b, TE, H}, n_t, H, H, st))) return rc;
   if ((rc = launch_gemm<float>(LoadF32<float>{spk, d->S}, d->cw, d->S, EpiBiasAct<float, 0>{d->cb, CE, H}, n_spk, H, d->S, st))) return rc;
-  if ((rc = launch_gemm<float>(LoadAdaY{TE, CE, tidx, sidx, H}, d->adaw, H, EpiBiasAct<float, 0>{d->adab, mods, d->MS}, R, d->MS, H, st))) return rc;
+  if ((rc = launch_gemm<float>(LoadAdaY{TE, CE, tidx, sidx, H}, d->adaw, H, EpiBiasAct<float, 0>{d->adab, mods, d->MS}, R, d->MS0, H, st))) return rc;
+  if (d->fold) {  // LayerNorm-fold tables of every mlp.0 / conv_out GEMM for these rows (den_fold_gemms)
+    for (int i = 0; i <= d->NB; ++i) {
+      const bool fin = i == d->NB;
+      const float* md = mods + (size_t)i * 6 * H + 3 * H;  // [shift, scale] of the LN feeding this GEMM
+      const bf16* W = reinterpret_cast<const bf16*>(fin ? d->wout : d->blk[i].m0);
+      const int N = fin ? 3 * d->C : H;
+      float* wa = mods + d->MS0 + (size_t)i * 2 * H;
+      const float* lw = fin ? nullptr : d->blk[i].lnmw;
+      const float* lb = fin ? nullptr : d->blk[i].lnmb;
+      const float* bias = fin ? nullptr : d->blk[i].mb0;
+      if ((rc = launch_gemm<bf16>(LoadFold<0>{md + H, md, d->MS, lw, lb}, W, H, EpiBiasAct<float, 0>{nullptr, wa, d->MS}, R, N, H, st))) return rc;
+      if ((rc = launch_gemm<bf16>(LoadFold<1>{md + H, md, d->MS, lw, lb}, W, H, EpiBiasAct<float, 0>{bias, wa + N, d->MS}, R, N, H, st))) return rc;
+    }
+  }
   return kOk;
 }
 
@@ -1194,6 +1336,7 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   } a16_scope(w.A16);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
+  const bool fold = std::is_same<DT, bf16>::value && d->fold && g_lnfold && w.XA;
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (g_stamp_class >= 0) stamp_select(cls, st); TRY(x); if (g_dup_class == (cls)) TRY(x); kt_mark(cls, st); } while (0)
@@ -1207,11 +1350,21 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
     K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
                                         EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
-    K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
-                                        EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
-                                        M, H, H, st)));
-    K_(5, (den_gemm<DT>(cfg, true, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
-                                        EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
+    if (fold) {  // mlp.0 on x * alpha (written by conv_3's epilogue) with the LayerNorm in its epilogue
+      K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+                                          EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT,
+                                                                 w.XA, Bw.lnmw, md + 4 * H},
+                                          M, H, H, st)));
+      K_(5, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.XA, H}, (const DT*)Bw.m0, H,
+                                          EpiLNFold<DT, 2>{U, H, w.S1, NT, BN, 1e-6f, mods + d->MS0 + (size_t)i * 2 * H, H, MS, mod_div, so},
+                                          M, H, H, st)));
+    } else {
+      K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
+                                          EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
+                                          M, H, H, st)));
+      K_(5, (den_gemm<DT>(cfg, true, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
+                                          EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
+    }
     K_(6, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
                                         EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st)));
   }
@@ -1222,11 +1375,21 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
   K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
   K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
-  K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
-                                      EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
-                                      M, H, H, st)));
-  K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
-                                      EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
+  if (fold) {
+    K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
+                                        EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT,
+                                                                w.XA, nullptr, mf + 4 * H},
+                                        M, H, H, st)));
+    K_(7, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.XA, H}, (const DT*)d->wout, H,
+                                        EpiLNFold<float, 0>{w.Y, 3 * C, w.S1, NT, BN, 1e-6f, mods + d->MS0 + (size_t)d->NB * 2 * H, 3 * C, MS, mod_div, so},
+                                        M, 3 * C, H, st)));
+  } else {
+    K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
+                                        EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
+                                        M, H, H, st)));
+    K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
+                                        EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
+  }
   {
     size_t n = (size_t)M * C;
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, ctr);
@@ -1353,6 +1516,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   if (k == "stamp_class") { g_stamp_class = value; return kOk; }
   if (k == "dw_cg") { FL_REQUIRE(value == 16 || value == 32, "flamed_tune: dw_cg in {16, 32}"); g_dw_cg_small = value; return kOk; }
   if (k == "dw_cg32") { FL_REQUIRE(value >= 0, "flamed_tune: dw_cg32 >= 0"); g_dw_cg32_rows = value; return kOk; }
+  if (k == "lnfold") { g_lnfold = value != 0; return kOk; }
   if (k == "dma_ns") { FL_REQUIRE(value == 3 || value == 4 || value == 6 || value == 8, "flamed_tune: dma_ns in {3, 4, 6, 8}"); g_dma_ns = value; return kOk; }
   if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
   if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }

@@ -28,6 +28,7 @@ SIGNATURES = {
     "flamed_den_destroy": (c_int, [P]),
     "flamed_den_num_weights": (c_int, [P]),
     "flamed_den_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_den_mods_stride": (c_int, [P]),
     "flamed_den_adaln_workspace_size": (c_size_t, [P, c_int, c_int]),
     "flamed_den_adaln": (c_int, [P, P, c_int, P, c_int, P, P, c_int, P, P, c_size_t, P]),
     "flamed_den_workspace_size": (c_size_t, [P, c_int, c_int]),

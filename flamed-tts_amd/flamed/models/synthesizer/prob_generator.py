@@ -362,7 +362,7 @@ class DenoiserHIP:
         tidx = tidx.to(device=dev, dtype=torch.int32).contiguous()
         sidx = sidx.to(device=dev, dtype=torch.int32).contiguous()
         R = tidx.numel()
-        ms = (6 * self.den.num_res_blocks + 5) * self.den.model_channels
+        ms = L.flamed_den_mods_stride(self.handle)  # modulation floats (+ LayerNorm-fold tables, bf16)
         mods = torch.empty((R, ms), dtype=torch.float32, device=dev)
         nbytes = L.flamed_den_adaln_workspace_size(self.handle, t_vals.numel(), spk.shape[0])
         ws = self.ada_ws.get(nbytes, dev)

@@ -59,9 +59,13 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* weights, int 
 
 /* AdaLN precompute for R modulation rows (TimestepEmbedder :35-72, cond_embed :358, y = t + c :359,
  * every adaLN_modulation Linear :131-134/:224-227 at once).  Row r uses t_vals[tidx[r]] and
- * spk[sidx[r]] (tidx/sidx: device int32[R]).  mods: R x ((6*n_blocks+5)*hidden) fp32, per row the
- * chunks [shift_c, scale_c, gate_c, shift_m, scale_m, gate_m] per block then the final layer's
- * [shift_c, scale_c, gate_c, shift_o, scale_o]. */
+ * spk[sidx[r]] (tidx/sidx: device int32[R]).  mods: R x flamed_den_mods_stride(h) fp32; per row
+ * first the (6*n_blocks+5)*hidden modulation floats — chunks [shift_c, scale_c, gate_c, shift_m,
+ * scale_m, gate_m] per block then the final layer's [shift_c, scale_c, gate_c, shift_o, scale_o] —
+ * and, for bf16 handles, the LayerNorm-fold tables of the LN-consuming GEMMs: per block
+ * [W_mlp0 alpha_m, W_mlp0 beta_m + b_mlp0] (2 x hidden), then [W_out alpha_o, W_out beta_o]
+ * (2 x 3 latent_dim; alpha = w (1 + scale), beta = b (1 + scale) + shift of that LayerNorm). */
+FLAMED_API int flamed_den_mods_stride(flamed_den_t h);
 FLAMED_API size_t flamed_den_adaln_workspace_size(flamed_den_t h, int n_t, int n_spk);
 FLAMED_API int flamed_den_adaln(flamed_den_t h, const float* t_vals, int n_t, const float* spk, int n_spk,
                                 const int* tidx, const int* sidx, int R, float* mods, void* ws, size_t ws_bytes,
@@ -118,6 +122,9 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     pipeline (gemm_dma.hpp); 2: also those with fp32 (LayerNorm/GroupNorm) A
  *                     operands; 0: the register-staged main loop only;
  *   "dma_ns"        — LDS ring depth of those tiles: 3 (default), 4, 6 or 8;
+ *   "lnfold"        — 1 (default, bf16 handles): mlp.0 and conv_out run as plain bf16 GEMMs on
+ *                     x * alpha (written by the preceding conv_3 epilogue) with the LayerNorm and
+ *                     modulation folded into their epilogues; 0: applied in the A-operand loader;
  *   "bn32"          — 1 (default): denoiser GEMMs over fewer than 320 rows use 32 x 32 tiles (LN row
  *                     partials 32 columns wide); 0: 32 x 64 as above 320 rows;
  *   "big"           — 1 (default): bf16 denoiser steps over >= big_rows rows write each transforming A

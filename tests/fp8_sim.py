@@ -1,7 +1,8 @@
 """CPU estimate of what fp8 (OCP e4m3) pointwise projections would cost in accuracy (BASELINE configs[4]):
 the oracle denoiser forward with every GEMM's weights quantized per output channel (amax/448) and its
 input activations quantized at unit scale (clamped to +-448), against fp32; the same with bf16 rounding.
-Usage: PYTHONPATH=flamed-tts_amd:. python tools/fp8_sim.py   (runs from tests/ helpers; CPU only)."""
+Usage: PYTHONPATH=flamed-tts_amd:. python tests/fp8_sim.py   (CPU only; lives under tests/ because it runs the
+oracle, which only test code may import)."""
 import os
 import sys
 
@@ -9,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tests"))
+sys.path.insert(0, HERE)
 from _common import seeded, orc  # noqa: E402  (checker only)
 
 NAMES = ["proj_in", "conv_2", "conv_3", "mlp.0", "mlp.2", "conv_out"]

@@ -167,6 +167,7 @@ def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
     ({"dma": 0, "bn32": 1}, 1, 200), ({"dma": 2, "bn32": 1}, 1, 200), ({"dma": 1, "bn32": 1}, 3, 1000),
     ({"big_ns": 3}, 17, 500), ({"big": 1, "dw_tc": 128}, 17, 500),
     ({"dw_cg": 16}, 2, 300), ({"dw_cg32": 0}, 1, 131), ({"dma_ns": 8}, 1, 400), ({"dma_ns": 4, "dma": 2}, 1, 250),
+    ({"lnfold": 0}, 1, 400), ({"lnfold": 0}, 17, 500), ({"lnfold": 0, "big": 0}, 5, 400),
 ])
 def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     """Every GEMM main-loop / tile / pipeline variant behind flamed_tune computes the same velocity (vs the
@@ -180,7 +181,7 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     t = torch.tensor([[0.35]])
     ref = orc.denoiser_forward(sd, x, t, c)
     L = nat.lib()
-    defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536, "dma_ns": 3}
+    defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536, "dma_ns": 3, "lnfold": 1}
     try:
         for k, v in knobs.items():
             nat.check(L.flamed_tune(k.encode(), v), "tune")
@@ -189,3 +190,26 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
         for k in knobs:
             nat.check(L.flamed_tune(k.encode(), defaults[k]), "tune")
     assert rel_l2(v_hip, ref) < 2e-2
+
+
+@pytest.mark.parametrize("B,T,per_frame_t", [(1, 400, False), (2, 300, True), (17, 500, False)])
+def test_lnfold_error_budget(B, T, per_frame_t, pg_bf16):
+    """The LayerNorm fold (mlp.0 / conv_out on bf16 x*alpha with rstd (acc - mean wa) + wb in the epilogue)
+    keeps the bf16 velocity error at the level of the A-loader LayerNorm path: at most 1.5x its rel-L2
+    (+1e-3) against the fp32 oracle, small-M (DMA), per-frame-t and large-M (128x128) paths."""
+    from flamed import _native as nat
+    pg, sd = pg_bf16
+    g = torch.Generator().manual_seed(B * 5 + T)
+    x = torch.randn(B, T, 256, generator=g)
+    c = torch.randn(B, 256, generator=g)
+    t = torch.rand(B, T, generator=g) if per_frame_t else torch.tensor([[0.55]])
+    ref = orc.denoiser_forward(sd, x, t, c)
+    L = nat.lib()
+    e_fold = rel_l2(_vel(pg, x, t, c), ref)
+    try:
+        nat.check(L.flamed_tune(b"lnfold", 0), "tune")
+        e_ln = rel_l2(_vel(pg, x, t, c), ref)
+    finally:
+        nat.check(L.flamed_tune(b"lnfold", 1), "tune")
+    print(f"bf16 velocity rel-L2: lnfold {e_fold:.3e}, A-loader LN {e_ln:.3e}")
+    assert e_fold < 1.5 * e_ln + 1e-3
