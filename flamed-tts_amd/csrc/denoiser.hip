@@ -298,9 +298,7 @@ struct EpiConvNeXtResid {
       const int slot = m / mod.div - bm / mod.div;
       const float* v = vec + slot * 3 * S + (n - bn);
       float h = xh * v[0] + v[S];
-      const float r = x + v[2 * S] * (h + (acc + vec[6 * S + (n - bn)]));
-      if (ya) ya[(size_t)m * ld + n] = (bf16)(r * vec[(7 + slot) * S + (n - bn)]);
-      return r;
+      return x + v[2 * S] * (h + (acc + vec[6 * S + (n - bn)]));
     }
     const long long so = mod.so.get();
     const ModRef md = mod.at();
@@ -308,9 +306,27 @@ struct EpiConvNeXtResid {
     float sc1 = 1.0f + md.sc[mo];
     float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
     float h = xh * (w * sc1) + (b * sc1 + md.sh[mo]);
-    const float r = x + gate[so + mo] * (h + (acc + b3[n]));
-    if (ya) ya[(size_t)m * ld + n] = (bf16)(r * ((yw ? yw[n] : 1.0f) * (1.0f + ysc[so + mo])));
-    return r;
+    return x + gate[so + mo] * (h + (acc + b3[n]));
+  }
+  // alpha_next of column n for row m (staged, or from the mods table)
+  __device__ float alpha_next(int m, int n, const float* vec, bool use, int bm, int bn) const {
+    if (use) return vec[(7 + m / mod.div - bm / mod.div) * kEVecStride + (n - bn)];
+    const size_t mo = (size_t)(m / mod.div) * mod.ms + n;
+    return (yw ? yw[n] : 1.0f) * (1.0f + ysc[mod.so.get() + mo]);
+  }
+  static constexpr bool kStoreV = true;
+  __device__ void store_v(int m, int n, float v, const float* vec, bool use, int bm, int bn) const {
+    X[(size_t)m * ld + n] = v;
+    if (ya) ya[(size_t)m * ld + n] = (bf16)(v * alpha_next(m, n, vec, use, bm, bn));
+  }
+  __device__ void store4_v(int m, int n, const float* v, const float* vec, bool use, int bm, int bn) const {
+    store_val4<float>(X + (size_t)m * ld + n, v);
+    if (ya) {
+      float y[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = v[e] * alpha_next(m, n + e, vec, use, bm, bn);
+      store_val4<bf16>(ya + (size_t)m * ld + n, y);
+    }
   }
   __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
   __device__ void store4(int m, int n, const float* v) const { store_val4<float>(X + (size_t)m * ld + n, v); }

@@ -34,6 +34,16 @@ template <class T> struct kevec_of<T, std::void_t<decltype(T::kEVec)>> { static 
 template <class T, class = void> struct kpre_of { static constexpr bool value = false; };
 template <class T> struct kpre_of<T, std::void_t<decltype(T::kPre)>> { static constexpr bool value = T::kPre; };
 
+// Epilogues with a side output that needs the staged per-column vectors (store_v / store4_v) get them
+// at the store; the others take plain store / store4.
+template <class T, class = void> struct kstorev_of { static constexpr bool value = false; };
+template <class T> struct kstorev_of<T, std::void_t<decltype(T::kStoreV)>> { static constexpr bool value = T::kStoreV; };
+template <class EP>
+__device__ __forceinline__ void ep_store(const EP& ep, int m, int n, float v, const float* vec, bool use, int bm, int bn) {
+  if constexpr (kstorev_of<EP>::value) ep.store_v(m, n, v, vec, use, bm, bn);
+  else ep.store(m, n, v);
+}
+
 template <int BM, int BN, int KCH, int NSTAGE, class AL, class EP>
 struct GemmSmem {
   static constexpr int ROWB = KCH * 16;  // unpadded; 16-B chunks XOR-swizzled by row
@@ -462,7 +472,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_kernel(AL al, const DT* __r
       for (int r = 0; r < 4; ++r) {
         int m = bm + wr * WTM + i * 16 + fq * 4 + r;
         int n = bn + wc * WTN + j * 16 + fr;
-        if (m < M) ep.store(m, n, val[i][j][r]);
+        if (m < M) ep_store(ep, m, n, val[i][j][r], e_vec, e_uv, bm, bn);
       }
   FL_STAMP(4);
 }

@@ -67,8 +67,10 @@ struct has_store4<T, std::void_t<decltype(std::declval<const T&>().store4(0, 0, 
   static constexpr bool value = true;
 };
 template <class EP>
-__device__ __forceinline__ void store4(const EP& ep, int m, int n, const float* v) {
-  if constexpr (has_store4<EP>::value) {
+__device__ __forceinline__ void store4(const EP& ep, int m, int n, const float* v, const float* vec, bool use, int bm, int bn) {
+  if constexpr (kstorev_of<EP>::value) {
+    ep.store4_v(m, n, v, vec, use, bm, bn);
+  } else if constexpr (has_store4<EP>::value) {
     ep.store4(m, n, v);
   } else {
 #pragma unroll
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
         for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o);
         if ((tid & 31) == 0 && bm + row < M) ep.store_stats(bm + row, tx, mean, q);
       }
-      if (bm + row < M) store4(ep, bm + row, bn + c, v);
+      if (bm + row < M) store4(ep, bm + row, bn + c, v, e_vec, e_uv, bm, bn);
     }
   } else {
     // ---- epilogue (gemm_kernel's, verbatim in effect)
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
         for (int r = 0; r < 4; ++r) {
           int m = bm + wr * WTM + i * 16 + fq * 4 + r;
           int n = bn + wc * WTN + j * 16 + fr;
-          if (m < M) ep.store(m, n, val[i][j][r]);
+          if (m < M) ep_store(ep, m, n, val[i][j][r], e_vec, e_uv, bm, bn);
         }
   }
   FL_STAMP(4);
