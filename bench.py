@@ -37,6 +37,7 @@ KERNEL_NAMES = ["proj_in_gemm", "lnmod_dwconv_gnpartials", "gn_finalize", "gnapp
 N_CLASSES = len(KERNEL_NAMES)
 HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md chip table (spec)
 MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}   # dense peaks
+FOLD = None  # LayerNorm fold active (set in main: bf16 and flamed_tune lnfold != 0)
 
 
 def parse():
@@ -73,9 +74,14 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int):
+def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fold: bool | None = None):
     """Algorithmic (bytes, flops) per launch of each kernel class, and launches per Euler step.
-    Bytes = every operand read once + every output written once."""
+    Bytes = every operand read once + every output written once.  With the
+    LayerNorm fold (bf16 default) conv_3 also writes x*alpha in bf16 and mlp.0 / conv_out read it
+    instead of the fp32 residual stream."""
+    if fold is None:
+        fold = es == 2
+    ea = 2 if fold else 4  # bytes per A element of the LayerNorm-consuming GEMMs
     M = B * T
     NT = H // 64
     TS = (T + 63) // 64
@@ -89,13 +95,13 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int):
     if cls == 3:
         return M * H * 4 + B * H * 8 + H * H * es + M * H * es, 2 * M * H * H, NB + 1
     if cls == 4:
-        return M * H * es + H * H * es + 2 * M * H * 4 + 2 * stats, 2 * M * H * H, NB + 1
+        return M * H * es + H * H * es + 2 * M * H * 4 + 2 * stats + (M * H * 2 if fold else 0), 2 * M * H * H, NB + 1
     if cls == 5:
-        return M * H * 4 + stats + H * H * es + M * H * es, 2 * M * H * H, NB
+        return M * H * ea + stats + H * H * es + M * H * es, 2 * M * H * H, NB
     if cls == 6:
         return M * H * es + H * H * es + 2 * M * H * 4 + stats, 2 * M * H * H, NB
     if cls == 7:
-        return M * H * 4 + stats + 3 * C * H * es + M * 3 * C * 4, 2 * M * 3 * C * H, 1
+        return M * H * ea + stats + 3 * C * H * es + M * 3 * C * 4, 2 * M * 3 * C * H, 1
     return M * 3 * C * 4 + 2 * M * C * 4, 4 * M * C, 1
 
 
@@ -228,12 +234,12 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
     for cls in range(N_CLASSES):
         if cls == 2 and ms[cls] <= 0.0:
             continue
-        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es, FOLD)
         t = max(ms[cls], 1e-6) * 1e-3
         ks.append({"name": KERNEL_NAMES[cls], "us": round(ms[cls] * 1e3, 2), "per_step": per_step,
                    "GBps": round(nbytes / t / 1e9, 1), "TFLOPs": round(flops / t / 1e12, 2)})
     dom = max(ks, key=lambda k: k["us"] * k["per_step"])
-    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es)
+    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es, FOLD)
     ridge = MFMA_PEAK_TFS[args.dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
     if flops / nbytes > ridge:
         roof = {"bound": "mfma", "achieved": dom["TFLOPs"], "peak": MFMA_PEAK_TFS[args.dtype], "unit": "TFLOP/s"}
@@ -249,7 +255,9 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
 
 
 def main():
+    global FOLD
     args = parse()
+    FOLD = args.dtype == "bf16" and args.lnfold != 0
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -328,7 +336,7 @@ def main():
     es = 2 if args.dtype == "bf16" else 4
     kernels = []
     for cls in range(N_CLASSES):
-        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es, FOLD)
         if cls == 2 and ms[cls] <= 0.0:  # GroupNorm finalize fused into class 1 (the last-arriving block)
             continue
         t = max(ms[cls], 1e-6) * 1e-3

@@ -22,9 +22,9 @@ CLASSES = [
     ("gn_finalize", [r"gn_finalize_kernel"]),
     ("gnapply_conv2_gemm_gelu", [r"LoadGN"]),
     ("conv3_gemm_gated_resid", [r"EpiConvNeXtResid"]),
-    ("lnmod_mlp0_gemm_silu", [r"LoadLNMod<[^>]*true>", r"LoadLNModI\w+Lb1E"]),
+    ("lnmod_mlp0_gemm_silu", [r"LoadLNMod<[^>]*true>", r"LoadLNModI\w+Lb1E", r"EpiLNFold<[^>]*bf16", r"EpiLNFoldIDF16b"]),
     ("mlp2_gemm_gated_resid", [r"EpiGatedResid"]),
-    ("lnmod_conv_out_gemm", [r"LoadLNMod<[^>]*false>", r"LoadLNModI\w+Lb0E"]),
+    ("lnmod_conv_out_gemm", [r"LoadLNMod<[^>]*false>", r"LoadLNModI\w+Lb0E", r"EpiLNFold<float", r"EpiLNFoldIf"]),
     ("conv_out_combine_euler", [r"conv3_combine_kernel"]),
 ]
 
