@@ -5,6 +5,8 @@
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
 
+#include <vector>
+
 namespace fl {
 
 __global__ void empty_kernel(int* p) {
@@ -229,6 +231,25 @@ __global__ __launch_bounds__(256) void stream_probe_kernel(const char* __restric
   }
   if (acc == 12345.678f) out[blockIdx.x] = acc;
 }
+// L2 warm-up of the NEXT GEMM's weights (probe): `gridDim.x` workgroups, those of XCD x (dispatch id
+// mod 8) together read all `bytes` of w, so every XCD's L2 ends up holding the whole matrix.
+__global__ __launch_bounds__(256) void l2_prefetch_kernel(const char* __restrict__ w, size_t bytes, float* sink) {
+  const int per = gridDim.x >> 3, j = blockIdx.x >> 3;
+  const size_t slice = (bytes / per + 4095) & ~(size_t)4095;
+  const size_t b0 = (size_t)j * slice, b1 = b0 + slice < bytes ? b0 + slice : bytes;
+  float acc = 0.f;
+  for (size_t o = b0 + (size_t)threadIdx.x * 16; o < b1; o += 256 * 16 * 4) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t q = o + (size_t)u * 256 * 16;
+      v[u] = q < b1 ? *reinterpret_cast<const u32x4*>(w + q) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += __uint_as_float(v[u].x);
+  }
+  if (acc == 12345.678f && sink) sink[blockIdx.x] = acc;
+}
 }  // namespace fl
 
 using namespace fl;
@@ -244,6 +265,40 @@ FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int
     return probe_variant(variant, (const bf16*)A, w, (bf16*)C, M, N, K, s);
   };
   return time_graph(body, reps, st, us_out);
+}
+
+// GEMM chain with a concurrent L2 warm-up of the next launch's weights on a second captured stream
+// (pf_blocks workgroups; 0 = no warm-up, same graph shape otherwise).
+FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, int wbufs, int pf_blocks, const void* A,
+                                    const void* W, void* C, float* us_out, hipStream_t st) {
+  FL_REQUIRE(A && W && C && us_out && reps > 1 && wbufs > 0 && pf_blocks >= 0 && pf_blocks % 8 == 0, "flamed_probe_gemm_pf: bad args");
+  hipStream_t s1;
+  FL_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  std::vector<hipEvent_t> evs;
+  auto mk = [&]() { hipEvent_t e; (void)hipEventCreateWithFlags(&e, hipEventDisableTiming); evs.push_back(e); return e; };
+  std::vector<hipEvent_t> done(reps, nullptr);
+  int i = 0;
+  const size_t wbytes = (size_t)N * K * 2;
+  auto body = [&](hipStream_t cap) -> int {
+    const int k = i++;
+    if (pf_blocks && k + 1 < reps) {  // warm W[k+1] while GEMM k runs (starts when GEMM k-1 has finished)
+      hipEvent_t e0 = mk();
+      FL_HIP(hipEventRecord(e0, cap));
+      FL_HIP(hipStreamWaitEvent(s1, e0, 0));
+      const char* wn = (const char*)W + (size_t)((k + 1) % wbufs) * wbytes;
+      hipLaunchKernelGGL(l2_prefetch_kernel, dim3(pf_blocks), dim3(256), 0, s1, wn, wbytes, nullptr);
+      FL_LAUNCH_CHECK();
+      done[k + 1] = mk();
+      FL_HIP(hipEventRecord(done[k + 1], s1));
+    }
+    if (done[k]) FL_HIP(hipStreamWaitEvent(cap, done[k], 0));
+    const bf16* w = (const bf16*)W + (size_t)(k % wbufs) * N * K;
+    return probe_variant(variant, (const bf16*)A, w, (bf16*)C, M, N, K, cap);
+  };
+  const int rc = time_graph(body, reps, st, us_out);
+  for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(s1);
+  return rc;
 }
 
 FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t st) {

@@ -41,6 +41,7 @@ SIGNATURES = {
     "flamed_stamp_buffer": (c_int, [P]),
     "flamed_probe_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_empty": (c_int, [c_int, c_int, ctypes.POINTER(c_float), P]),
+    "flamed_probe_gemm_pf": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
     "flamed_dur_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(P)]),
     "flamed_dur_destroy": (c_int, [P]),

@@ -160,6 +160,10 @@ FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int
  * (mode 1: LDS-DMA ring, mode 0: register loads).  src must hold blocks x kb KB. */
 FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const void* src, float* us_out, hipStream_t stream);
 FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t stream);
+/* flamed_probe_gemm_pf: flamed_probe_gemm's chain with a concurrent L2 warm-up of the next launch's
+ * weights on a second captured stream (pf_blocks workgroups, a multiple of 8; 0 = none). */
+FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, int wbufs, int pf_blocks, const void* A,
+                                    const void* W, void* C, float* us_out, hipStream_t stream);
 
 /* ==================== PVA duration / silence generators + length regulator ====================
  * Replaces ProbabilisticModule.forward (pva.py:221-238) inside the Euler loop of PVA.sample
