@@ -79,10 +79,10 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fol
     Bytes = every operand read once + every output written once.  With the
     LayerNorm fold (bf16 default) conv_3 also writes x*alpha in bf16 and mlp.0 / conv_out read it
     instead of the fp32 residual stream."""
-    if fold is None:
-        fold = es == 2
-    ea = 2 if fold else 4  # bytes per A element of the LayerNorm-consuming GEMMs
     M = B * T
+    if fold is None:  # the denoiser's default policy: folded below the large-M path and from 6144 rows on it
+        fold = es == 2 and FOLD is not False and (M < 1536 or M >= 6144)
+    ea = 2 if fold else 4  # bytes per A element of the LayerNorm-consuming GEMMs
     NT = H // 64
     TS = (T + 63) // 64
     stats = M * NT * 8
@@ -234,12 +234,12 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
     for cls in range(N_CLASSES):
         if cls == 2 and ms[cls] <= 0.0:
             continue
-        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es, FOLD)
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
         t = max(ms[cls], 1e-6) * 1e-3
         ks.append({"name": KERNEL_NAMES[cls], "us": round(ms[cls] * 1e3, 2), "per_step": per_step,
                    "GBps": round(nbytes / t / 1e9, 1), "TFLOPs": round(flops / t / 1e12, 2)})
     dom = max(ks, key=lambda k: k["us"] * k["per_step"])
-    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es, FOLD)
+    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es)
     ridge = MFMA_PEAK_TFS[args.dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
     if flops / nbytes > ridge:
         roof = {"bound": "mfma", "achieved": dom["TFLOPs"], "peak": MFMA_PEAK_TFS[args.dtype], "unit": "TFLOP/s"}
@@ -257,7 +257,7 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
 def main():
     global FOLD
     args = parse()
-    FOLD = args.dtype == "bf16" and args.lnfold != 0
+    FOLD = args.lnfold != 0  # flamed_tune lnfold (kernel_costs applies the size policy)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -336,7 +336,7 @@ def main():
     es = 2 if args.dtype == "bf16" else 4
     kernels = []
     for cls in range(N_CLASSES):
-        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es, FOLD)
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
         if cls == 2 and ms[cls] <= 0.0:  # GroupNorm finalize fused into class 1 (the last-arriving block)
             continue
         t = max(ms[cls], 1e-6) * 1e-3

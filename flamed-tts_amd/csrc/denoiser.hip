@@ -1000,6 +1000,11 @@ static int launch_big(const LoadPlain<bf16>& al, const bf16* W, int ldw, const E
 // flamed_tune "lnfold": 1 (default, bf16 handles) mlp.0 / conv_out run as plain bf16 GEMMs with the
 // LayerNorm folded into the epilogue (EpiLNFold); 0: LayerNorm + modulation in the A loader.
 static int g_lnfold = 1;
+// On the large-M path the fold pays only from this many rows (flamed_tune "fold_rows"): measured
+// (ms/solve, fold vs not) M = 1600: 84.8 vs 81.7, 2400 (nfe 256): 187.1 vs 182.8, 3200: 94.2 vs 93.2,
+// 6400: 116.2 vs 118.0, 25600: 409.5 vs 411.1 — with few 128 x 128 tiles the x*alpha stores lengthen
+// conv_3 more than the dropped LayerNorm pass saves.
+static int g_fold_big_rows = 6144;
 
 // Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
 template <typename DT, class AL, class EP>
@@ -1352,7 +1357,7 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   } a16_scope(w.A16);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
-  const bool fold = std::is_same<DT, bf16>::value && d->fold && g_lnfold && w.XA;
+  const bool fold = std::is_same<DT, bf16>::value && d->fold && g_lnfold && w.XA && (!big || M >= g_fold_big_rows);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (g_stamp_class >= 0) stamp_select(cls, st); TRY(x); if (g_dup_class == (cls)) TRY(x); kt_mark(cls, st); } while (0)
@@ -1533,6 +1538,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   if (k == "dw_cg") { FL_REQUIRE(value == 16 || value == 32, "flamed_tune: dw_cg in {16, 32}"); g_dw_cg_small = value; return kOk; }
   if (k == "dw_cg32") { FL_REQUIRE(value >= 0, "flamed_tune: dw_cg32 >= 0"); g_dw_cg32_rows = value; return kOk; }
   if (k == "lnfold") { g_lnfold = value != 0; return kOk; }
+  if (k == "fold_rows") { FL_REQUIRE(value >= 0, "flamed_tune: fold_rows >= 0"); g_fold_big_rows = value; return kOk; }
   if (k == "dma_ns") { FL_REQUIRE(value == 3 || value == 4 || value == 6 || value == 8, "flamed_tune: dma_ns in {3, 4, 6, 8}"); g_dma_ns = value; return kOk; }
   if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
   if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }
