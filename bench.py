@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--dw-cg", type=int, default=None, help="flamed_tune dw_cg (16 or 32)")
     ap.add_argument("--dma-ns", type=int, default=None, help="flamed_tune dma_ns (small-M DMA ring depth)")
     ap.add_argument("--lnfold", type=int, default=None, help="flamed_tune lnfold (LayerNorm folded into mlp.0/conv_out epilogues)")
+    ap.add_argument("--graph-steps", type=int, default=None, help="flamed_tune graph_steps (Euler steps per captured graph)")
     ap.add_argument("--dw-cg32", type=int, default=None, help="flamed_tune dw_cg32 (rows below which 32-channel dwconv)")
     ap.add_argument("--dw-tc", type=int, default=None, help="flamed_tune dw_tc (large-M depthwise T-chunk)")
     ap.add_argument("--bn32", type=int, default=None, help="flamed_tune bn32 (32-wide small-M GEMM tiles)")
@@ -273,7 +274,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "xcd_strips"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")

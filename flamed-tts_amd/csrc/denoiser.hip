@@ -1434,10 +1434,12 @@ static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, in
   return den_step_impl<float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
 }
 
-// Steps per captured graph: the largest divisor of nfe that is <= 16 (the graph is replayed nfe/G
-// times per solve, so a new (B, T) costs one G-step capture instead of an nfe-step one).
+// Steps per captured graph: the largest divisor of nfe that is <= g_graph_steps (flamed_tune
+// "graph_steps", default 16; the graph is replayed nfe/G times per solve, so a new (B, T) costs one
+// G-step capture instead of an nfe-step one).
+static int g_graph_steps = 16;
 static int graph_chunk(int nfe) {
-  for (int g = 16; g > 1; --g)
+  for (int g = g_graph_steps < nfe ? g_graph_steps : nfe; g > 1; --g)
     if (nfe % g == 0) return g;
   return 1;
 }
@@ -1538,6 +1540,7 @@ FLAMED_API int flamed_tune(const char* key, int value) {
   if (k == "dw_cg") { FL_REQUIRE(value == 16 || value == 32, "flamed_tune: dw_cg in {16, 32}"); g_dw_cg_small = value; return kOk; }
   if (k == "dw_cg32") { FL_REQUIRE(value >= 0, "flamed_tune: dw_cg32 >= 0"); g_dw_cg32_rows = value; return kOk; }
   if (k == "lnfold") { g_lnfold = value != 0; return kOk; }
+  if (k == "graph_steps") { FL_REQUIRE(value >= 1 && value <= 1024, "flamed_tune: graph_steps in [1, 1024]"); g_graph_steps = value; return kOk; }
   if (k == "fold_rows") { FL_REQUIRE(value >= 0, "flamed_tune: fold_rows >= 0"); g_fold_big_rows = value; return kOk; }
   if (k == "dma_ns") { FL_REQUIRE(value == 3 || value == 4 || value == 6 || value == 8, "flamed_tune: dma_ns in {3, 4, 6, 8}"); g_dma_ns = value; return kOk; }
   if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }

@@ -126,6 +126,7 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     x * alpha (written by the preceding conv_3 epilogue) with the LayerNorm and
  *                     modulation folded into their epilogues; 0: applied in the A-operand loader;
  *   "fold_rows"     — on the large-M path the fold is used from this many rows (default 6144);
+ *   "graph_steps"   — Euler steps per captured solve graph (largest divisor of nfe up to this; 16);
  *   "bn32"          — 1 (default): denoiser GEMMs over fewer than 320 rows use 32 x 32 tiles (LN row
  *                     partials 32 columns wide); 0: 32 x 64 as above 320 rows;
  *   "big"           — 1 (default): bf16 denoiser steps over >= big_rows rows write each transforming A
