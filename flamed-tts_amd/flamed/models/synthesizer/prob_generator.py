@@ -371,10 +371,18 @@ class DenoiserHIP:
                                      nat.stream_ptr(dev)), "flamed_den_adaln")
         return mods
 
+    def _check_groupnorm(self, B: int, T: int):
+        """The reference's GroupNorm(H, H) over T (F.group_norm's batch-size check) rejects a single
+        value per channel; the HIP path raises the same ValueError instead of normalising it."""
+        if B * T == 1:
+            raise ValueError(f"Expected more than 1 value per channel when training, got input size "
+                             f"{[1, self.den.model_channels, 1]}")
+
     def velocity(self, x: torch.Tensor, t: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
         dev = x.device
         self._ensure(dev)
         B, T, C = x.shape
+        self._check_groupnorm(B, T)
         if t.dim() != 2:
             raise ValueError(f"t must be 2-D ((1,1), (B,1) or (B,T)); got shape {tuple(t.shape)}")
         tb, tt = t.shape
@@ -403,6 +411,7 @@ class DenoiserHIP:
         dev = xt.device
         self._ensure(dev)
         B, T, C = xt.shape
+        self._check_groupnorm(B, T)
         L = nat.lib()
         key = (B, T, nfe)
         bufs = self._solve_bufs.get(key)

@@ -53,7 +53,7 @@ def test_velocity_golden(mode, tol, pg_f32, pg_bf16):
     assert rel_l2(_vel(pg, g["xB"], g["t_mid"], g["cB"]), g["vB1"]) < tol    # batched, padded-free
 
 
-@pytest.mark.parametrize("B,T", [(1, 33), (3, 70), (2, 130)])
+@pytest.mark.parametrize("B,T", [(1, 33), (3, 70), (2, 130), (2, 1), (1, 2), (2, 5), (1, 31)])
 def test_velocity_ragged_shapes_f32(B, T, pg_f32):
     pg, sd = pg_f32
     g = torch.Generator().manual_seed(B * 1000 + T)
@@ -217,3 +217,31 @@ def test_lnfold_error_budget(B, T, per_frame_t, pg_bf16):
         nat.check(L.flamed_tune(b"lnfold", 1), "tune")
     print(f"bf16 velocity rel-L2: lnfold {e_fold:.3e}, A-loader LN {e_ln:.3e}")
     assert e_fold < 1.5 * e_ln + 1e-3
+
+
+def test_single_value_groupnorm_raises(pg_f32):
+    """B*T == 1 leaves one value per GroupNorm(H, H) group: the reference's F.group_norm raises ValueError
+    (prob_generator.py:89); the HIP path raises the same error for velocity() and solve()."""
+    pg, sd = pg_f32
+    x, c, t = torch.randn(1, 1, 256), torch.randn(1, 256), torch.tensor([[0.4]])
+    with pytest.raises(ValueError, match="more than 1 value per channel"):
+        orc.denoiser_forward(sd, x, t, c)
+    with pytest.raises(ValueError, match="more than 1 value per channel"):
+        _vel(pg, x, t, c)
+    with pytest.raises(ValueError, match="more than 1 value per channel"):
+        pg.denoiser.hip().solve(x.to(DEV), torch.linspace(0, 1, 5, device=DEV), c.to(DEV), 4)
+
+
+@pytest.mark.parametrize("B,T", [(2, 1), (1, 2), (1, 17), (1, 319), (1, 320), (2, 160), (1, 1535), (1, 1536),
+                                 (3, 512), (4, 1536), (1, 6144)])
+def test_velocity_path_boundaries_bf16(B, T, pg_bf16):
+    """bf16 velocity at the row counts where the dispatch changes path: T shorter than the depthwise
+    halo, 32x32 -> 32x64 tiles (320 rows), small-M -> large-M 128x128 path (1536 rows), LayerNorm fold on
+    the large-M path (6144 rows), single- and multi-utterance tiles."""
+    pg, sd = pg_bf16
+    g = torch.Generator().manual_seed(B * 100 + T)
+    x = torch.randn(B, T, 256, generator=g)
+    c = torch.randn(B, 256, generator=g)
+    t = torch.tensor([[0.3]])
+    ref = orc.denoiser_forward(sd, x, t, c)
+    assert rel_l2(_vel(pg, x, t, c), ref) < 2e-2
