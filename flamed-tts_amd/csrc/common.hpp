@@ -4,6 +4,10 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
+#include <set>
+#include <utility>
+#include <vector>
 
 namespace fl {
 
@@ -48,6 +52,121 @@ enum Status : int {
       return ::fl::kHip;                                                                   \
     }                                                                                      \
   } while (0)
+
+// ---- device pinning ----
+// A handle lives on the device of the weights it was loaded from (hipPointerGetAttributes); every entry
+// point makes that device current for its duration and restores the caller's, so a call from a thread
+// whose current device differs (e.g. `--device cuda:1` in one process) allocates and launches on the
+// handle's device instead of dereferencing its memory from another GPU.
+int device_of(const void* p, int* dev);  // kOk, or kBadArg for a pointer HIP does not know
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if (dev < 0) return;
+    int cur = -1;
+    err = hipGetDevice(&cur);
+    if (err == hipSuccess && cur != dev) {
+      err = hipSetDevice(dev);
+      if (err == hipSuccess) prev = cur;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+#define FL_ON_DEVICE(dev)                                                          \
+  ::fl::DeviceGuard dg_(dev);                                                      \
+  do {                                                                             \
+    if (dg_.err != hipSuccess) {                                                   \
+      ::fl::set_error("%s:%d hipSetDevice(%d) -> %s", __FILE__, __LINE__, (dev),  \
+                      hipGetErrorString(dg_.err));                                 \
+      return ::fl::kHip;                                                           \
+    }                                                                              \
+  } while (0)
+// `p` (a caller tensor) must live on the handle's device `dev`.
+#define FL_REQUIRE_ON(p, dev, what)                                                                   \
+  do {                                                                                                \
+    int pd_ = -1;                                                                                     \
+    if (::fl::device_of((p), &pd_) == ::fl::kOk && (dev) >= 0 && pd_ != (dev)) {                      \
+      ::fl::set_error("%s: tensor on device %d but the handle lives on device %d", (what), pd_, (dev)); \
+      return ::fl::kBadArg;                                                                           \
+    }                                                                                                 \
+  } while (0)
+
+// ---- tuning knobs (flamed_tune / flamed_den_tune) ----
+// Process defaults are set by flamed_tune under a mutex and bump an epoch; a handle snapshots them
+// (or keeps its own, after flamed_den_tune) and every launch of a handle call reads the calling
+// thread's active snapshot (TuneScope), so concurrent calls on different handles / threads never see a
+// knob change halfway through a step.
+struct Tune {
+  int split_target = 1;    // split-K off by default: slower at B = 1 (profiles/r01_splitk_sweep.txt)
+  int split_max = 4;
+  int small_stages = 3;    // small-M register pipeline (3 | 5 | 7)
+  int xcd_strips = 0;      // small/mid-M tile placement strips (0 = off)
+  int bn32 = 1;            // 32 x 32 tiles below kTinyRows rows
+  int use_dma = 1;         // 1: LDS-DMA main loop for bf16-A small-M GEMMs; 2: also fp32-A; 0: off
+  int dma_ns = 3;          // small-M DMA ring depth
+  int noctr = 0;           // diagnostic: ignore the device step counter
+  int dup_class = -1;      // ablation: launch this kernel class twice per step
+  int stamp_class = -1;    // diagnostic (FL_STAMPS builds)
+  int dw_cg32_rows = 1536; // below: narrow depthwise workgroups
+  int dw_cg_small = 32;    // their channel width (16 | 32)
+  int dw_tc_big = 64;      // large-M depthwise T-chunk (64 | 128)
+  int big = 1;             // large-M bf16 path
+  int big_min_rows = 1536;
+  int big_ns = 2;          // its LDS ring depth
+  int lnfold = 1;          // LayerNorm fold into mlp.0 / conv_out epilogues (bf16)
+  int fold_big_rows = 6144;
+  int graph_steps = 16;    // Euler steps per captured solve graph
+};
+int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)
+Tune tune_snapshot(int* epoch);                       // process defaults + their epoch
+int tune_epoch();
+extern thread_local const Tune* tl_tune;
+const Tune& tune_defaults_unlocked();
+inline const Tune& tn() { return tl_tune ? *tl_tune : tune_defaults_unlocked(); }
+struct TuneScope {
+  const Tune* prev;
+  explicit TuneScope(const Tune* t) : prev(tl_tune) { tl_tune = t; }
+  ~TuneScope() { tl_tune = prev; }
+};
+
+// Opt a kernel into 160 KB of dynamic LDS once per (kernel, device): the attribute is per device, so a
+// process driving several GPUs sets it on each.
+template <typename Tag = void>
+inline hipError_t set_max_lds(const void* kern) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({kern, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (e == hipSuccess) done.insert({kern, dev});
+  return e;
+}
+
+// Copies of the caller's small vectors (biases, norm gains, activation parameters, filters) into a
+// handle's own arena, so a handle never points at caller memory: collected while the arena is laid out
+// (add), copied once it is allocated (commit, stream-ordered device-to-device).
+struct VecCopies {
+  struct Item { const float* src; size_t n; const float** dst; size_t off; };
+  std::vector<Item> items;
+  size_t bytes = 0;
+  void add(const float* src, size_t n, const float** dst) {
+    items.push_back(Item{src, n, dst, bytes});
+    bytes += (4 * n + 15) & ~(size_t)15;
+  }
+  int commit(char* base, hipStream_t st) {
+    for (const Item& it : items) {
+      FL_HIP(hipMemcpyAsync(base + it.off, it.src, 4 * it.n, hipMemcpyDeviceToDevice, st));
+      *it.dst = reinterpret_cast<const float*>(base + it.off);
+    }
+    return kOk;
+  }
+};
 
 // ---- device helpers ----
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }

@@ -14,41 +14,27 @@
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
 
+#include <mutex>
 #include <string>
 #include <vector>
 
 namespace fl {
 
-thread_local SplitCtx* g_split = nullptr;
-int g_small_stages = 3;
-int g_xcd_strips = 0;
-// Below kTinyRows rows (flamed_tune "bn32" 1, default) the denoiser GEMMs use 32 x 32 tiles: measured
-// at B = 1 (profiles/r01_dma_ab.txt) 34.6 vs 37.5 ms/solve at T = 131, but 41.9 vs 40.5 at T = 400.
-int g_bn32 = 1;
+// Below kTinyRows rows (tune bn32 1, default) the denoiser GEMMs use 32 x 32 tiles: measured at B = 1
+// (profiles/r01_dma_ab.txt) 34.6 vs 37.5 ms/solve at T = 131, but 41.9 vs 40.5 at T = 400.
 constexpr int kTinyRows = 320;
-// Tuning knobs (flamed_tune): split-K workgroup target and maximum split for small-M GEMMs.
-static int g_tune_split_target = 1;  // split-K off by default: measured slower at B=1 (profiles/r01_splitk_sweep.txt)
-static int g_tune_split_max = 4;
-// Ablation (flamed_tune "dup_class"): launch every kernel of this class twice per step, so the solve
-// time delta is the class's in-graph cost.  -1 = off.
-static int g_dup_class = -1;
-// Bumped by every flamed_tune call: a captured solve graph built under other settings is re-captured.
-static int g_tune_epoch = 0;
-// flamed_tune "dma": 1 routes small-M bf16 GEMMs whose A operand is bf16 through the LDS-DMA pipeline
-// (gemm_dma.hpp), 2 also those with fp32 (transforming) A loaders, 0 (default) = gemm_kernel only.
-// In-graph per-launch costs at B = 1 (profiles/r01_dma_ab.txt): no gain for 1, a loss for 2.
-static int g_use_dma = 1;
-// Ring depth of the small-M DMA tiles: at M = 400, K = 1024 with the step's weights streaming from
-// MALL (tools/probe_gemm.py, 24 weight buffers) 3 stages 6.48 us, 4: 6.70, 8: 7.14, 2: 8.36 per launch.
-int g_dma_ns = 3;
-static int g_noctr = 0;  // diagnostic: kernels ignore the device step counter (wrong modulation rows)
+// Knob notes (values live in Tune, common.hpp; set by flamed_tune / flamed_den_tune):
+//   use_dma 1: small-M bf16 GEMMs whose A operand is bf16 run on the LDS-DMA pipeline (gemm_dma.hpp),
+//     2 also those with fp32 (transforming) A loaders; in-graph per-launch costs at B = 1
+//     (profiles/r01_dma_ab.txt): no gain for 2.
+//   dma_ns: at M = 400, K = 1024 with the step's weights streaming from MALL (tools/probe_gemm.py, 24
+//     weight buffers) 3 stages 6.48 us, 4: 6.70, 8: 7.14, 2: 8.36 per launch.
 
-// Diagnostic stamps (FL_STAMPS builds): kernel class whose launches point fl_stamp_buf at g_stamp_dev.
-static int g_stamp_class = -1;
-static unsigned long long* g_stamp_dev = nullptr;
+// Diagnostic stamps (FL_STAMPS builds): kernels of class tn().stamp_class point fl_stamp_buf at g_stamp_dev.
 #ifdef FL_STAMPS
+static unsigned long long* g_stamp_dev = nullptr;
 static void stamp_select(int cls, hipStream_t st) {
-  unsigned long long* p = (cls == g_stamp_class) ? g_stamp_dev : nullptr;
+  unsigned long long* p = (cls == tn().stamp_class) ? g_stamp_dev : nullptr;
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(fl_stamp_buf), &p, sizeof(p), 0, hipMemcpyHostToDevice, st);
 }
 #else
@@ -497,11 +483,9 @@ struct EpiEuler {  // xt = xt + dt * (acc + b)   (prob_generator.py:445)
 // whole T axis (:89) are finished by gn_finalize; the normalisation itself is applied in the conv_2
 // GEMM's A-operand loader (LoadGN).
 constexpr int kDwCG = 64, kDwTC = 64;
-// T-chunk of the depthwise-conv workgroups at large M (B*T >= 8192): half the workgroups, half the halo
-// re-read (30 of 128 rows instead of 30 of 64); flamed_tune "dw_tc" 64 | 128.
-int g_dw_cg32_rows = 1536;  // flamed_tune "dw_cg32": below this many rows, narrow depthwise workgroups
-int g_dw_cg_small = 32;     // flamed_tune "dw_cg": their channel width (32 or 16)
-int g_dw_tc_big = 64;  // 128 measured slower at B = 64 (97 vs 82 us per launch, profiles/r01_b64_bigpath.txt)
+// T-chunk of the depthwise-conv workgroups at large M (B*T >= 8192): tn().dw_tc_big 64 | 128 (128: half
+// the workgroups, half the halo re-read; measured slower at B = 64, 97 vs 82 us per launch,
+// profiles/r01_b64_bigpath.txt).  Below tn().dw_cg32_rows rows: narrow tn().dw_cg_small-channel groups.
 
 template <bool AFF, int KS, int TC, int CG = kDwCG>
 __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restrict__ X, int H, const float* __restrict__ S,
@@ -700,15 +684,15 @@ static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, in
                                const float* lnb, const float* dww, const float* dwb, float* D, float* GP, float* GNS,
                                int B, int T, hipStream_t st, int part, int* gcnt) {
   FL_REQUIRE(H % kDwCG == 0 && H % 256 == 0, "dwconv: H=%d must be a multiple of 256", H);
-  const int TC = ((size_t)B * T >= 8192 && g_dw_tc_big == 128) ? 128 : kDwTC;
+  const int TC = ((size_t)B * T >= 8192 && tn().dw_tc_big == 128) ? 128 : kDwTC;
   const int TS = (T + TC - 1) / TC;
   // fewer than g_dw_cg32_rows frames: 32-channel workgroups (twice the workgroups, half the serial work each)
-  const bool cg32 = (size_t)B * T < (size_t)g_dw_cg32_rows;
+  const bool cg32 = (size_t)B * T < (size_t)tn().dw_cg32_rows;
   if (part != 2) {
     if (TC == 128)
       hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, 128>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
                          mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
-    else if (cg32 && g_dw_cg_small == 16)
+    else if (cg32 && tn().dw_cg_small == 16)
       hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 16>), dim3(H / 16, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
                          mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     else if (cg32)
@@ -896,12 +880,11 @@ __global__ void stack_taps_kernel(const float* __restrict__ src, DT* __restrict_
 // GEMM re-does that work for every column tile.  There each transforming A operand is written once as
 // bf16 rows (A16) by a streaming pass — LayerNorm + AdaLN modulate, GroupNorm apply or a plain cast,
 // the same arithmetic as the fused loaders — and the GEMM runs on 128 x 128 LDS-DMA tiles with
-// XCD-aware placement (gemm_dma.hpp).  flamed_tune "big" 0 keeps the fused register-staged GEMMs.
-int g_big = 1;
-int g_big_min_rows = 1536;  // flamed_tune "big_rows": smallest B*T on the large-M path (B=4/8/16 at T=400:
-                            // 93.6/113.4/188.5 -> 80.1/91.2/116.0 ms per solve; B=3 even)
-int g_big_ns = 2;  // LDS ring depth of the 128 x 128 tiles (2: two workgroups per CU, 635 TF plain at M = 25600; 3: one, 418 TF)
-thread_local bf16* g_a16 = nullptr;
+// XCD-aware placement (gemm_dma.hpp).  tn().big 0 keeps the fused register-staged GEMMs;
+// tn().big_min_rows: smallest B*T on the large-M path (B=4/8/16 at T=400: 93.6/113.4/188.5 ->
+// 80.1/91.2/116.0 ms per solve; B=3 even); tn().big_ns: LDS ring depth of the 128 x 128 tiles (2: two
+// workgroups per CU, 635 TF plain at M = 25600; 3: one, 418 TF).
+thread_local bf16* g_a16 = nullptr;  // the calling thread's step workspace (set per step, A16Scope)
 
 __global__ void cast_bf16x8_kernel(const float* __restrict__ src, int ld, bf16* __restrict__ dst, int M, int K) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -993,25 +976,23 @@ static int big_prep(const LoadLNMod<bf16, AFF>& al, int M, int K, bf16* a16, hip
 }
 template <class EP>
 static int launch_big(const LoadPlain<bf16>& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
-  if (g_big_ns == 2) return launch_gemm_dma_fixed<128, 128, 2, true>(al, W, ldw, ep, M, N, K, st);
+  if (tn().big_ns == 2) return launch_gemm_dma_fixed<128, 128, 2, true>(al, W, ldw, ep, M, N, K, st);
   return launch_gemm_dma_fixed<128, 128, 3, true>(al, W, ldw, ep, M, N, K, st);
 }
 
-// flamed_tune "lnfold": 1 (default, bf16 handles) mlp.0 / conv_out run as plain bf16 GEMMs with the
+// tn().lnfold: 1 (default, bf16 handles) mlp.0 / conv_out run as plain bf16 GEMMs with the
 // LayerNorm folded into the epilogue (EpiLNFold); 0: LayerNorm + modulation in the A loader.
-static int g_lnfold = 1;
-// On the large-M path the fold pays only from this many rows (flamed_tune "fold_rows"): measured
+// On the large-M path the fold pays only from tn().fold_big_rows rows (default 6144): measured
 // (ms/solve, fold vs not) M = 1600: 84.8 vs 81.7, 2400 (nfe 256): 187.1 vs 182.8, 3200: 94.2 vs 93.2,
 // 6400: 116.2 vs 118.0, 25600: 409.5 vs 411.1 — with few 128 x 128 tiles the x*alpha stores lengthen
 // conv_3 more than the dropped LayerNorm pass saves.
-static int g_fold_big_rows = 6144;
 
 // Denoiser GEMM dispatch: DMA pipeline for bf16 at small/mid M, gemm_kernel otherwise.
 template <typename DT, class AL, class EP>
 static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K,
                     hipStream_t st) {
   if constexpr (std::is_same<DT, bf16>::value) {
-    if (c == kCfgLarge && g_big) {
+    if (c == kCfgLarge && tn().big) {
       if constexpr (AL::kSrcBytes == 2) {
         return launch_big(al, W, ldw, ep, M, N, K, st);
       } else {
@@ -1024,7 +1005,7 @@ static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, 
   }
   if (c == kCfgTiny) {  // row partials are 32 columns wide (cfg_bn): every GEMM of the step uses BN = 32
     if constexpr (std::is_same<DT, bf16>::value) {
-      if (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)) return launch_gemm_dma<32, 32>(al, W, ldw, ep, M, N, K, st);
+      if (tn().use_dma >= 2 || (tn().use_dma == 1 && AL::kSrcBytes == 2)) return launch_gemm_dma<32, 32>(al, W, ldw, ep, M, N, K, st);
     }
     return launch_gemm_cfg<32, 32, 3, DT>(al, W, ldw, ep, M, N, K, st);
   }
@@ -1032,7 +1013,7 @@ static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, 
     // measured (B = 1, T = 400, stamps + in-graph dup timing): the DMA ring shortens the K loop of
     // the bf16-A GEMMs; for fp32-A loaders its LDS->LDS transform pass costs more LDS bandwidth than
     // the ring saves, and at mid M its ~150 KB of LDS drops residency to one block per CU
-    if (c == kCfgSmall && (g_use_dma >= 2 || (g_use_dma == 1 && AL::kSrcBytes == 2)))
+    if (c == kCfgSmall && (tn().use_dma >= 2 || (tn().use_dma == 1 && AL::kSrcBytes == 2)))
       return launch_gemm_dma<32, 64>(al, W, ldw, ep, M, N, K, st);
   }
   return wide_a ? launch_gemm_auto<DT>(c, kWideA, al, W, ldw, ep, M, N, K, st) : launch_gemm_auto<DT>(c, al, W, ldw, ep, M, N, K, st);
@@ -1059,6 +1040,12 @@ struct Den {
   std::vector<DenBlockW> blk;
   DenBlockW fin;  // m0/m2/lnmw.. unused
   void* wout; const float* bout;
+  int device = -1;          // device of the weight arena (from the loaded weights' pointers)
+  std::recursive_mutex mu;  // one call at a time per handle (single-stream use: counters, graph cache)
+  Tune tune;                // knob snapshot of this handle (process defaults unless tune_own)
+  int tune_seen = -1;       // process tune epoch of that snapshot
+  bool tune_own = false;    // set by flamed_den_tune: this handle keeps its own knobs
+  int tune_ver = 0;         // bumped on every change of `tune` (graph cache key)
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
@@ -1072,6 +1059,38 @@ struct Den {
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Active knobs of a handle call: the process defaults (re-snapshotted when flamed_tune moved the epoch)
+// unless flamed_den_tune gave the handle its own.
+static const Tune* den_tune_sync(Den* d) {
+  if (!d->tune_own) {
+    int ep = 0;
+    Tune t = tune_snapshot(&ep);
+    if (ep != d->tune_seen) {
+      d->tune = t;
+      d->tune_seen = ep;
+      ++d->tune_ver;
+    }
+  }
+  return &d->tune;
+}
+
+// Prologue of every compute entry point on a handle: serialise calls on the handle, make its device
+// current, and install its knob snapshot for the launches of this call.
+struct DenCall {
+  std::lock_guard<std::recursive_mutex> lk;
+  DeviceGuard dg;
+  TuneScope ts;
+  explicit DenCall(Den* d) : lk(d->mu), dg(d->device), ts(den_tune_sync(d)) {}
+};
+#define FL_DEN_CALL(d)                                                                              \
+  ::fl::DenCall call_(d);                                                                           \
+  do {                                                                                              \
+    if (call_.dg.err != hipSuccess) {                                                               \
+      ::fl::set_error("hipSetDevice(%d) -> %s", (d)->device, hipGetErrorString(call_.dg.err));     \
+      return ::fl::kHip;                                                                            \
+    }                                                                                               \
+  } while (0)
 
 struct DenWs {
   float* X;    // residual stream, M x H
@@ -1102,7 +1121,7 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t NTmax = d->H / 32;  // LN row partials per row: H / BN, BN >= 32
   size_t TS = (T + 63) / 64;
   const size_t sl = den_slab_floats(d, B, T);
-  const size_t a16 = (d->dt == FLAMED_BF16 && M >= (size_t)g_big_min_rows) ? 2 * M * d->H : 0;  // large-M path range
+  const size_t a16 = (d->dt == FLAMED_BF16 && M >= (size_t)tn().big_min_rows) ? 2 * M * d->H : 0;  // large-M path range
   const size_t xa = d->fold ? 2 * M * d->H : 0;
   size_t sizes[11] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
                       8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16, xa};
@@ -1147,12 +1166,16 @@ FLAMED_API int flamed_den_create(int C, int H, int n_blocks, int kernel, int spk
 FLAMED_API int flamed_den_destroy(flamed_den_t h) {
   Den* d = reinterpret_cast<Den*>(h);
   if (!d) return kOk;
-  if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
-  if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
-  if (d->ctr) (void)hipFree(d->ctr);
-  if (d->scnt) (void)hipFree(d->scnt);
-  if (d->gcnt) (void)hipFree(d->gcnt);
-  if (d->dev) (void)hipFree(d->dev);
+  {
+    std::lock_guard<std::recursive_mutex> lk(d->mu);
+    DeviceGuard dg(d->device);
+    if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
+    if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
+    if (d->ctr) (void)hipFree(d->ctr);
+    if (d->scnt) (void)hipFree(d->scnt);
+    if (d->gcnt) (void)hipFree(d->gcnt);
+    if (d->dev) (void)hipFree(d->dev);
+  }
   delete d;
   return kOk;
 }
@@ -1162,14 +1185,48 @@ FLAMED_API int flamed_den_num_weights(flamed_den_t h) {
   return d ? FLAMED_DEN_HEAD_W + FLAMED_DEN_BLOCK_W * d->NB + FLAMED_DEN_FINAL_W : -1;
 }
 
+FLAMED_API int flamed_den_device(flamed_den_t h) {
+  Den* d = reinterpret_cast<Den*>(h);
+  return d ? d->device : -1;
+}
+
+FLAMED_API int flamed_den_tune(flamed_den_t h, const char* key, int value) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d, "flamed_den_tune: null handle");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  den_tune_sync(d);
+  Tune t = d->tune;
+  const int rc = tune_apply(t, key, value);
+  if (rc) return rc;
+  d->tune = t;
+  d->tune_own = true;
+  ++d->tune_ver;
+  return kOk;
+}
+
 FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hipStream_t st) {
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && w, "flamed_den_load: null handle/weights");
   FL_REQUIRE(n == flamed_den_num_weights(h), "flamed_den_load: expected %d weight pointers, got %d", flamed_den_num_weights(h), n);
   for (int i = 0; i < n; ++i) FL_REQUIRE(w[i], "flamed_den_load: weight %d is null", i);
+  int wdev = -1;
+  FL_REQUIRE(device_of(w[0], &wdev) == kOk, "flamed_den_load: weights must be device memory");
+  for (int i = 1; i < n; ++i) FL_REQUIRE_ON(w[i], wdev, "flamed_den_load");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  if (d->device >= 0 && d->device != wdev) {  // re-load onto another device: drop the old device's state
+    DeviceGuard og(d->device);
+    if (d->gexec) { (void)hipGraphExecDestroy(d->gexec); d->gexec = nullptr; }
+    if (d->cap_stream) { (void)hipStreamDestroy(d->cap_stream); d->cap_stream = nullptr; }
+    if (d->ctr) { (void)hipFree(d->ctr); d->ctr = nullptr; }
+    if (d->scnt) { (void)hipFree(d->scnt); d->scnt = nullptr; }
+    if (d->gcnt) { (void)hipFree(d->gcnt); d->gcnt = nullptr; }
+    if (d->dev) { (void)hipFree(d->dev); d->dev = nullptr; }
+  }
+  d->device = wdev;
+  FL_ON_DEVICE(wdev);
   const int H = d->H, C = d->C, S = d->S, NB = d->NB, KS = d->KS;
   const size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
-  // arena layout
+  // arena layout: packed GEMM weights and copies of every vector (the caller may free its tensors)
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
   size_t o_t0w = take(4ull * H * 256), o_t0b = take(4ull * H), o_t2w = take(4ull * H * H), o_t2b = take(4ull * H);
@@ -1182,6 +1239,8 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   size_t o_out = take(es * (size_t)C * 3 * H);
   std::vector<size_t> o_dw(NB + 1);
   for (int i = 0; i <= NB; ++i) o_dw[i] = take(4ull * KS * H);
+  const size_t n_vec = 1 + 11ull * NB + 5;  // H-wide vectors: proj_in bias, 11 per block, 5 final
+  const size_t o_vec = take(4ull * (n_vec * H + C));
   if (d->dev) { FL_HIP(hipFree(d->dev)); d->dev = nullptr; }
   FL_HIP(hipMalloc(&d->dev, off));
   d->dev_bytes = off;
@@ -1201,13 +1260,21 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   };
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
+  size_t vcur = o_vec;
+  auto vec = [&](const float* src, size_t n, const float** dst) -> int {
+    TRY(cpy(vcur, src, n));
+    *dst = reinterpret_cast<const float*>(base + vcur);
+    vcur += 4 * n;
+    return kOk;
+  };
   TRY(cpy(o_t0w, w[0], (size_t)H * 256)); TRY(cpy(o_t0b, w[1], H));
   TRY(cpy(o_t2w, w[2], (size_t)H * H)); TRY(cpy(o_t2b, w[3], H));
   TRY(cpy(o_cw, w[4], (size_t)H * S)); TRY(cpy(o_cb, w[5], H));
   TRY(cast(o_win, w[6], (size_t)H * C));
   d->t0w = (float*)(base + o_t0w); d->t0b = (float*)(base + o_t0b); d->t2w = (float*)(base + o_t2w); d->t2b = (float*)(base + o_t2b);
   d->cw = (float*)(base + o_cw); d->cb = (float*)(base + o_cb); d->adaw = (float*)(base + o_adaw); d->adab = (float*)(base + o_adab);
-  d->win = base + o_win; d->bin = w[7];
+  d->win = base + o_win;
+  TRY(vec(w[7], H, &d->bin));
   d->blk.resize(NB);
   for (int i = 0; i < NB; ++i) {
     const float* const* bw = w + FLAMED_DEN_HEAD_W + FLAMED_DEN_BLOCK_W * i;
@@ -1222,8 +1289,10 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     B.w2 = base + ob; B.w3 = base + ob + es * H * H; B.m0 = base + ob + 2 * es * H * H; B.m2 = base + ob + 3 * es * H * H;
     hipLaunchKernelGGL(taps_t_kernel, dim3((H * KS + 255) / 256), dim3(256), 0, st, bw[4], reinterpret_cast<float*>(base + o_dw[i]), H, KS);
     FL_LAUNCH_CHECK();
-    B.lnw = bw[2]; B.lnb = bw[3]; B.dww = reinterpret_cast<float*>(base + o_dw[i]); B.dwb = bw[5]; B.gnw = bw[6]; B.gnb = bw[7];
-    B.b2 = bw[9]; B.b3 = bw[11]; B.lnmw = bw[12]; B.lnmb = bw[13]; B.mb0 = bw[15]; B.mb2 = bw[17];
+    B.dww = reinterpret_cast<float*>(base + o_dw[i]);
+    TRY(vec(bw[2], H, &B.lnw)); TRY(vec(bw[3], H, &B.lnb)); TRY(vec(bw[5], H, &B.dwb)); TRY(vec(bw[6], H, &B.gnw));
+    TRY(vec(bw[7], H, &B.gnb)); TRY(vec(bw[9], H, &B.b2)); TRY(vec(bw[11], H, &B.b3)); TRY(vec(bw[12], H, &B.lnmw));
+    TRY(vec(bw[13], H, &B.lnmb)); TRY(vec(bw[15], H, &B.mb0)); TRY(vec(bw[17], H, &B.mb2));
   }
   {
     const float* const* fw = w + FLAMED_DEN_HEAD_W + FLAMED_DEN_BLOCK_W * NB;
@@ -1232,9 +1301,10 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     DenBlockW& F = d->fin;
     hipLaunchKernelGGL(taps_t_kernel, dim3((H * KS + 255) / 256), dim3(256), 0, st, fw[2], reinterpret_cast<float*>(base + o_dw[NB]), H, KS);
     FL_LAUNCH_CHECK();
-    F.dww = reinterpret_cast<float*>(base + o_dw[NB]); F.dwb = fw[3]; F.gnw = fw[4]; F.gnb = fw[5];
-    TRY(cast(o_fin, fw[6], (size_t)H * H)); F.b2 = fw[7];
-    TRY(cast(o_fin + es * H * H, fw[8], (size_t)H * H)); F.b3 = fw[9];
+    F.dww = reinterpret_cast<float*>(base + o_dw[NB]);
+    TRY(vec(fw[3], H, &F.dwb)); TRY(vec(fw[4], H, &F.gnw)); TRY(vec(fw[5], H, &F.gnb));
+    TRY(cast(o_fin, fw[6], (size_t)H * H)); TRY(vec(fw[7], H, &F.b2));
+    TRY(cast(o_fin + es * H * H, fw[8], (size_t)H * H)); TRY(vec(fw[9], H, &F.b3));
     F.w2 = base + o_fin; F.w3 = base + o_fin + es * H * H;
     size_t n = (size_t)C * H * 3;
     if (d->dt == FLAMED_BF16)
@@ -1242,7 +1312,8 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     else
       hipLaunchKernelGGL(stack_taps_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, st, fw[10], reinterpret_cast<float*>(base + o_out), C, H, 3);
     FL_LAUNCH_CHECK();
-    d->wout = base + o_out; d->bout = fw[11];
+    d->wout = base + o_out;
+    TRY(vec(fw[11], C, &d->bout));
   }
 #undef TRY
   if (!d->scnt) FL_HIP(hipMalloc(&d->scnt, sizeof(int) * Den::kSplitCounters));
@@ -1270,6 +1341,8 @@ FLAMED_API int flamed_den_adaln(flamed_den_t h, const float* t_vals, int n_t, co
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && d->dev, "flamed_den_adaln: handle not loaded");
   FL_REQUIRE(t_vals && spk && tidx && sidx && mods && ws && n_t > 0 && n_spk > 0 && R > 0, "flamed_den_adaln: bad args");
+  FL_DEN_CALL(d);
+  FL_REQUIRE_ON(mods, d->device, "flamed_den_adaln");
   if (ws_bytes < flamed_den_adaln_workspace_size(h, n_t, n_spk)) {
     set_error("flamed_den_adaln: workspace too small");
     return kNoWorkspace;
@@ -1307,29 +1380,14 @@ FLAMED_API int flamed_den_adaln(flamed_den_t h, const float* t_vals, int n_t, co
 FLAMED_API size_t flamed_den_workspace_size(flamed_den_t h, int B, int T) {
   Den* d = reinterpret_cast<Den*>(h);
   if (!d) return 0;
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  TuneScope ts(den_tune_sync(d));  // the layout depends on the handle's large-M threshold
   return den_ws_bytes(d, B, T);
 }
 
 }  // extern "C"
 
 namespace fl {
-
-// In-context kernel timer (diagnostic): when set, an event is recorded after every launch of a
-// full step, tagged with the kernel class, so per-kernel device time is measured inside the real
-// sequence (flamed_den_time_kernels).
-struct KTimer {
-  static constexpr int kMax = 128;
-  hipEvent_t ev[kMax];
-  int cls[kMax];
-  int n = 0;
-};
-static thread_local KTimer* g_kt = nullptr;
-static inline void kt_mark(int c, hipStream_t st) {
-  if (g_kt && g_kt->n < KTimer::kMax) {
-    (void)hipEventRecord(g_kt->ev[g_kt->n], st);
-    g_kt->cls[g_kt->n++] = c;
-  }
-}
 
 // One velocity evaluation (+ Euler update when vout == nullptr).
 // `ctr` (optional): device step counter; when set the modulation rows are read at
@@ -1338,16 +1396,17 @@ template <typename DT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
                          const DenWs& w, int* ctr, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
-  const StepOff so{g_noctr ? nullptr : ctr, (long long)B * MS};
+  const Tune& tu = tn();
+  const StepOff so{tu.noctr ? nullptr : ctr, (long long)B * MS};
   SplitCtx sctx;
   sctx.slab = w.SL; sctx.slab_floats = w.SLn; sctx.cnt = d->scnt; sctx.cnt_n = Den::kSplitCounters;
-  sctx.target = g_tune_split_target; sctx.max_split = g_tune_split_max;
+  sctx.target = tu.split_target; sctx.max_split = tu.split_max;
   SplitScope split_scope(w.SLn ? &sctx : nullptr);
   // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
   int* gcnt = (d->gcnt && (size_t)B * (H / 16) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;  // >= 16-channel groups
-  const GemmCfg cfg = (g_bn32 && M < kTinyRows) ? kCfgTiny
-                      : (std::is_same<DT, bf16>::value && g_big && M >= g_big_min_rows) ? kCfgLarge : pick_cfg(M);
-  const bool big = std::is_same<DT, bf16>::value && cfg == kCfgLarge && g_big;
+  const GemmCfg cfg = (tu.bn32 && M < kTinyRows) ? kCfgTiny
+                      : (std::is_same<DT, bf16>::value && tu.big && M >= tu.big_min_rows) ? kCfgLarge : pick_cfg(M);
+  const bool big = std::is_same<DT, bf16>::value && cfg == kCfgLarge && tu.big;
   FL_REQUIRE(!big || w.A16, "den_step: large-M workspace without the A16 buffer");
   const int BN = big ? 128 : cfg_bn(cfg);  // LN row-partial width = the N tile of the stats epilogues
   struct A16Scope {
@@ -1357,10 +1416,10 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   } a16_scope(w.A16);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
-  const bool fold = std::is_same<DT, bf16>::value && d->fold && g_lnfold && w.XA && (!big || M >= g_fold_big_rows);
+  const bool fold = std::is_same<DT, bf16>::value && d->fold && tu.lnfold && w.XA && (!big || M >= tu.fold_big_rows);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
-#define K_(cls, x) do { if (g_stamp_class >= 0) stamp_select(cls, st); TRY(x); if (g_dup_class == (cls)) TRY(x); kt_mark(cls, st); } while (0)
+#define K_(cls, x) do { if (tu.stamp_class >= 0) stamp_select(cls, st); TRY(x); if (tu.dup_class == (cls)) TRY(x); } while (0)
   K_(0, (den_gemm<DT>(cfg, false, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
@@ -1415,11 +1474,10 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     size_t n = (size_t)M * C;
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, ctr);
     FL_LAUNCH_CHECK();
-    if (g_dup_class == 8) {  // duplicate without a second counter increment
+    if (tu.dup_class == 8) {  // duplicate without a second counter increment
       hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, nullptr);
       FL_LAUNCH_CHECK();
     }
-    kt_mark(8, st);
   }
 #undef K_
 #undef TRY
@@ -1434,12 +1492,12 @@ static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, in
   return den_step_impl<float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
 }
 
-// Steps per captured graph: the largest divisor of nfe that is <= g_graph_steps (flamed_tune
-// "graph_steps", default 16; the graph is replayed nfe/G times per solve, so a new (B, T) costs one
-// G-step capture instead of an nfe-step one).
-static int g_graph_steps = 16;
+// Steps per captured graph: the largest divisor of nfe that is <= tn().graph_steps (default 16; the
+// graph is replayed nfe/G times per solve, so a new (B, T) costs one G-step capture instead of an
+// nfe-step one).
 static int graph_chunk(int nfe) {
-  for (int g = g_graph_steps < nfe ? g_graph_steps : nfe; g > 1; --g)
+  const int gs = tn().graph_steps;
+  for (int g = gs < nfe ? gs : nfe; g > 1; --g)
     if (nfe % g == 0) return g;
   return 1;
 }
@@ -1453,8 +1511,10 @@ FLAMED_API int flamed_den_velocity(flamed_den_t h, const float* x, const float* 
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && d->dev, "flamed_den_velocity: handle not loaded");
   FL_REQUIRE(x && mods && v_out && ws && B > 0 && T > 0 && mod_div > 0, "flamed_den_velocity: bad args");
-  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
-    set_error("flamed_den_velocity: workspace too small (%zu < %zu)", ws_bytes, flamed_den_workspace_size(h, B, T));
+  FL_DEN_CALL(d);
+  FL_REQUIRE_ON(x, d->device, "flamed_den_velocity");
+  if (ws_bytes < den_ws_bytes(d, B, T)) {
+    set_error("flamed_den_velocity: workspace too small (%zu < %zu)", ws_bytes, den_ws_bytes(d, B, T));
     return kNoWorkspace;
   }
   return den_step(d, const_cast<float*>(x), mods, mod_div, B, T, 0.f, v_out, ws, st);
@@ -1465,7 +1525,9 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && d->dev, "flamed_den_step: handle not loaded");
   FL_REQUIRE(xt && mods && ws && B > 0 && T > 0 && mod_div > 0, "flamed_den_step: bad args");
-  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
+  FL_DEN_CALL(d);
+  FL_REQUIRE_ON(xt, d->device, "flamed_den_step");
+  if (ws_bytes < den_ws_bytes(d, B, T)) {
     set_error("flamed_den_step: workspace too small");
     return kNoWorkspace;
   }
@@ -1477,7 +1539,9 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && d->dev, "flamed_den_solve: handle not loaded");
   FL_REQUIRE(xt && mods && ws && B > 0 && T > 0 && nfe > 0, "flamed_den_solve: bad args");
-  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
+  FL_DEN_CALL(d);
+  FL_REQUIRE_ON(xt, d->device, "flamed_den_solve");
+  if (ws_bytes < den_ws_bytes(d, B, T)) {
     set_error("flamed_den_solve: workspace too small");
     return kNoWorkspace;
   }
@@ -1495,7 +1559,7 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // the graph bakes in dt = 1/nfe, so nfe is part of the key
   const bool hit = d->gexec && d->g_B == B && d->g_T == T && d->g_nfe == nfe && d->g_xt == xt && d->g_mods == mods && d->g_ws == ws &&
-                   d->g_epoch == g_tune_epoch;
+                   d->g_epoch == d->tune_ver;
   if (!hit) {
     if (d->gexec) { FL_HIP(hipGraphExecDestroy(d->gexec)); d->gexec = nullptr; }
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
@@ -1509,7 +1573,7 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     hipError_t ie = hipGraphInstantiate(&d->gexec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     FL_HIP(ie);
-    d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_epoch = g_tune_epoch; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
+    d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_epoch = d->tune_ver; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
   }
   FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
   for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
@@ -1520,43 +1584,12 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
 
 extern "C" {
 
-// Diagnostic: device buffer (blocks x 8 u64) that FL_STAMPS kernels of the selected class write into.
+#ifdef FL_STAMPS  // diagnostic library only (include/flamed_diag.h)
 FLAMED_API int flamed_stamp_buffer(void* buf) {
   g_stamp_dev = reinterpret_cast<unsigned long long*>(buf);
-#ifdef FL_STAMPS
   return kOk;
-#else
-  set_error("flamed_stamp_buffer: library built without FL_STAMPS");
-  return kBadArg;
+}
 #endif
-}
-
-FLAMED_API int flamed_tune(const char* key, int value) {
-  FL_REQUIRE(key, "flamed_tune: null key");
-  ++g_tune_epoch;
-  const std::string k(key);
-  if (k == "splitk_target") { FL_REQUIRE(value >= 1, "flamed_tune: splitk_target >= 1"); g_tune_split_target = value; return kOk; }
-  if (k == "stamp_class") { g_stamp_class = value; return kOk; }
-  if (k == "dw_cg") { FL_REQUIRE(value == 16 || value == 32, "flamed_tune: dw_cg in {16, 32}"); g_dw_cg_small = value; return kOk; }
-  if (k == "dw_cg32") { FL_REQUIRE(value >= 0, "flamed_tune: dw_cg32 >= 0"); g_dw_cg32_rows = value; return kOk; }
-  if (k == "lnfold") { g_lnfold = value != 0; return kOk; }
-  if (k == "graph_steps") { FL_REQUIRE(value >= 1 && value <= 1024, "flamed_tune: graph_steps in [1, 1024]"); g_graph_steps = value; return kOk; }
-  if (k == "fold_rows") { FL_REQUIRE(value >= 0, "flamed_tune: fold_rows >= 0"); g_fold_big_rows = value; return kOk; }
-  if (k == "dma_ns") { FL_REQUIRE(value == 3 || value == 4 || value == 6 || value == 8, "flamed_tune: dma_ns in {3, 4, 6, 8}"); g_dma_ns = value; return kOk; }
-  if (k == "dw_tc") { FL_REQUIRE(value == 64 || value == 128, "flamed_tune: dw_tc in {64, 128}"); g_dw_tc_big = value; return kOk; }
-  if (k == "big_rows") { FL_REQUIRE(value >= 1024, "flamed_tune: big_rows >= 1024"); g_big_min_rows = value; return kOk; }
-  if (k == "big") { g_big = value != 0; return kOk; }
-  if (k == "big_ns") { FL_REQUIRE(value == 2 || value == 3, "flamed_tune: big_ns in {2, 3}"); g_big_ns = value; return kOk; }
-  if (k == "xcd_strips") { FL_REQUIRE(value >= 0 && value <= 64, "flamed_tune: xcd_strips in [0, 64]"); g_xcd_strips = value; return kOk; }
-  if (k == "bn32") { g_bn32 = value != 0; return kOk; }
-  if (k == "noctr") { g_noctr = value; return kOk; }
-  if (k == "dma") { FL_REQUIRE(value >= 0 && value <= 2, "flamed_tune: dma in {0, 1, 2}"); g_use_dma = value; return kOk; }
-  if (k == "small_stages") { FL_REQUIRE(value == 3 || value == 5 || value == 7, "flamed_tune: small_stages must be 3, 5 or 7"); g_small_stages = value; return kOk; }
-  if (k == "dup_class") { FL_REQUIRE(value >= -1 && value < FLAMED_DEN_KERNEL_CLASSES, "flamed_tune: dup_class in [-1, %d)", FLAMED_DEN_KERNEL_CLASSES); g_dup_class = value; return kOk; }
-  if (k == "splitk_max") { FL_REQUIRE(value == 1 || value == 2 || value == kMaxSplit, "flamed_tune: splitk_max must be 1, 2 or 4"); g_tune_split_max = value; return kOk; }
-  set_error("flamed_tune: unknown key '%s'", key);
-  return kBadArg;
-}
 
 // In-graph per-launch cost of every kernel class: a graph of `steps` Euler steps (dt = 0) is timed
 // as captured and again with one class launched twice per occurrence (flamed_tune dup_class); the
@@ -1567,7 +1600,8 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
                                              size_t ws_bytes, int reps, float* ms_out, hipStream_t st) {
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && d->dev && xt && mods && ws && ms_out && reps > 0, "flamed_den_time_kernels_graph: bad args");
-  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
+  FL_DEN_CALL(d);
+  if (ws_bytes < den_ws_bytes(d, B, T)) {
     set_error("flamed_den_time_kernels_graph: workspace too small");
     return kNoWorkspace;
   }
@@ -1576,15 +1610,15 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
   hipEvent_t e0, e1;
   FL_HIP(hipEventCreate(&e0));
   FL_HIP(hipEventCreate(&e1));
-  const int saved_dup = g_dup_class;
+  const int saved_dup = d->tune.dup_class;  // the handle's active snapshot (this call's TuneScope)
   auto timed = [&](int dup, float* ms) -> int {
-    g_dup_class = dup;
+    d->tune.dup_class = dup;
     FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
     int rc = kOk;
     for (int i = 0; i < kSteps && rc == kOk; ++i) rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
-    g_dup_class = saved_dup;
+    d->tune.dup_class = saved_dup;
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
     FL_HIP(e);
     hipGraphExec_t ex;
@@ -1614,41 +1648,6 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
   ms_out[FLAMED_DEN_KERNEL_CLASSES] = base;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  return rc;
-}
-
-FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
-                                       size_t ws_bytes, int iters, float* ms_out, hipStream_t st) {
-  Den* d = reinterpret_cast<Den*>(h);
-  FL_REQUIRE(d && d->dev && xt && mods && ws && ms_out && iters > 0, "flamed_den_time_kernels: bad args");
-  if (ws_bytes < flamed_den_workspace_size(h, B, T)) {
-    set_error("flamed_den_time_kernels: workspace too small");
-    return kNoWorkspace;
-  }
-  KTimer kt;
-  for (int i = 0; i < KTimer::kMax; ++i) FL_HIP(hipEventCreate(&kt.ev[i]));
-  double sum[FLAMED_DEN_KERNEL_CLASSES] = {0};
-  int cnt[FLAMED_DEN_KERNEL_CLASSES] = {0};
-  int rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st);  // warm
-  for (int it = 0; it < iters && rc == kOk; ++it) {
-    kt.n = 0;
-    (void)hipEventRecord(kt.ev[0], st);
-    kt.cls[0] = -1;
-    kt.n = 1;
-    g_kt = &kt;
-    rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, st);
-    g_kt = nullptr;
-    if (rc) break;
-    FL_HIP(hipEventSynchronize(kt.ev[kt.n - 1]));
-    for (int i = 1; i < kt.n; ++i) {
-      float ms = 0.f;
-      FL_HIP(hipEventElapsedTime(&ms, kt.ev[i - 1], kt.ev[i]));
-      sum[kt.cls[i]] += ms;
-      cnt[kt.cls[i]] += 1;
-    }
-  }
-  for (int c = 0; c < FLAMED_DEN_KERNEL_CLASSES; ++c) ms_out[c] = cnt[c] ? (float)(sum[c] / cnt[c]) : 0.f;
-  for (int i = 0; i < KTimer::kMax; ++i) (void)hipEventDestroy(kt.ev[i]);
   return rc;
 }
 

@@ -14,6 +14,7 @@
 #include "flamed_hip.h"
 #include "gemm.hpp"
 
+#include <mutex>
 #include <vector>
 
 namespace fl {
@@ -126,21 +127,32 @@ __global__ __launch_bounds__(256) void dur_head_kernel(const float* __restrict__
   }
 }
 
-struct DurNet {
-  int D, F, KT;
-  char* dev = nullptr;
-  float *w0, *we, *c1w, *c2w;  // packed
-  const float *pb, *t1w, *t1b, *t2w, *t2b, *c1b, *g1, *b1, *c2b, *g2, *b2, *lw, *lb;
-};
-
 struct PvaGraph {
   hipGraphExec_t exec = nullptr;
   hipStream_t cap = nullptr, cap2 = nullptr;  // the two nets' chains are captured as parallel branches
   hipEvent_t fork = nullptr, join = nullptr;
   std::vector<const void*> key;
   int* ctr = nullptr;  // device Euler step counters: [0] duration chain, [1] silence chain
+  void release() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (cap) (void)hipStreamDestroy(cap);
+    if (cap2) (void)hipStreamDestroy(cap2);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    if (ctr) (void)hipFree(ctr);
+    *this = PvaGraph();
+  }
 };
-static PvaGraph g_pva;  // one cached graph per process (durgen is tiny; recaptured on any change)
+
+struct DurNet {
+  int D, F, KT;
+  int device = -1;  // device of the packed weights
+  std::mutex mu;    // one call at a time per handle
+  char* dev = nullptr;
+  float *w0, *we, *c1w, *c2w;  // packed
+  const float *pb, *t1w, *t1b, *t2w, *t2b, *c1b, *g1, *b1, *c2b, *g2, *b2, *lw, *lb;  // copies in the arena
+  PvaGraph graph;   // the (duration, silence) pair's cached flow graph, kept on the duration net's handle
+};
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -287,7 +299,12 @@ FLAMED_API int flamed_dur_create(int input_size, int filter_size, int kernel, fl
 FLAMED_API int flamed_dur_destroy(flamed_dur_t h) {
   DurNet* n = reinterpret_cast<DurNet*>(h);
   if (!n) return kOk;
-  if (n->dev) (void)hipFree(n->dev);
+  {
+    std::lock_guard<std::mutex> lk(n->mu);
+    DeviceGuard dg(n->device);
+    n->graph.release();
+    if (n->dev) (void)hipFree(n->dev);
+  }
   delete n;
   return kOk;
 }
@@ -296,10 +313,26 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* w, int nw, hi
   DurNet* n = reinterpret_cast<DurNet*>(h);
   FL_REQUIRE(n && w && nw == FLAMED_DUR_W, "flamed_dur_load: expected %d weights", FLAMED_DUR_W);
   for (int i = 0; i < nw; ++i) FL_REQUIRE(w[i], "flamed_dur_load: weight %d is null", i);
+  int wdev = -1;
+  FL_REQUIRE(device_of(w[0], &wdev) == kOk, "flamed_dur_load: weights must be device memory");
+  for (int i = 1; i < nw; ++i) FL_REQUIRE_ON(w[i], wdev, "flamed_dur_load");
+  std::lock_guard<std::mutex> lk(n->mu);
+  if (n->device >= 0 && n->device != wdev) {
+    DeviceGuard og(n->device);
+    n->graph.release();
+    if (n->dev) { (void)hipFree(n->dev); n->dev = nullptr; }
+  }
+  n->device = wdev;
+  FL_ON_DEVICE(wdev);
   const int D = n->D, F = n->F;
   size_t o_w0 = 0, o_we = a256(4ull * D), o_c1 = o_we + a256(4ull * D * D), o_c2 = o_c1 + a256(4ull * F * 3 * D);
-  size_t total = o_c2 + a256(4ull * F * 3 * F);
+  size_t o_vec = o_c2 + a256(4ull * F * 3 * F);
+  // vectors copied (the caller may free its tensors): pb D, t1w 4D x D, t1b 4D, t2w D x 4D, t2b D,
+  // c1b g1 b1 c2b g2 b2 lw (F each), lb 1
+  const size_t vec_floats = (size_t)D + 4ull * D * D + 4ull * D + 4ull * D * D + D + 7ull * F + 1;
+  size_t total = o_vec + a256(4 * vec_floats + 64 * 4);
   if (n->dev) { FL_HIP(hipFree(n->dev)); n->dev = nullptr; }
+  n->graph.release();
   FL_HIP(hipMalloc(&n->dev, total));
   n->w0 = (float*)(n->dev + o_w0); n->we = (float*)(n->dev + o_we);
   n->c1w = (float*)(n->dev + o_c1); n->c2w = (float*)(n->dev + o_c2);
@@ -310,8 +343,20 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* w, int nw, hi
   FL_LAUNCH_CHECK();
   hipLaunchKernelGGL(taps_major_kernel, dim3((t2 + 255) / 256), dim3(256), 0, st, w[10], n->c2w, F, F, 3);
   FL_LAUNCH_CHECK();
-  n->pb = w[1]; n->t1w = w[2]; n->t1b = w[3]; n->t2w = w[4]; n->t2b = w[5]; n->c1b = w[7]; n->g1 = w[8]; n->b1 = w[9];
-  n->c2b = w[11]; n->g2 = w[12]; n->b2 = w[13]; n->lw = w[14]; n->lb = w[15];
+  size_t vcur = o_vec;
+  auto vec = [&](const float* src, size_t cnt, const float** dst) -> int {
+    FL_HIP(hipMemcpyAsync(n->dev + vcur, src, 4 * cnt, hipMemcpyDeviceToDevice, st));
+    *dst = reinterpret_cast<const float*>(n->dev + vcur);
+    vcur += (4 * cnt + 15) & ~(size_t)15;  // 16-B aligned slots
+    return kOk;
+  };
+  int rc;
+#define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
+  TRY(vec(w[1], D, &n->pb)); TRY(vec(w[2], 4ull * D * D, &n->t1w)); TRY(vec(w[3], 4ull * D, &n->t1b));
+  TRY(vec(w[4], 4ull * D * D, &n->t2w)); TRY(vec(w[5], D, &n->t2b)); TRY(vec(w[7], F, &n->c1b)); TRY(vec(w[8], F, &n->g1));
+  TRY(vec(w[9], F, &n->b1)); TRY(vec(w[11], F, &n->c2b)); TRY(vec(w[12], F, &n->g2)); TRY(vec(w[13], F, &n->b2));
+  TRY(vec(w[14], F, &n->lw)); TRY(vec(w[15], 1, &n->lb));
+#undef TRY
   return kOk;
 }
 
@@ -328,6 +373,14 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   FL_REQUIRE(nd && ns && nd->dev && ns->dev, "flamed_pva_flow: handles not loaded");
   FL_REQUIRE(nd->D == ns->D && nd->F == ns->F, "flamed_pva_flow: dur/sil nets differ in dims");
   FL_REQUIRE(enc && mask && dur_t && sil_t && ts && ws && nfe > 0 && B > 0 && L > 0, "flamed_pva_flow: bad args");
+  FL_REQUIRE(nd->device == ns->device, "flamed_pva_flow: dur/sil handles live on different devices");
+  std::unique_lock<std::mutex> lk_d(nd->mu, std::defer_lock), lk_s(ns->mu, std::defer_lock);
+  if (nd == ns) lk_d.lock();
+  else std::lock(lk_d, lk_s);
+  FL_ON_DEVICE(nd->device);
+  FL_REQUIRE_ON(enc, nd->device, "flamed_pva_flow");
+  const Tune tsnap = tune_snapshot(nullptr);  // process defaults, read once for this call's GEMM launches
+  TuneScope ts_(&tsnap);
   if (ws_bytes < pva_ws_layout(nd, B, L, nfe, nullptr, nullptr)) {
     set_error("flamed_pva_flow: workspace too small");
     return kNoWorkspace;
@@ -355,45 +408,49 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   int G = 1;
   for (int g = 16; g > 1; --g)
     if (nfe % g == 0) { G = g; break; }
-  if (!g_pva.ctr) FL_HIP(hipMalloc(&g_pva.ctr, 256));
+  PvaGraph& gp = nd->graph;
+  if (!gp.ctr) FL_HIP(hipMalloc(&gp.ctr, 256));
   std::vector<const void*> key = {nd, ns, enc, mask, dur_t, sil_t, ts, ws, (const void*)(intptr_t)nfe,
                                   (const void*)(intptr_t)B, (const void*)(intptr_t)L, nd->dev, ns->dev};
-  if (!g_pva.exec || g_pva.key != key) {
-    if (g_pva.exec) { FL_HIP(hipGraphExecDestroy(g_pva.exec)); g_pva.exec = nullptr; }
-    if (!g_pva.cap) FL_HIP(hipStreamCreateWithFlags(&g_pva.cap, hipStreamNonBlocking));
-    if (!g_pva.cap2) FL_HIP(hipStreamCreateWithFlags(&g_pva.cap2, hipStreamNonBlocking));
-    if (!g_pva.fork) FL_HIP(hipEventCreateWithFlags(&g_pva.fork, hipEventDisableTiming));
-    if (!g_pva.join) FL_HIP(hipEventCreateWithFlags(&g_pva.join, hipEventDisableTiming));
-    FL_HIP(hipStreamBeginCapture(g_pva.cap, hipStreamCaptureModeRelaxed));
+  if (!gp.exec || gp.key != key) {
+    if (gp.exec) { FL_HIP(hipGraphExecDestroy(gp.exec)); gp.exec = nullptr; }
+    if (!gp.cap) FL_HIP(hipStreamCreateWithFlags(&gp.cap, hipStreamNonBlocking));
+    if (!gp.cap2) FL_HIP(hipStreamCreateWithFlags(&gp.cap2, hipStreamNonBlocking));
+    if (!gp.fork) FL_HIP(hipEventCreateWithFlags(&gp.fork, hipEventDisableTiming));
+    if (!gp.join) FL_HIP(hipEventCreateWithFlags(&gp.join, hipEventDisableTiming));
+    FL_HIP(hipStreamBeginCapture(gp.cap, hipStreamCaptureModeRelaxed));
     int r = kOk;
-    hipError_t fe = hipEventRecord(g_pva.fork, g_pva.cap);
-    if (fe == hipSuccess) fe = hipStreamWaitEvent(g_pva.cap2, g_pva.fork, 0);
+    hipError_t fe = hipEventRecord(gp.fork, gp.cap);
+    if (fe == hipSuccess) fe = hipStreamWaitEvent(gp.cap2, gp.fork, 0);
     if (fe != hipSuccess) r = kHip;
-    for (int i = 0; i < G && r == kOk; ++i) r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, bd, g_pva.cap, g_pva.ctr, g_pva.ctr);
+    for (int i = 0; i < G && r == kOk; ++i) r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, bd, gp.cap, gp.ctr, gp.ctr);
     for (int i = 0; i < G && r == kOk; ++i)
-      r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, bs, g_pva.cap2, g_pva.ctr + 1, g_pva.ctr + 1);
+      r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, bs, gp.cap2, gp.ctr + 1, gp.ctr + 1);
     if (r == kOk) {
-      fe = hipEventRecord(g_pva.join, g_pva.cap2);
-      if (fe == hipSuccess) fe = hipStreamWaitEvent(g_pva.cap, g_pva.join, 0);
+      fe = hipEventRecord(gp.join, gp.cap2);
+      if (fe == hipSuccess) fe = hipStreamWaitEvent(gp.cap, gp.join, 0);
       if (fe != hipSuccess) r = kHip;
     }
     hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(g_pva.cap, &g);
+    hipError_t e = hipStreamEndCapture(gp.cap, &g);
     if (r) { if (g) (void)hipGraphDestroy(g); return r; }
     FL_HIP(e);
-    hipError_t ie = hipGraphInstantiate(&g_pva.exec, g, nullptr, nullptr, 0);
+    hipError_t ie = hipGraphInstantiate(&gp.exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     FL_HIP(ie);
-    g_pva.key = key;
+    gp.key = key;
   }
-  FL_HIP(hipMemsetAsync(g_pva.ctr, 0, 2 * sizeof(int), st));
-  for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(g_pva.exec, st));
+  FL_HIP(hipMemsetAsync(gp.ctr, 0, 2 * sizeof(int), st));
+  for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(gp.exec, st));
   return kOk;
 }
 
 FLAMED_API int flamed_lr_lengths(const float* phone, const float* sil, const int64_t* src_lens, int B, int L,
                                  int log_domain, int64_t* cum, int64_t* tgt_len, hipStream_t st) {
   FL_REQUIRE(phone && sil && src_lens && cum && tgt_len && B > 0 && L > 0, "flamed_lr_lengths: bad args");
+  int dv = -1;
+  (void)device_of(cum, &dv);
+  FL_ON_DEVICE(dv);
   hipLaunchKernelGGL(lr_lengths_kernel, dim3(B), dim3(256), 0, st, phone, sil, src_lens, L, log_domain, cum, tgt_len);
   FL_LAUNCH_CHECK();
   return kOk;
@@ -402,6 +459,9 @@ FLAMED_API int flamed_lr_lengths(const float* phone, const float* sil, const int
 FLAMED_API int flamed_lr_expand(const float* x, const int64_t* cum, int B, int L, int H, int T_out, float* out,
                                 hipStream_t st) {
   FL_REQUIRE(x && cum && out && B > 0 && L > 0 && H > 0 && T_out >= 0, "flamed_lr_expand: bad args");
+  int dv = -1;
+  (void)device_of(out, &dv);
+  FL_ON_DEVICE(dv);
   if (T_out == 0) return kOk;
   hipLaunchKernelGGL(lr_expand_kernel, dim3((T_out + 3) / 4, B), dim3(256), 0, st, x, cum, L, H, T_out, out);
   FL_LAUNCH_CHECK();

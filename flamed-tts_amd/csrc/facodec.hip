@@ -251,9 +251,18 @@ struct Fac {
   float* wout; const float* bout;
   int cfin;
   char* dev = nullptr;
+  int device = -1;  // device of the arena (from the loaded weights)
+  std::mutex mu;    // one call at a time per handle
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap = nullptr;
   std::vector<const void*> gkey;
+  void release() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (cap) (void)hipStreamDestroy(cap);
+    if (dev) (void)hipFree(dev);
+    gexec = nullptr; cap = nullptr; dev = nullptr;
+    gkey.clear();
+  }
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -360,9 +369,11 @@ FLAMED_API int flamed_fac_create(int in_channels, int upsample_initial_channel, 
 FLAMED_API int flamed_fac_destroy(flamed_fac_t h) {
   Fac* f = reinterpret_cast<Fac*>(h);
   if (!f) return kOk;
-  if (f->gexec) (void)hipGraphExecDestroy(f->gexec);
-  if (f->cap) (void)hipStreamDestroy(f->cap);
-  if (f->dev) (void)hipFree(f->dev);
+  {
+    std::lock_guard<std::mutex> lk(f->mu);
+    DeviceGuard dg(f->device);
+    f->release();
+  }
   delete f;
   return kOk;
 }
@@ -377,7 +388,21 @@ FLAMED_API int flamed_fac_load(flamed_fac_t h, const float* const* w, int nw, hi
   FL_REQUIRE(f && w, "flamed_fac_load: null args");
   FL_REQUIRE(nw == flamed_fac_num_weights(h), "flamed_fac_load: expected %d weights, got %d", flamed_fac_num_weights(h), nw);
   for (int i = 0; i < nw; ++i) FL_REQUIRE(w[i], "flamed_fac_load: weight %d is null", i);
+  int wdev = -1;
+  FL_REQUIRE(device_of(w[0], &wdev) == kOk, "flamed_fac_load: weights must be device memory");
+  for (int i = 1; i < nw; ++i) FL_REQUIRE_ON(w[i], wdev, "flamed_fac_load");
+  std::lock_guard<std::mutex> lk(f->mu);
+  if (f->device >= 0 && f->device != wdev) {
+    DeviceGuard og(f->device);
+    f->release();
+  }
+  f->device = wdev;
+  FL_ON_DEVICE(wdev);
   const size_t es = f->dt == FLAMED_BF16 ? 2 : 4;
+  VecCopies vc;  // every vector is copied into the arena (the caller may free its tensors)
+  auto act = [&](FacAct& a, const float* const* p, int ch) {
+    vc.add(p[0], ch, &a.alpha); vc.add(p[1], ch, &a.beta); vc.add(p[2], 12, &a.fu); vc.add(p[3], 12, &a.fd);
+  };
   // ---- arena layout
   struct Conv { const float *g, *v, *b; int dim0, inner, kind, N, Cin, KT, s; size_t off; };  // kind 0 conv, 1 convT
   std::vector<Conv> convs;
@@ -389,42 +414,48 @@ FLAMED_API int flamed_fac_load(flamed_fac_t h, const float* const* w, int nw, hi
     convs.push_back(c);
     return (int)convs.size() - 1;
   };
-  f->tlw = w[0]; f->tlb = w[1];
+  vc.add(w[0], 2ull * f->C0 * f->C0, &f->tlw); vc.add(w[1], 2ull * f->C0, &f->tlb);
   int ci = add(w[2], w[3], w[4], 0, f->CI, f->C0, 7, 0);
-  f->bin = w[4];
+  vc.add(w[4], f->CI, &f->bin);
   std::vector<int> idx_t(f->NUP), idx7(f->NUP * 3), idx1(f->NUP * 3);
   int c = f->CI;
   for (int i = 0; i < f->NUP; ++i) {
     const float* const* bw = w + 5 + FLAMED_FAC_BLOCK_W * i;
     FacBlk& bk = f->blk[i];
     bk.s = f->ups[i]; bk.cin = c; bk.cout = c / 2;
-    bk.a = FacAct{bw[0], bw[1], bw[2], bw[3]};
+    act(bk.a, bw, bk.cin);
     idx_t[i] = add(bw[4], bw[5], bw[6], 1, bk.cout, bk.cin, 2 * bk.s, bk.s);
-    bk.bt = bw[6];
+    vc.add(bw[6], bk.cout, &bk.bt);
     const int dils[3] = {1, 3, 9};
     for (int j = 0; j < 3; ++j) {
       const float* const* rw = bw + 7 + 14 * j;
       FacRU& ru = bk.ru[j];
       ru.dil = dils[j];
-      ru.a1 = FacAct{rw[0], rw[1], rw[2], rw[3]};
+      act(ru.a1, rw, bk.cout);
       idx7[i * 3 + j] = add(rw[4], rw[5], rw[6], 0, bk.cout, bk.cout, 7, 0);
-      ru.b7 = rw[6];
-      ru.a2 = FacAct{rw[7], rw[8], rw[9], rw[10]};
+      vc.add(rw[6], bk.cout, &ru.b7);
+      act(ru.a2, rw + 7, bk.cout);
       idx1[i * 3 + j] = add(rw[11], rw[12], rw[13], 0, bk.cout, bk.cout, 1, 0);
-      ru.b1 = rw[13];
+      vc.add(rw[13], bk.cout, &ru.b1);
     }
     c /= 2;
   }
   f->cfin = c;
   const float* const* fw = w + 5 + FLAMED_FAC_BLOCK_W * f->NUP;
-  f->afin = FacAct{fw[0], fw[1], fw[2], fw[3]};
-  f->bout = fw[6];
+  act(f->afin, fw, c);
+  vc.add(fw[6], 1, &f->bout);
   size_t o_out = off;
   off = al256(off + 4ull * c * 7);
   size_t o_tmp = off;
   off = al256(off + 4 * maxfold);
-  if (f->dev) { FL_HIP(hipFree(f->dev)); f->dev = nullptr; }
+  const size_t o_vec = off;
+  off = al256(off + vc.bytes);
+  f->release();
   FL_HIP(hipMalloc(&f->dev, off));
+  {
+    const int rc = vc.commit(f->dev + o_vec, st);
+    if (rc) return rc;
+  }
   float* tmp = reinterpret_cast<float*>(f->dev + o_tmp);
   for (const Conv& cv : convs) {
     hipLaunchKernelGGL(wn_fold_kernel, dim3(cv.dim0), dim3(256), 0, st, cv.g, cv.v, cv.inner, tmp);
@@ -467,6 +498,11 @@ FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const flo
   Fac* f = reinterpret_cast<Fac*>(h);
   FL_REQUIRE(f && f->dev, "flamed_fac_decode: handle not loaded");
   FL_REQUIRE(latents && spk && wav && ws && B > 0 && T > 0, "flamed_fac_decode: bad args");
+  std::lock_guard<std::mutex> lk(f->mu);
+  FL_ON_DEVICE(f->device);
+  FL_REQUIRE_ON(latents, f->device, "flamed_fac_decode");
+  const Tune tsnap = tune_snapshot(nullptr);
+  TuneScope ts_(&tsnap);
   if (ws_bytes < fac_ws_layout(f, B, T, nullptr, nullptr)) {
     set_error("flamed_fac_decode: workspace too small");
     return kNoWorkspace;
@@ -600,9 +636,18 @@ struct Enc {
   void* wfin = nullptr; const float* bfin = nullptr;
   int cfin;
   char* dev = nullptr;
+  int device = -1;  // device of the arena (from the loaded weights)
+  std::mutex mu;    // one call at a time per handle
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap = nullptr;
   std::vector<const void*> gkey;
+  void release() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (cap) (void)hipStreamDestroy(cap);
+    if (dev) (void)hipFree(dev);
+    gexec = nullptr; cap = nullptr; dev = nullptr;
+    gkey.clear();
+  }
 };
 
 static int kpad64(int k) { return (k + 63) / 64 * 64; }
@@ -700,9 +745,11 @@ FLAMED_API int flamed_enc_create(int ngf, int n_down, const int* ratios, int out
 FLAMED_API int flamed_enc_destroy(flamed_enc_t h) {
   Enc* e = reinterpret_cast<Enc*>(h);
   if (!e) return kOk;
-  if (e->gexec) (void)hipGraphExecDestroy(e->gexec);
-  if (e->cap) (void)hipStreamDestroy(e->cap);
-  if (e->dev) (void)hipFree(e->dev);
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    DeviceGuard dg(e->device);
+    e->release();
+  }
   delete e;
   return kOk;
 }
@@ -722,7 +769,21 @@ FLAMED_API int flamed_enc_load(flamed_enc_t h, const float* const* w, int nw, hi
   FL_REQUIRE(e && w, "flamed_enc_load: null args");
   FL_REQUIRE(nw == flamed_enc_num_weights(h), "flamed_enc_load: expected %d weights, got %d", flamed_enc_num_weights(h), nw);
   for (int i = 0; i < nw; ++i) FL_REQUIRE(w[i], "flamed_enc_load: weight %d is null", i);
+  int wdev = -1;
+  FL_REQUIRE(device_of(w[0], &wdev) == kOk, "flamed_enc_load: weights must be device memory");
+  for (int i = 1; i < nw; ++i) FL_REQUIRE_ON(w[i], wdev, "flamed_enc_load");
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (e->device >= 0 && e->device != wdev) {
+    DeviceGuard og(e->device);
+    e->release();
+  }
+  e->device = wdev;
+  FL_ON_DEVICE(wdev);
   const size_t es = e->dt == FLAMED_BF16 ? 2 : 4;
+  VecCopies vc;  // every vector is copied into the arena (the caller may free its tensors)
+  auto act = [&](FacAct& a, const float* const* p, int ch) {
+    vc.add(p[0], ch, &a.alpha); vc.add(p[1], ch, &a.beta); vc.add(p[2], 12, &a.fu); vc.add(p[3], 12, &a.fd);
+  };
   struct Conv { const float *g, *v; int N, Cin, KT, ldk; size_t off; };
   std::vector<Conv> convs;
   size_t off = 0, maxfold = 0;
@@ -735,7 +796,7 @@ FLAMED_API int flamed_enc_load(flamed_enc_t h, const float* const* w, int nw, hi
   // conv_in (ngf, 1, 7): folded fp32 for the direct kernel
   const size_t o_in = off;
   off = al256(off + 4ull * e->ngf * 7);
-  e->b_in = w[2];
+  vc.add(w[2], e->ngf, &e->b_in);
   std::vector<int> i7(e->NDN * 3), i1(e->NDN * 3), ic(e->NDN);
   int d = e->ngf;
   for (int i = 0; i < e->NDN; ++i) {
@@ -747,29 +808,35 @@ FLAMED_API int flamed_enc_load(flamed_enc_t h, const float* const* w, int nw, hi
       const float* const* rw = bw + 14 * j;
       EncRU& ru = bk.ru[j];
       ru.dil = dils[j];
-      ru.a1 = FacAct{rw[0], rw[1], rw[2], rw[3]};
+      act(ru.a1, rw, d);
       ru.k7 = kpad64(7 * d);
       i7[i * 3 + j] = add(rw[4], rw[5], d, d, 7, ru.k7);
-      ru.b7 = rw[6];
-      ru.a2 = FacAct{rw[7], rw[8], rw[9], rw[10]};
+      vc.add(rw[6], d, &ru.b7);
+      act(ru.a2, rw + 7, d);
       ru.k1 = kpad64(d);
       i1[i * 3 + j] = add(rw[11], rw[12], d, d, 1, ru.k1);
-      ru.b1 = rw[13];
+      vc.add(rw[13], d, &ru.b1);
     }
-    bk.a = FacAct{bw[42], bw[43], bw[44], bw[45]};
+    act(bk.a, bw + 42, d);
     ic[i] = add(bw[46], bw[47], 2 * d, d, 2 * bk.s, 2 * bk.s * d);
-    bk.bc = bw[48];
+    vc.add(bw[48], 2 * d, &bk.bc);
     d *= 2;
   }
   e->cfin = d;
   const float* const* fw = w + 3 + FLAMED_ENC_BLOCK_W * e->NDN;
-  e->afin = FacAct{fw[0], fw[1], fw[2], fw[3]};
+  act(e->afin, fw, d);
   const int ifin = add(fw[4], fw[5], e->cout, d, 3, kpad64(3 * d));
-  e->bfin = fw[6];
+  vc.add(fw[6], e->cout, &e->bfin);
   const size_t o_tmp = off;
   off = al256(off + 4 * maxfold);
-  if (e->dev) { FL_HIP(hipFree(e->dev)); e->dev = nullptr; }
+  const size_t o_vec = off;
+  off = al256(off + vc.bytes);
+  e->release();
   FL_HIP(hipMalloc(&e->dev, off));
+  {
+    const int rc = vc.commit(e->dev + o_vec, st);
+    if (rc) return rc;
+  }
   FL_HIP(hipMemsetAsync(e->dev, 0, o_tmp, st));  // zero K padding of the packed weights
   float* tmp = reinterpret_cast<float*>(e->dev + o_tmp);
   hipLaunchKernelGGL(wn_fold_kernel, dim3(e->ngf), dim3(256), 0, st, w[0], w[1], 7, reinterpret_cast<float*>(e->dev + o_in));
@@ -808,6 +875,11 @@ FLAMED_API int flamed_enc_encode(flamed_enc_t h, const float* wav, int B, int n,
   FL_REQUIRE(e && e->dev, "flamed_enc_encode: handle not loaded");
   FL_REQUIRE(wav && out && ws && B > 0 && n > 0, "flamed_enc_encode: bad args");
   FL_REQUIRE(enc_len_after(e, n, e->NDN) > 0, "flamed_enc_encode: n=%d too short", n);
+  std::lock_guard<std::mutex> lk(e->mu);
+  FL_ON_DEVICE(e->device);
+  FL_REQUIRE_ON(wav, e->device, "flamed_enc_encode");
+  const Tune tsnap = tune_snapshot(nullptr);
+  TuneScope ts_(&tsnap);
   if (ws_bytes < enc_ws_layout(e, B, n, nullptr, nullptr)) {
     set_error("flamed_enc_encode: workspace too small");
     return kNoWorkspace;

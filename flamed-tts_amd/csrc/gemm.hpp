@@ -674,11 +674,9 @@ struct SplitCtx {
   int max_split = 4;
 };
 extern thread_local SplitCtx* g_split;
-// Pipeline depth of the small-M (32 x 64) config: 3 = LDS ring of 3 / 2 K-steps in flight,
-// 5 / 7 = 4 / 6 K-steps of register prefetch (flamed_tune "small_stages").
-extern int g_small_stages;
-// XCD strip width of small/mid-M tile placement (SplitK::strips; flamed_tune "xcd_strips", 0 = off).
-extern int g_xcd_strips;
+// Pipeline depth of the small-M (32 x 64) config: tn().small_stages 3 = LDS ring of 3 / 2 K-steps in
+// flight, 5 / 7 = 4 / 6 K-steps of register prefetch; XCD strip width of small/mid-M tile placement:
+// tn().xcd_strips (SplitK::strips, 0 = off).
 
 struct SplitScope {
   SplitCtx* prev;
@@ -692,7 +690,8 @@ inline SplitK choose_split(int M, int N, int K) {
   SplitK sk{1, nullptr, nullptr, 0};
   {
     const int gx = N / BN;
-    if (g_xcd_strips > 0 && gx % g_xcd_strips == 0 && M < 8192) sk.strips = g_xcd_strips;
+    const int xs = tn().xcd_strips;
+    if (xs > 0 && gx % xs == 0 && M < 8192) sk.strips = xs;
   }
   SplitCtx* c = g_split;
   if (!c || DTraits<DT>::kCode != 1) return sk;  // fp32 parity mode keeps one exact FMA chain
@@ -714,13 +713,7 @@ inline int launch_gemm_cfg(const AL& al, const DT* W, int ldw, const EP& ep, int
   auto kern = gemm_kernel<BM, BN, KCH, NSTAGE, DT, AL, EP>;
   const size_t bytes = SM::bytes + (size_t)kvec_of<AL>::value * K * 4;
   FL_REQUIRE(bytes <= 160 * 1024, "gemm: LDS request %zu B too large (K=%d)", bytes, K);
-  if (bytes > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr_set = true;
-    }
-  }
+  if (bytes > 64 * 1024) FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
   hipLaunchKernelGGL(kern, grid, dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K, sk);
   FL_LAUNCH_CHECK();
   return kOk;
@@ -736,8 +729,8 @@ inline int cfg_bn(GemmCfg c) { return c == kCfgTiny ? 32 : 64; }
 template <typename DT, class AL, class EP>
 inline int launch_gemm_auto(GemmCfg c, const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   if (c == kCfgSmall) {
-    if (g_small_stages == 5) return launch_gemm_cfg<32, 64, 5, DT>(al, W, ldw, ep, M, N, K, st);
-    if (g_small_stages == 7) return launch_gemm_cfg<32, 64, 7, DT>(al, W, ldw, ep, M, N, K, st);
+    if (tn().small_stages == 5) return launch_gemm_cfg<32, 64, 5, DT>(al, W, ldw, ep, M, N, K, st);
+    if (tn().small_stages == 7) return launch_gemm_cfg<32, 64, 7, DT>(al, W, ldw, ep, M, N, K, st);
     return launch_gemm_cfg<32, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);
   }
   if (c == kCfgMid) return launch_gemm_cfg<64, 64, 3, DT>(al, W, ldw, ep, M, N, K, st);

@@ -23,8 +23,6 @@
 
 namespace fl {
 
-// LDS ring depth of the small-M DMA tiles (launch_gemm_dma; flamed_tune "dma_ns": 3, 4, 6 or 8).
-extern int g_dma_ns;
 
 // One wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane `g` to LDS [lds, lds + 1024).  Written
 // as inline asm (M0 saved and restored inside the statement, guide §5.7): hipcc does not see the DMA,
@@ -466,11 +464,7 @@ inline int launch_gemm_dma_ns(const AL& al, const bf16* W, int ldw, const EP& ep
   FL_REQUIRE(bytes <= 160 * 1024, "gemm_dma: LDS request %zu B too large (K=%d)", bytes, K);
   auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP>;
   if (bytes > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr_set = true;
-    }
+    FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
   }
   hipLaunchKernelGGL(kern, dim3(N / BN, (M + BM - 1) / BM), dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K);
   FL_LAUNCH_CHECK();
@@ -486,11 +480,7 @@ inline int launch_gemm_dma_fixed(const AL& al, const bf16* W, int ldw, const EP&
   FL_REQUIRE(bytes <= 160 * 1024, "gemm_dma: LDS request %zu B too large (K=%d)", bytes, K);
   auto kern = gemm_dma_kernel<BM, BN, NS, AL, EP, XCD, KB>;
   if (bytes > 64 * 1024) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr_set = true;
-    }
+    FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
   }
   hipLaunchKernelGGL(kern, dim3(N / BN, (M + BM - 1) / BM), dim3(kGemmThreads), bytes, st, al, W, ldw, ep, M, N, K);
   FL_LAUNCH_CHECK();
@@ -500,7 +490,7 @@ inline int launch_gemm_dma_fixed(const AL& al, const bf16* W, int ldw, const EP&
 template <int BM, int BN, class AL, class EP>
 inline int launch_gemm_dma(const AL& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
   FL_REQUIRE(M > 0 && N % BN == 0 && K % 64 == 0, "gemm_dma: unsupported shape M=%d N=%d K=%d (BN=%d)", M, N, K, BN);
-  switch (g_dma_ns) {  // ring depth (flamed_tune "dma_ns"); deeper rings fall back while LDS does not fit
+  switch (tn().dma_ns) {  // ring depth (flamed_tune "dma_ns"); deeper rings fall back while LDS does not fit
     case 8: return launch_gemm_dma_ns<BM, BN, 8>(al, W, ldw, ep, M, N, K, st);
     case 6: return launch_gemm_dma_ns<BM, BN, 6>(al, W, ldw, ep, M, N, K, st);
     case 4: return launch_gemm_dma_ns<BM, BN, 4>(al, W, ldw, ep, M, N, K, st);

@@ -1,7 +1,7 @@
 // Diagnostic probes (no reference counterpart): per-launch device time of GEMM tile variants and of
 // an empty kernel, measured as graph replays of `reps` back-to-back launches (what a captured Euler
 // step sees), to separate the fixed per-node cost from the K-chain and epilogue costs.
-#include "flamed_hip.h"
+#include "flamed_diag.h"
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
 
@@ -319,7 +319,7 @@ FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const
     FL_LAUNCH_CHECK();
     return kOk;
   };
-  FL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(stream_probe_kernel), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  FL_HIP(set_max_lds(reinterpret_cast<const void*>(stream_probe_kernel)));
   return time_graph(body, reps, st, us_out);
 }
 }  // extern "C"

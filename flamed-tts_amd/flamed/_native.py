@@ -35,14 +35,10 @@ SIGNATURES = {
     "flamed_den_velocity": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
     "flamed_den_step": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, c_size_t, P]),
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
-    "flamed_den_time_kernels": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_den_time_kernels_graph": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),
-    "flamed_stamp_buffer": (c_int, [P]),
-    "flamed_probe_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
-    "flamed_probe_empty": (c_int, [c_int, c_int, ctypes.POINTER(c_float), P]),
-    "flamed_probe_gemm_pf": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
-    "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
+    "flamed_den_tune": (c_int, [P, ctypes.c_char_p, c_int]),
+    "flamed_den_device": (c_int, [P]),
     "flamed_dur_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(P)]),
     "flamed_dur_destroy": (c_int, [P]),
     "flamed_dur_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
@@ -65,6 +61,17 @@ SIGNATURES = {
     "flamed_enc_encode": (c_int, [P, P, c_int, c_int, P, P, c_size_t, c_int, P]),
 }
 
+# include/flamed_diag.h: probes in libflamed_diag.so, phase stamps in libflamed_hip_stamps.so (tools only)
+DIAG_LIB_PATH = os.path.join(_HERE, "_native", "libflamed_diag.so")
+DIAG_SIGNATURES = {
+    "flamed_last_error": (ctypes.c_char_p, []),
+    "flamed_probe_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
+    "flamed_probe_empty": (c_int, [c_int, c_int, ctypes.POINTER(c_float), P]),
+    "flamed_probe_gemm_pf": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
+    "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
+    "flamed_stamp_buffer": (c_int, [P]),
+}
+
 FLAMED_F32, FLAMED_BF16 = 0, 1
 DTYPES = {"f32": FLAMED_F32, "fp32": FLAMED_F32, "float32": FLAMED_F32, "bf16": FLAMED_BF16, "bfloat16": FLAMED_BF16}
 
@@ -80,15 +87,32 @@ def lib():
                 raise RuntimeError(
                     f"Flamed HIP extension not found at {LIB_PATH}. Build it with "
                     "`make -C flamed-tts_amd/csrc` (or `python -c 'import __graft_entry__ as g; g.build()'`).")
-            so = ctypes.CDLL(LIB_PATH)
-            for name, (res, args) in SIGNATURES.items():
-                fn = getattr(so, name, None)
-                if fn is None:
-                    continue
-                fn.restype = res
-                fn.argtypes = args
-            _lib = so
+            _lib = _bind(ctypes.CDLL(LIB_PATH), {**DIAG_SIGNATURES, **SIGNATURES})
     return _lib
+
+
+def _bind(so, sigs):
+    for name, (res, args) in sigs.items():
+        fn = getattr(so, name, None)
+        if fn is None:  # e.g. flamed_stamp_buffer exists only in the FL_STAMPS build
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return so
+
+
+_diag = None
+
+
+def diag_lib():
+    """The diagnostic probe library (tools only; never loaded by the product path)."""
+    global _diag
+    with _lock:
+        if _diag is None:
+            if not os.path.exists(DIAG_LIB_PATH):
+                raise RuntimeError(f"diagnostic library not found at {DIAG_LIB_PATH} (make -C flamed-tts_amd/csrc diag)")
+            _diag = _bind(ctypes.CDLL(DIAG_LIB_PATH), DIAG_SIGNATURES)
+    return _diag
 
 
 def check(rc: int, what: str) -> None:

@@ -148,6 +148,15 @@ class FACodecEncoder(nn.Module):
                 nn.init.trunc_normal_(m.weight, std=0.02)
                 nn.init.constant_(m.bias, 0)
 
+    def hip_invalidate(self):
+        """Force the next HIP call to re-pack the weights (load_state_dict does this by itself)."""
+        if self._hip is not None:
+            self._hip._sig = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.hip_invalidate()  # load_state_dict copies in place: same pointers, maybe no version bump
+        super()._load_from_state_dict(*args, **kwargs)
+
     def _use_hip(self, x):
         return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
 
@@ -241,6 +250,15 @@ class FACodecDecoder(nn.Module):
         extra = {k: v for k, v in state_dict.items() if k not in own}
         self.unused_state = extra
         return super().load_state_dict({k: v for k, v in state_dict.items() if k in own}, strict=strict, assign=assign)
+
+    def hip_invalidate(self):
+        """Force the next HIP call to re-pack the weights (load_state_dict does this by itself)."""
+        if self._hip is not None:
+            self._hip._sig = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.hip_invalidate()  # load_state_dict copies in place: same pointers, maybe no version bump
+        super()._load_from_state_dict(*args, **kwargs)
 
     def _use_hip(self, x):
         return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))

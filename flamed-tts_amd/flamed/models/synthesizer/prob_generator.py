@@ -235,6 +235,17 @@ class SimpleMLPAdaLN(nn.Module):
             self._hip = DenoiserHIP(self, self.hip_dtype)
         return self._hip
 
+    def hip_invalidate(self):
+        """Force the next HIP call to re-pack the weights.  load_state_dict does this by itself (below);
+        call it after writing parameters in place under inference_mode, where tensors carry no
+        version counter."""
+        if self._hip is not None:
+            self._hip._sig = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.hip_invalidate()  # load_state_dict copies in place: same pointers, maybe no version bump
+        super()._load_from_state_dict(*args, **kwargs)
+
     def forward(self, x, t, c):
         if self._use_hip(x):
             return self.hip().velocity(x, t, c)

@@ -112,11 +112,18 @@ def _hip_ok(t: torch.Tensor, module: nn.Module) -> bool:
     return not (torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()))
 
 
+def _lr_hip_ok(x: torch.Tensor) -> bool:
+    """The HIP length regulator writes a fresh buffer (no autograd graph): it serves inference only.
+    Under autograd (training, PVA.compute_loss -> Flamed.forward) the differentiable repeat_interleave
+    path runs, as in the reference (pva.py:125-166)."""
+    return x.is_cuda and not (torch.is_grad_enabled() and x.requires_grad)
+
+
 class LengthRegulator(nn.Module):
     """Interleaved phone/silence length regulation (reference pva.py:119-170)."""
 
     def LR(self, x, phone_duration, sil_duration, src_lens, max_len, log_domain=False):
-        if x.is_cuda:
+        if _lr_hip_ok(x):
             return hip_length_regulate(x, phone_duration, sil_duration, src_lens, max_len, log_domain)
         if log_domain:
             phone_duration = torch.clamp(torch.round(torch.exp(phone_duration) - 1), min=0)
@@ -202,7 +209,7 @@ class PVA(nn.Module):
     def sample(self, x, src_len, src_mask, max_tgt_len=None, nfe=32, temperature=1.0):
         """reference pva.py:88-116"""
         dur_t, sil_t = self.flow(x, src_mask, nfe, temperature)
-        if x.is_cuda:
+        if _lr_hip_ok(x):
             return self.length_regulator.LR(x, dur_t, sil_t, src_len, max_tgt_len, log_domain=True)
         phone_duration = torch.clamp(torch.round(torch.exp(dur_t) - 1), min=0)
         sil_duration = torch.clamp(torch.round(torch.exp(sil_t) - 1), min=0)
@@ -212,6 +219,16 @@ class PVA(nn.Module):
         if self._hip is None:
             self._hip = PvaHIP(self)
         return self._hip
+
+    def hip_invalidate(self):
+        """Force the next HIP call to re-pack the weights (after an in-place weight update that
+        load_state_dict does not cover)."""
+        if self._hip is not None:
+            self._hip._sig = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.hip_invalidate()  # load_state_dict copies in place: same pointers, maybe no version bump
+        super()._load_from_state_dict(*args, **kwargs)
 
 
 class PvaHIP:

@@ -1,0 +1,41 @@
+/* flamed_diag.h — diagnostic probes of the MI355X Flamed-TTS kernels (NOT the product library).
+ *
+ * flamed_probe_* live in libflamed_diag.so (csrc/probe.hip, `make -C flamed-tts_amd/csrc diag`);
+ * flamed_stamp_buffer lives only in libflamed_hip_stamps.so (`make stamps`: the product sources built
+ * with -DFL_STAMPS).  Nothing on the product path loads either library (tools/*.py only).
+ */
+#ifndef FLAMED_DIAG_H
+#define FLAMED_DIAG_H
+
+#include "flamed_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Average device time (us) per launch inside a graph of `reps` back-to-back launches.
+ * flamed_probe_gemm: C[M][N] (bf16) = A[M][K] (bf16) . W[N][K]^T with tile variant
+ * 0: 32x64 3-stage, 1: 64x64 3-stage, 2: 32x64 2-stage, 3: 128x128, 4: 64x128, 5: 128x64,
+ * 6: 32x64 with 4 K-steps of register prefetch, 7: 32x64 with 6, 8: 64x64 with 4.  Launch i reads
+ * weight matrix i % wbufs of W (wbufs x N x K), so a large wbufs streams weights from MALL/HBM as
+ * in a real Euler step.
+ * flamed_probe_empty: an empty kernel of `blocks` x 256 threads (the per-node floor). */
+FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int wbufs, const void* A, const void* W,
+                                 void* C, float* us_out, hipStream_t stream);
+/* flamed_probe_stream: per-CU ingest — `blocks` workgroups each stream their own `kb` KB slice of src
+ * (mode 1: LDS-DMA ring, mode 0: register loads).  src must hold blocks x kb KB. */
+FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const void* src, float* us_out, hipStream_t stream);
+FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t stream);
+/* flamed_probe_gemm_pf: flamed_probe_gemm's chain with a concurrent L2 warm-up of the next launch's
+ * weights on a second captured stream (pf_blocks workgroups, a multiple of 8; 0 = none). */
+FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, int wbufs, int pf_blocks, const void* A,
+                                    const void* W, void* C, float* us_out, hipStream_t stream);
+
+/* libflamed_hip_stamps.so only: device buffer of blocks x 8 u64 into which the denoiser kernels of
+ * class `flamed_tune("stamp_class", c)` write s_memtime at their phase boundaries (eager steps). */
+FLAMED_API int flamed_stamp_buffer(void* buf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLAMED_DIAG_H */

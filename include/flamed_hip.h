@@ -9,6 +9,11 @@
  * unless stated; work is enqueued on `stream` and is stream-ordered (no host synchronisation
  * inside, so every call is hipGraph-capturable except the *_load / *_create calls).  Scratch memory
  * comes from a caller-provided workspace sized by the matching *_workspace_size query.
+ * Handles: *_load copies or packs every weight and vector into the handle's own device arena (the
+ * caller's tensors may be freed afterwards) on the device those tensors live on; each call on a
+ * handle runs on that device and is serialised per handle (one stream at a time: the handle's step
+ * counters and cached graphs are per handle).  Diagnostic probes live in include/flamed_diag.h
+ * (libflamed_diag.so), not in this library.
  * Return value: 0 on success, otherwise a status code (1001 bad argument, 1002 workspace too small,
  * 1003 HIP runtime error); flamed_last_error() describes the last failure of the calling thread.
  */
@@ -44,9 +49,8 @@ FLAMED_API int flamed_version(void);
  *   final (12): final_layer.adaLN_modulation.1.{weight,bias}, final_layer.conv_in.conv_1.{weight,bias},
  *               final_layer.conv_in.ln_1.{weight,bias}, final_layer.conv_in.conv_2.{weight,bias},
  *               final_layer.conv_in.conv_3.{weight,bias}, final_layer.conv_out.{weight,bias}
- * The non-GEMM vectors (biases, norm gains, depthwise taps) are referenced in place: keep those
- * tensors alive while the handle is used.  GEMM weights are packed (cast / tap-reordered) into the
- * handle's own device arena.
+ * GEMM weights are packed (cast / tap-reordered) and every other vector (biases, norm gains, depthwise
+ * taps) copied into the handle's own device arena.
  */
 enum { FLAMED_DEN_HEAD_W = 8, FLAMED_DEN_BLOCK_W = 18, FLAMED_DEN_FINAL_W = 12 };
 typedef struct flamed_den_s* flamed_den_t;
@@ -91,20 +95,15 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t stream);
 
-/* Diagnostic: average device time per launch (ms) of each kernel class of an Euler step, measured
- * IN CONTEXT: `iters` full steps run eagerly with a HIP event recorded on `stream` after every
- * launch (the interval before a launch's end event = that kernel, incl. its dispatch gap).
- * Classes: 0 proj_in GEMM, 1 LN/mod+depthwise conv (+GN
- * partials, + GroupNorm finalize by the last-arriving T-chunk), 2 standalone GroupNorm finalize (only
- * when B x H/64 exceeds the handle's counters; otherwise ~0), 3 GN-apply+conv_2 GEMM+GELU, 4 conv_3 GEMM+gated residual,
- * 5 LN/mod+mlp.0 GEMM+SiLU, 6 mlp.2 GEMM+gated residual, 7 LN/mod+conv_out tap-stacked GEMM,
- * 8 conv_out tap combine.  ms_out must hold FLAMED_DEN_KERNEL_CLASSES floats.  Runs dt = 0 steps
- * (xt unchanged); clobbers the workspace. */
+/* Kernel classes of an Euler step (flamed_den_time_kernels_graph): 0 proj_in GEMM, 1 LN/mod +
+ * depthwise conv (+ GroupNorm partials, + finalize by the last-arriving T-chunk), 2 standalone GroupNorm
+ * finalize (only when B x H/64 exceeds the handle's counters; otherwise ~0), 3 GN-apply + conv_2 GEMM +
+ * GELU, 4 conv_3 GEMM + gated residual, 5 LN/mod + mlp.0 GEMM + SiLU, 6 mlp.2 GEMM + gated residual,
+ * 7 LN/mod + conv_out tap-stacked GEMM, 8 conv_out tap combine + Euler update. */
 enum { FLAMED_DEN_KERNEL_CLASSES = 9 };
-FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
-                                       size_t ws_bytes, int iters, float* ms_out, hipStream_t stream);
 
-/* Diagnostic: in-graph device time per launch (ms) of each kernel class: a captured graph of 4
+/* Measurement API (bench.py's live per-kernel timing): in-graph device time per launch (ms) of each
+ * kernel class: a captured graph of 4
  * dt = 0 Euler steps is replayed `reps` times as is and once per class with that class's launches
  * doubled (flamed_tune "dup_class"); ms_out[c] = (t_dup - t_base) / launches of c, and
  * ms_out[FLAMED_DEN_KERNEL_CLASSES] = t_base per step.  ms_out holds FLAMED_DEN_KERNEL_CLASSES + 1
@@ -112,7 +111,9 @@ FLAMED_API int flamed_den_time_kernels(flamed_den_t h, float* xt, const float* m
 FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const float* mods, int B, int T, void* ws,
                                              size_t ws_bytes, int reps, float* ms_out, hipStream_t stream);
 
-/* Tuning knobs (process-wide; diagnostic / benchmarking).  Keys:
+/* Tuning knobs.  flamed_tune sets the process defaults (thread-safe; every handle re-snapshots them at
+ * its next call); flamed_den_tune gives one denoiser handle its own values (the defaults no longer
+ * apply to it).  A handle call reads one snapshot for its whole duration.  Keys:
  *   "splitk_target" — bf16 small-M GEMMs (M < 2048 rows) split K over workgroups until about this
  *                     many workgroups are launched (default 1 = off: slower at B = 1 on gfx950);
  *   "splitk_max"    — maximum number of K slices (1, 2 or 4; default 4).
@@ -140,32 +141,14 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "xcd_strips"    — XCD strip width of small/mid-M register-staged tile placement (0 = off);
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
- *                     flamed_den_time_kernels) twice per Euler step; -1 (default) = off.
+ *                     FLAMED_DEN_KERNEL_CLASSES) twice per Euler step; -1 (default) = off.
  * Split-K sums the slices in a fixed order (deterministic).  Returns 1001 for an unknown key. */
 FLAMED_API int flamed_tune(const char* key, int value);
-
-/* Diagnostic (libflamed_hip_stamps.so only, built with -DFL_STAMPS): device buffer of blocks x 8
- * u64 into which the denoiser kernels of class `flamed_tune("stamp_class", c)` write s_memtime at
- * their phase boundaries (eager steps only).  Returns 1001 in the regular library. */
-FLAMED_API int flamed_stamp_buffer(void* buf);
-
-/* Diagnostic probes: average device time (us) per launch inside a graph of `reps` back-to-back
- * launches.  flamed_probe_gemm: C[M][N] (bf16) = A[M][K] (bf16) . W[N][K]^T with tile variant
- * 0: 32x64 3-stage, 1: 64x64 3-stage, 2: 32x64 2-stage, 3: 128x128, 4: 64x128, 5: 128x64,
- * 6: 32x64 with 4 K-steps of register prefetch, 7: 32x64 with 6, 8: 64x64 with 4.  Launch i reads
- * weight matrix i % wbufs of W (wbufs x N x K), so a large wbufs streams weights from MALL/HBM as
- * in a real Euler step.
- * flamed_probe_empty: an empty kernel of `blocks` x 256 threads (the per-node floor). */
-FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int wbufs, const void* A, const void* W,
-                                 void* C, float* us_out, hipStream_t stream);
-/* flamed_probe_stream: per-CU ingest — `blocks` workgroups each stream their own `kb` KB slice of src
- * (mode 1: LDS-DMA ring, mode 0: register loads).  src must hold blocks x kb KB. */
-FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const void* src, float* us_out, hipStream_t stream);
-FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t stream);
-/* flamed_probe_gemm_pf: flamed_probe_gemm's chain with a concurrent L2 warm-up of the next launch's
- * weights on a second captured stream (pf_blocks workgroups, a multiple of 8; 0 = none). */
-FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, int wbufs, int pf_blocks, const void* A,
-                                    const void* W, void* C, float* us_out, hipStream_t stream);
+FLAMED_API int flamed_den_tune(flamed_den_t h, const char* key, int value);
+/* Device index the handle's weights live on (-1 before flamed_den_load).  Every call on a handle runs
+ * on that device (made current for the call, the caller's restored after) and rejects tensors that
+ * live on another device. */
+FLAMED_API int flamed_den_device(flamed_den_t h);
 
 /* ==================== PVA duration / silence generators + length regulator ====================
  * Replaces ProbabilisticModule.forward (pva.py:221-238) inside the Euler loop of PVA.sample
@@ -174,7 +157,8 @@ FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, 
  *   proj.{weight,bias}, time_emb.time_emb.1.{weight,bias}, time_emb.time_emb.3.{weight,bias},
  *   conv_layer.conv1d_1.conv.{weight,bias}, conv_layer.layer_norm_1.{weight,bias},
  *   conv_layer.conv1d_2.conv.{weight,bias}, conv_layer.layer_norm_2.{weight,bias}, linear_layer.{weight,bias}
- * Vectors are referenced in place (keep them alive); the proj split and conv taps are packed. */
+ * Vectors are copied into the handle's arena; the proj split and conv taps are packed.  The
+ * (duration, silence) pair's flow graph is cached on the duration handle. */
 enum { FLAMED_DUR_W = 16 };
 typedef struct flamed_dur_s* flamed_dur_t;
 FLAMED_API int flamed_dur_create(int input_size, int filter_size, int kernel, flamed_dur_t* out);
@@ -209,7 +193,7 @@ FLAMED_API int flamed_lr_expand(const float* x, const int64_t* cum, int B, int L
  *     j.block.2.upsample.filter, j.block.2.downsample.lowpass.filter, j.block.3.{weight_g,weight_v,bias}
  *   final: model.{n_up+1}.act.{alpha,beta}, .upsample.filter, .downsample.lowpass.filter,
  *          model.{n_up+2}.{weight_g,weight_v,bias}
- * Weight norm is folded and conv weights packed at load; vectors are referenced in place. */
+ * Weight norm is folded and conv weights packed at load; vectors are copied into the arena. */
 enum { FLAMED_FAC_BLOCK_W = 49 };
 typedef struct flamed_fac_s* flamed_fac_t;
 FLAMED_API int flamed_fac_create(int in_channels, int upsample_initial_channel, int n_up, const int* up_ratios, int dtype,

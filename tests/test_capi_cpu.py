@@ -60,3 +60,55 @@ def test_host_side_validation_errors(lib):
     assert lib.flamed_fac_destroy(f) == 0
     with pytest.raises(RuntimeError, match="status 1001"):
         _native.check(lib.flamed_den_create(256, 1024, 4, 31, 256, 9, ctypes.byref(h)), "create")
+
+
+DIAG_HDR = os.path.join(os.path.dirname(PKG), "include", "flamed_diag.h")
+
+
+def test_diag_header_bound_and_separate(lib):
+    """Diagnostic probes live in libflamed_diag.so (include/flamed_diag.h), not in the product library."""
+    from flamed import _native
+    names = re.findall(r"FLAMED_API\s+[\w\s\*]+?\b(flamed_\w+)\s*\(", open(DIAG_HDR).read())
+    assert set(names) | {"flamed_last_error"} == set(_native.DIAG_SIGNATURES)
+    assert not set(names) & set(declared())
+    for n in names:
+        assert not hasattr(lib, n), f"{n} must not be exported by the product library"
+    dl = _native.diag_lib()
+    for n in names:
+        if n != "flamed_stamp_buffer":  # FL_STAMPS build only
+            assert hasattr(dl, n), n
+
+
+def test_tune_validation_and_per_handle_knobs(lib):
+    assert lib.flamed_tune(b"no_such_knob", 1) == 1001
+    assert b"unknown key" in lib.flamed_last_error()
+    assert lib.flamed_tune(b"dma_ns", 5) == 1001
+    assert lib.flamed_tune(b"dma_ns", 3) == 0
+    h = ctypes.c_void_p()
+    assert lib.flamed_den_create(256, 1024, 4, 31, 256, 1, ctypes.byref(h)) == 0
+    try:
+        assert lib.flamed_den_device(h) == -1  # not loaded yet
+        assert lib.flamed_den_tune(h, b"lnfold", 0) == 0
+        assert lib.flamed_den_tune(h, b"big_ns", 7) == 1001
+        assert lib.flamed_den_tune(None, b"lnfold", 0) == 1001
+    finally:
+        assert lib.flamed_den_destroy(h) == 0
+
+
+def test_tune_is_thread_safe(lib):
+    """flamed_tune from many threads at once: every call succeeds (the defaults are mutex-guarded)."""
+    import threading
+    errs = []
+
+    def worker(i):
+        for k in range(200):
+            rc = lib.flamed_tune(b"graph_steps", 1 + (i * 7 + k) % 64)
+            if rc:
+                errs.append(rc)
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs
+    assert lib.flamed_tune(b"graph_steps", 16) == 0

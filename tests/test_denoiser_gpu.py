@@ -3,8 +3,9 @@ reference-generated golden vectors.
 
 Tolerances (rel-L2 = ||a-b|| / ||b||):
   * f32 mode (exact fp32 MFMA, different summation order): velocity <= 2e-5, 4-step solve <= 1e-4
-  * bf16 mode (bf16 GEMM operands, fp32 accumulate/residual/norms): velocity <= 2e-2, solve <= 2e-2
-    (reference under CPU bf16 autocast drifts to 8.5e-3 velocity rel-L2)
+  * bf16 mode (bf16 GEMM operands, fp32 accumulate/residual/norms): velocity <= 8e-3 (~2x the measured
+    3.7e-3 .. 3.9e-3), short solves <= 6e-3 (SURVEY.md §8(c) allows 2e-2; the reference itself under
+    CPU bf16 autocast drifts to 8.5e-3 velocity rel-L2).  128/256-step solves: test_configs_gpu.py.
 """
 import numpy as np
 import pytest
@@ -16,6 +17,8 @@ from _common import golden, seeded, t32, rel_l2, orc, PKG
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
+BF16_VEL = 8e-3
+BF16_SOLVE = 6e-3
 
 
 def _prob_gen(dtype):
@@ -44,7 +47,7 @@ def _vel(pg, x, t, c):
         return pg.denoiser(t32(x).to(DEV), t32(t).to(DEV), t32(c).to(DEV)).cpu()
 
 
-@pytest.mark.parametrize("mode,tol", [("f32", 2e-5), ("bf16", 2e-2)])
+@pytest.mark.parametrize("mode,tol", [("f32", 2e-5), ("bf16", BF16_VEL)])
 def test_velocity_golden(mode, tol, pg_f32, pg_bf16):
     pg, _ = pg_f32 if mode == "f32" else pg_bf16
     g = golden("den_full")
@@ -64,7 +67,7 @@ def test_velocity_ragged_shapes_f32(B, T, pg_f32):
     assert rel_l2(_vel(pg, x, t, c), ref) < 2e-5
 
 
-@pytest.mark.parametrize("mode,tol", [("f32", 1e-4), ("bf16", 2e-2)])
+@pytest.mark.parametrize("mode,tol", [("f32", 1e-4), ("bf16", BF16_SOLVE)])
 def test_prob_sample_golden(mode, tol, pg_f32, pg_bf16):
     pg, _ = pg_f32 if mode == "f32" else pg_bf16
     g = golden("prob_sample")
@@ -135,7 +138,7 @@ def test_split_k_solve_bf16(target, mx, pg_bf16):
     assert torch.equal(a, b) and torch.equal(b, c)  # deterministic reduction, graph == eager
     assert rel_l2(a, base) < 5e-3  # bf16 re-rounding of U after a different fp32 summation order
     ref = orc.euler_solve(sd, x0, spk, nfe)
-    assert rel_l2(a, ref) < 2e-2
+    assert rel_l2(a, ref) < BF16_SOLVE
 
 
 @pytest.mark.parametrize("per_frame_t", [False, True])
@@ -158,8 +161,8 @@ def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
         v_fused = _vel(pg, x, t, c)
     finally:
         nat.check(L.flamed_tune(b"big", 1), "tune")
-    assert rel_l2(v_big, ref) < 2e-2
-    assert rel_l2(v_fused, ref) < 2e-2
+    assert rel_l2(v_big, ref) < BF16_VEL
+    assert rel_l2(v_fused, ref) < BF16_VEL
 
 
 @pytest.mark.parametrize("knobs,B,T", [
@@ -189,7 +192,7 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     finally:
         for k in knobs:
             nat.check(L.flamed_tune(k.encode(), defaults[k]), "tune")
-    assert rel_l2(v_hip, ref) < 2e-2
+    assert rel_l2(v_hip, ref) < BF16_VEL
 
 
 @pytest.mark.parametrize("B,T,per_frame_t", [(1, 400, False), (2, 300, True), (17, 500, False), (4, 400, False)])
@@ -244,4 +247,8 @@ def test_velocity_path_boundaries_bf16(B, T, pg_bf16):
     c = torch.randn(B, 256, generator=g)
     t = torch.tensor([[0.3]])
     ref = orc.denoiser_forward(sd, x, t, c)
-    assert rel_l2(_vel(pg, x, t, c), ref) < 2e-2
+    e = rel_l2(_vel(pg, x, t, c), ref)
+    print(f"B={B} T={T} bf16 velocity rel-L2 {e:.3e}")
+    # T <= 2: GroupNorm(H, H) over <= 2 frames per channel amplifies the bf16 rounding of the GEMM
+    # operands (measured 1.2e-2 at B=1, T=2); SURVEY.md §8(c)'s bf16 bar 2e-2 applies there
+    assert e < (BF16_VEL if T > 2 else 2e-2)

@@ -27,7 +27,7 @@ VSEL = [int(x) for x in os.environ.get("PROBE_VARIANTS", "").split(",") if x]
 
 def main():
     dev = torch.device("cuda:0")
-    L = nat.lib()
+    L = nat.diag_lib()
     st = nat.stream_ptr(dev)
     us = ctypes.c_float()
     nat.check(L.flamed_probe_empty(256, 64, ctypes.byref(us), st), "empty")
@@ -48,7 +48,7 @@ def main():
                     reps = 48 if M < 4000 else 24
                     rc = L.flamed_probe_gemm(v, M, N, K, reps, wb, nat.ptr(A), nat.ptr(W), nat.ptr(C), ctypes.byref(us), st)
                     if rc:
-                        row.append(f"{name}=ERR({nat.lib().flamed_last_error().decode()[:40]})")
+                        row.append(f"{name}=ERR({nat.diag_lib().flamed_last_error().decode()[:40]})")
                         continue
                     tf = 2 * M * N * K / (us.value * 1e-6) / 1e12
                     row.append(f"{name}={us.value:6.2f}({tf:4.0f}TF)")

@@ -13,7 +13,7 @@ from flamed import _native as nat  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    L = nat.lib()
+    L = nat.diag_lib()
     st = nat.stream_ptr(dev)
     us = ctypes.c_float()
     N = K = 1024

@@ -12,7 +12,7 @@ from flamed import _native as nat  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    L = nat.lib()
+    L = nat.diag_lib()
     st = nat.stream_ptr(dev)
     us = ctypes.c_float()
     for blocks, kb in ((208, 192), (256, 192), (208, 64), (208, 768), (1024, 192), (256, 1024)):
