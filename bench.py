@@ -70,6 +70,7 @@ def parse():
     ap.add_argument("--bn32", type=int, default=None, help="flamed_tune bn32 (32-wide small-M GEMM tiles)")
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary rows (PVA flow + LR, FaCodec decode / prompt encode, end-to-end RTF)")
     return ap.parse_args()
@@ -104,6 +105,62 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fol
     if cls == 7:
         return M * H * ea + stats + 3 * C * H * es + M * 3 * C * 4, 2 * M * 3 * C * H, 1
     return M * 3 * C * 4 + 2 * M * C * 4, 4 * M * C, 1
+
+
+def step_bytes_canonical(pg, B, T):
+    """SURVEY.md §8(d) canonical HBM bytes of one fused Euler step: W (every per-frame bf16 GEMM weight
+    + fp32 vectors and depthwise taps, streamed once per step; the AdaLN projections are hoisted out of
+    the loop) + 54,272 B per frame (bf16 activation rows of the fused design)."""
+    den = pg.denoiser
+    gemm = [den.proj_in.weight]
+    for blk in den.res_blocks:
+        gemm += [blk.conv_in.conv_2.weight, blk.conv_in.conv_3.weight, blk.mlp[0].weight, blk.mlp[2].weight]
+    fl = den.final_layer
+    gemm += [fl.conv_in.conv_2.weight, fl.conv_in.conv_3.weight, fl.conv_out.weight]
+    w_gemm = 2 * sum(w.numel() for w in gemm)
+    hoisted = {id(p) for m in [den.time_embed, den.cond_embed] + [b.adaLN_modulation for b in den.res_blocks]
+               + [fl.adaLN_modulation] for p in m.parameters()}
+    gemm_ids = {id(w) for w in gemm}
+    w_vec = 4 * sum(p.numel() for p in den.parameters() if id(p) not in hoisted and id(p) not in gemm_ids)
+    return w_gemm + w_vec + 54272 * B * T
+
+
+def measured_peaks(dev):
+    """Achievable peaks on this box: a STREAM-style copy of 2 x 1 GiB (torch's copy
+    kernel; read + write bytes) and a large bf16 library GEMM (8192^3, hipBLASLt via torch.matmul)."""
+    out = {}
+    n = 1 << 28  # 2^28 fp32 = 1 GiB
+    a = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
+    b = torch.empty_like(a)
+    ms = _time_ms(lambda: b.copy_(a), dev, reps=10, warm=3)
+    out["hbm_stream_copy_GBps"] = round(2 * 4 * n / ms / 1e6, 1)
+    del a, b
+    m = 8192
+    x = torch.randn(m, m, device=dev, dtype=torch.bfloat16)
+    y = torch.randn(m, m, device=dev, dtype=torch.bfloat16)
+    ms = _time_ms(lambda: torch.matmul(x, y), dev, reps=10, warm=3)
+    out["bf16_gemm_TFs"] = round(2 * m ** 3 / ms / 1e9, 1)
+    del x, y
+    torch.cuda.empty_cache()
+    return out
+
+
+def host_cpu():
+    """(model name, logical CPUs of the host, CPUs this process may run on)."""
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return model, os.cpu_count() or usable, usable
 
 
 def _time_ms(fn, dev, reps=5, warm=2):
@@ -364,11 +421,32 @@ def main():
                  if traffic is not None else None,
                  "algorithmic_bytes": dom["bytes"], "algorithmic_flops": dom["flops"]})
 
+    # ---- step-level roofline: SURVEY.md §8(d) canonical bytes per step / one Euler step in the graph
+    sbytes = step_bytes_canonical(pg, B, T)
+    step_s = ms[N_CLASSES] * 1e-3
+    roof["step"] = {"bytes_canonical": sbytes, "step_us": round(ms[N_CLASSES] * 1e3, 2),
+                    "achieved_GBps": round(sbytes / step_s / 1e9, 1),
+                    "frac": round(sbytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "bytes_model": "W (bf16 GEMM weights + fp32 vectors/taps) + 54,272 B per frame"}
+    peaks = None
+    if rank == 0 and world == 1 and not args.no_peaks:
+        try:
+            peaks = measured_peaks(dev)
+            roof["peak_measured"] = peaks["hbm_stream_copy_GBps"] if roof["unit"] == "GB/s" else peaks["bf16_gemm_TFs"]
+            roof["frac_of_measured"] = round(roof["achieved"] / roof["peak_measured"], 4)
+            roof["step"]["frac_of_measured"] = round(sbytes / step_s / 1e9 / peaks["hbm_stream_copy_GBps"], 4)
+        except Exception as e:  # reported, never fatal
+            peaks = {"error": f"{type(e).__name__}: {e}"}
+
     # ---- CPU baseline: oracle restatement on the host cores (rank 0, N=1 only), bounded sample
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import flamed_oracle as orc
-        ncores = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
+        cpu_model, n_host, n_usable = host_cpu()
+        # the CPU share this process is given: OMP_NUM_THREADS when the host sets it (16 per GPU on the GPU
+        # pool, whose host shows 256 logical CPUs: 256 torch threads there measured 18.5 s per Euler step
+        # against ~22 ms at 16 — oversubscribed), else every CPU in the affinity mask
+        ncores = min(n_usable, int(os.environ.get("OMP_NUM_THREADS") or n_usable))
         torch.set_num_threads(ncores)
         sd = {"prob_generator." + k: v.detach().float().cpu() for k, v in pg.state_dict().items()}
         xc = (noise * 0.3 + cond).float()
@@ -384,7 +462,7 @@ def main():
         cpu = {"value": round(B * T / solve_s, 2), "unit": "latent frames/s", "cores": ncores, "kind": "port",
                "sample": f"oracle fp32 torch-CPU restatement, B={B} T={T}: {k} of {nfe} Euler steps timed "
                          f"({tk:.2f} s), extrapolated to the full solve ({solve_s:.2f} s)",
-               "cpu": platform.processor() or platform.machine()}
+               "cpu": cpu_model, "host_logical_cpus": n_host, "threads": ncores}
 
     secondary = None
     if rank == 0 and world == 1 and not args.no_secondary:
@@ -418,6 +496,7 @@ def main():
         "kernel_timing": "in-graph per-launch cost (4-step graph with the class doubled minus as captured, HIP events)",
         "step_us_graph": round(ms[N_CLASSES] * 1e3, 2),
         "cpu_baseline": cpu,
+        "peaks": {"hbm_spec_GBps": HBM_PEAK_GBS, "bf16_dense_spec_TFs": MFMA_PEAK_TFS["bf16"], **(peaks or {})},
         "finite": finite,
         "secondary": secondary,
     }

@@ -72,6 +72,12 @@ def fill_state_dict(template: Mapping[str, torch.Tensor], seed: int) -> Dict[str
     return out
 
 
+def scale_weight_norm_gains(sd: Mapping[str, torch.Tensor], gain: float) -> Dict[str, torch.Tensor]:
+    """Scale every weight-norm gain (`*.weight_g`) by `gain`: effective conv weights x gain.  Used for
+    the non-saturating FaCodec decoder fixture (tests/golden/make_golden.py, CALM_GAIN)."""
+    return {k: (v * gain if k.endswith(".weight_g") else v) for k, v in sd.items()}
+
+
 def randomize_module(module: torch.nn.Module, seed: int) -> torch.nn.Module:
     """Load seeded weights into `module` in place (keys from its own state_dict)."""
     sd = fill_state_dict(module.state_dict(), seed)

@@ -11,7 +11,8 @@ On a ROCm device the denoiser solve, PVA flow + length regulator and FaCodec dec
 HIP library (flamed/_native); `--device cpu` runs the torch path.
 
 Multi-GPU: launched under torchrun (one process per GPU, `--master-addr 127.0.0.1`), each rank takes a
-round-robin shard of the prompts / metadata entries on cuda:LOCAL_RANK; there is no data-path
+shard of the prompts (round-robin) / metadata entries (length buckets balanced by total length,
+flamed.utils.dist.bucket_shard) on cuda:LOCAL_RANK, seeded seed + rank with --seed; there is no data-path
 collective, only the timing records are gathered for the RTF printed by rank 0.
 
 Additions (all optional; the reference's invocations behave the same):
@@ -234,7 +235,9 @@ def synthesize_with_metadata(model: Flamed, codec_encoder, codec_decoder, metada
         pending.append({"filename": filename, "prompt_path": _resolve_prompt_path(prompt_dir, prompt_filename),
                         "text": transcript, "out_path": out_path})
     rank, world, _ = fdist.dist_env()
-    pending = fdist.shard(pending, rank, world)
+    if world > 1:  # length buckets: phoneme count is the utterance-length (T x nfe work) proxy
+        costs = [int(model._preprocess_english(it["text"])[0].size(-1)) for it in pending]
+        pending = fdist.bucket_shard(pending, costs, rank, world)
     if not pending:
         return None
     for batch in _progress(chunked(pending, batch_size), total=math.ceil(len(pending) / batch_size),
@@ -297,6 +300,8 @@ def build_arg_parser():
     p.add_argument("--batch-size", type=int, default=4, help="Number of metadata samples to synthesize per batch.")
     p.add_argument("--codec-ckpt-dir", type=str, default=None,
                    help="Directory with ns3_facodec_{encoder,decoder}.bin (default: flamed/models/facodec/checkpoints).")
+    p.add_argument("--seed", type=int, default=None,
+                   help="Seed the global RNGs (rank r of a torchrun job uses seed + r); default: unseeded, as the reference.")
     return p
 
 
@@ -314,6 +319,8 @@ def main(args: Optional[argparse.Namespace] = None):
         raise
     device = resolve_device(args.device)
     distributed = fdist.init(device.type)
+    if getattr(args, "seed", None) is not None:
+        torch.manual_seed(fdist.rank_seed(args.seed))
     codec_encoder, codec_decoder = get_codec(device, getattr(args, "codec_ckpt_dir", None))
     model = prepare_model(args.cfg_path, args.ckpt_path, device, args.weights_only)
     meter = RtfMeter()

@@ -87,14 +87,42 @@ def save(name, **arrays):
     print(f"wrote {name}.npz  ({', '.join(f'{k}{tuple(v.shape)}' for k, v in out.items())})")
 
 
+CALM_GAIN = 0.6  # weight-norm gain of the non-saturating decoder fixture (see make_facodec_calm)
+
+
+def make_facodec_calm(filler, seed):
+    """FaCodec decoder fixture in a NON-saturating regime at T = 64 frames (12,800 samples): the seeded
+    unit-gain weights drive ~90 % of the output samples into tanh saturation (chaotic: bf16 rounding
+    alone costs ~20 dB), so every weight-norm gain g is scaled by CALM_GAIN (effective conv weights x
+    0.6): output std 0.04, no saturation, fp32 reference vs bf16-rounded weights 40 dB.  Pins the bf16
+    decode to an absolute SNR floor (30 dB) at a bench-like length."""
+    from flamed.models.facodec import FACodecDecoder
+    with torch.inference_mode():
+        dec = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, ngf=32, up_ratios=[5, 5, 4, 2],
+                             vq_num_q_c=2, vq_num_q_p=1, vq_num_q_r=3, vq_dim=256, codebook_dim=8,
+                             codebook_size_prosody=10, codebook_size_content=10, codebook_size_residual=10,
+                             use_gr_x_timbre=True, use_gr_residual_f0=True, use_gr_residual_phone=True).eval()
+        sd = filler.scale_weight_norm_gains(filler.fill_state_dict(dec.state_dict(), seed), CALM_GAIN)
+        dec.load_state_dict(sd)
+        g = torch.Generator().manual_seed(3)
+        lat = torch.randn(1, 256, 64, generator=g)
+        spk = torch.randn(1, 256, generator=g)
+        wav = dec.inference(lat, spk)
+        save("facodec_calm", lat=lat, spk=spk, wav=wav, gain=np.float32(CALM_GAIN), seed=seed)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", choices=["facodec_calm"], default=None, help="regenerate one fixture only")
     args = ap.parse_args()
     install_stubs()
     sys.path.insert(0, args.ref)
     filler = load_filler()
     torch.set_num_threads(8)
+    if args.only == "facodec_calm":
+        make_facodec_calm(filler, 20251205)
+        return
 
     from flamed.models.synthesizer.prob_generator import ProbGenerator, SimpleMLPAdaLN
     from flamed.models.synthesizer.pva import PVA, LengthRegulator, ProbabilisticModule
@@ -329,6 +357,7 @@ def main():
     with open(os.path.join(HERE, "state_dict_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=0, sort_keys=True)
     print("wrote state_dict_manifest.json")
+    make_facodec_calm(filler, SEED)
 
 
 if __name__ == "__main__":

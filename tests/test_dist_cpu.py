@@ -1,5 +1,7 @@
-"""Multi-GPU path rehearsed on CPU: utterances round-robin sharded over ranks, no
-data-path collective, timing records gathered once; world_size 2 over gloo via torch.distributed.run."""
+"""Multi-GPU path rehearsed on CPU: metadata utterances length-bucketed over ranks
+(contiguous buckets balanced by total length), prompts round-robin, no data-path collective, timing
+records gathered once, per-rank seeds seed + rank with per-shard parity against the oracle; world_size
+2 over gloo via torch.distributed.run."""
 import json
 import os
 import socket
@@ -13,7 +15,7 @@ from _common import PKG
 
 sys.path.insert(0, PKG)
 from flamed.utils.audio import write_wav  # noqa: E402
-from flamed.utils.dist import shard  # noqa: E402
+from flamed.utils.dist import bucket_bounds, bucket_shard, shard  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -26,6 +28,29 @@ def test_shard_partition():
     assert shard(items, 0, 1) == items
     with pytest.raises(ValueError):
         shard(items, 2, 2)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_bucket_shard_balance(world):
+    rng = np.random.default_rng(world)
+    costs = [int(c) for c in rng.integers(20, 600, 37)]
+    items = list(range(len(costs)))
+    parts = [bucket_shard(items, costs, r, world) for r in range(world)]
+    assert sorted(x for p in parts for x in p) == items
+    sums = [sum(costs[i] for i in p) for p in parts]
+    # contiguous in length order, and every bucket within one (largest) item of the mean
+    flat = [costs[i] for p in parts for i in p]
+    assert flat == sorted(costs)
+    assert max(abs(s_ - sum(costs) / world) for s_ in sums) <= max(costs)
+    assert all(parts)
+
+
+def test_bucket_bounds_edges():
+    assert bucket_bounds([], 3) == [(0, 0), (0, 0), (0, 0)]
+    assert bucket_bounds([5, 5], 4) == [(0, 1), (1, 2), (2, 2), (2, 2)]
+    assert bucket_bounds([1, 1, 1, 1], 2) == [(0, 2), (2, 4)]
+    with pytest.raises(ValueError):
+        bucket_shard([1], [1, 2], 0, 1)
 
 
 def _free_port():
@@ -59,3 +84,10 @@ def test_two_rank_sharded_synthesis(tmp_path, mode):
     else:
         assert files == [f"p{i}-2-2-0.3-0.3.wav" for i in range(3)]
     assert res["rtf"] > 0
+    if mode == "metadata":
+        ranks = [json.loads((tmp_path / f"rank{k}_{mode}.json").read_text()) for k in range(2)]
+        costs = ranks[0]["costs"]
+        assert sorted(ranks[0]["shard"] + ranks[1]["shard"]) == list(range(5))
+        assert max(costs[i] for i in ranks[0]["shard"]) <= min(costs[i] for i in ranks[1]["shard"])  # buckets
+        assert abs(ranks[0]["cost"] - ranks[1]["cost"]) <= max(costs)
+        assert all(r["shard_rel_l2"] < 1e-5 for r in ranks)

@@ -118,6 +118,17 @@ def test_facodec_decode():
     assert rel_l2(w2, g["wav2"]) < 1e-4
 
 
+def test_facodec_decode_calm():
+    """Oracle vs the reference on the non-saturating decoder fixture (weight-norm gains x 0.6, T = 64)."""
+    from flamed.utils.seeded_init import scale_weight_norm_gains
+    g = golden("facodec_calm")
+    sd = scale_weight_norm_gains(seeded("facodec_decoder"), float(g["gain"]))
+    w = orc.facodec_decode(sd, t32(g["lat"]), t32(g["spk"]))
+    assert w.shape == g["wav"].shape
+    assert float((w - t32(g["wav"])).abs().max()) < 1e-6
+    assert float(t32(g["wav"]).abs().max()) < 0.9  # not saturated
+
+
 def test_facodec_encode_and_vq():
     """Encoder, factorized RVQ codes (bit-exact) and timbre embedding vs the reference (§8(f) f3)."""
     g = golden("facodec_encode")
