@@ -213,29 +213,55 @@ def secondary_measurements(dev, nfe):
         wav = (0.1 * torch.randn(1, 1, 48000, generator=g)).to(dev)
         ms = _time_ms(lambda: enc_m(wav), dev)
         out["facodec_prompt_encode"] = {"ms": round(ms, 3), "samples": 48000, "dtype": enc_m.hip_dtype}
-        # end to end: Flamed.sample_batch (prior transformer + PVA + cond fold + denoiser) + decode
-        phon = torch.randint(1, 300, (1, L), generator=g).to(dev)
+        # condition fold (once per utterance, HIP) at the headline shape
+        pg = m.prob_generator
+        for Bc in (1, 64):
+            cond = torch.randn(Bc, 6, 400, 384, generator=g).to(dev)
+            cmask = torch.ones(Bc, 400, 1, dtype=torch.bool, device=dev)
+            ms = _time_ms(lambda: pg.fold_condition(cond, cmask), dev)
+            out[f"cond_fold_B{Bc}"] = {"ms": round(ms, 3), "frames": Bc * 400, "dtype": pg.cond_hip_dtype}
+        # end to end: Flamed.sample_batch (prior transformer + PVA + cond fold + denoiser) + decode, with
+        # both reference RTF definitions (synthesize.py:209-217 prompt mode incl. decode; :293-303
+        # metadata mode, decode excluded)
         z = enc_m(wav)
         _, codes, _, _, timbre = dec(z, eval_vq=False, vq=True)
         prompts = codes.permute(1, 0, 2).contiguous()
-        res = {}
 
-        def run():
-            torch.manual_seed(0)
-            res["o"] = m.sample_batch(phonemes=phon, src_lens=torch.tensor([L], device=dev), prompts=prompts,
-                                      timbres=timbre, codec_decoder=dec, nsteps_durgen=nfe_d, nsteps_denoiser=nfe)
-        total_ms = _time_ms(run, dev, reps=3, warm=1)
-        o = res["o"]
-        frames = int((~o["tgt_mask"]).sum().item())
-        audio_s = o["wav"].shape[-1] / 16000.0
-        t_sb = float(o["time"])
-        out["end_to_end"] = {
-            "frames": frames, "audio_s": round(audio_s, 3), "phonemes": L, "prompt_frames": int(prompts.shape[-1]),
-            "nsteps_durgen": nfe_d, "nsteps_denoiser": nfe,
-            "sample_batch_ms": round(t_sb * 1e3, 3), "with_decode_ms": round(total_ms, 3),
-            "rtf_metadata_mode": round(t_sb / audio_s, 5),
-            "rtf_with_decode": round(total_ms / 1e3 / audio_s, 5),
-            "note": "random-init weights: the utterance length T comes from the seeded duration flow"}
+        def e2e(L):
+            phon = torch.randint(1, 300, (1, L), generator=torch.Generator().manual_seed(L)).to(dev)
+            res = {}
+
+            def run():
+                torch.manual_seed(0)
+                res["o"] = m.sample_batch(phonemes=phon, src_lens=torch.tensor([L], device=dev), prompts=prompts,
+                                          timbres=timbre, codec_decoder=dec, nsteps_durgen=nfe_d, nsteps_denoiser=nfe)
+            total_ms = _time_ms(run, dev, reps=3, warm=1)
+            o = res["o"]
+            frames = int((~o["tgt_mask"]).sum().item())
+            audio_s = o["wav"].shape[-1] / 16000.0
+            t_sb = float(o["time"])
+            return {"frames": frames, "audio_s": round(audio_s, 3), "phonemes": L, "prompt_frames": int(prompts.shape[-1]),
+                    "nsteps_durgen": nfe_d, "nsteps_denoiser": nfe,
+                    "sample_batch_ms": round(t_sb * 1e3, 3), "with_decode_ms": round(total_ms, 3),
+                    "rtf_metadata_mode": round(t_sb / audio_s, 5),
+                    "rtf_with_decode": round(total_ms / 1e3 / audio_s, 5)}
+        r60 = e2e(L)
+        r60["note"] = "random-init weights: the utterance length T comes from the seeded duration flow"
+        out["end_to_end"] = r60
+        # the headline 5 s utterance: phoneme count scaled so the seeded duration flow yields ~400 frames
+        # (the seeded flow's frames per phoneme vary with the phoneme draw: a short secant search, closest kept)
+        best, Lc = r60, max(8, int(round(L * 400 / max(r60["frames"], 1))))
+        for _ in range(5):
+            r = e2e(Lc)
+            if abs(r["frames"] - 400) < abs(best["frames"] - 400):
+                best = r
+            if abs(r["frames"] - 400) <= 8:
+                break
+            Lc = max(8, int(round(Lc * 400 / max(r["frames"], 1))) + (1 if r["frames"] < 400 else -1))
+        r5 = dict(best)
+        r5["note"] = ("BASELINE metric at the configs[1] length: phoneme count chosen so the seeded duration "
+                      "flow gives ~400 frames (5 s); B = 1, nsteps-denoiser = 128")
+        out["end_to_end_5s"] = r5
     return out
 
 

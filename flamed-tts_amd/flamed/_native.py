@@ -39,6 +39,11 @@ SIGNATURES = {
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),
     "flamed_den_tune": (c_int, [P, ctypes.c_char_p, c_int]),
     "flamed_den_device": (c_int, [P]),
+    "flamed_cond_create": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(P)]),
+    "flamed_cond_destroy": (c_int, [P]),
+    "flamed_cond_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_cond_workspace_size": (c_size_t, [P, c_int, c_int]),
+    "flamed_cond_fold": (c_int, [P, P, P, c_int, c_int, P, P, c_size_t, P]),
     "flamed_dur_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(P)]),
     "flamed_dur_destroy": (c_int, [P]),
     "flamed_dur_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),

@@ -267,15 +267,36 @@ class ProbGenerator(nn.Module):
         self.cond_downsampling = ConditionDownSampler(in_channel=config["n_quantizers"] * config["cond_dim"],
                                                       out_channel=config["target_dim"],
                                                       n_stages=config["downsampling_stages"])
+        self.n_stages = config["downsampling_stages"]
         cx = config["convnext"]
         self.denoiser = SimpleMLPAdaLN(in_channels=config["target_dim"], model_channels=config["hidden_dim"],
                                        out_channels=config["target_dim"], spk_dim=config["spk_dim"],
                                        num_res_blocks=config["n_layers"], convnext_kernel=cx["kernel_size"],
                                        convnext_stride=cx["stride"], convnext_padding=cx["padding"],
                                        convnext_expand=cx["expand"], convnext_groups=cx["groups"])
+        self.cond_hip_dtype = "f32"  # condition fold GEMM operands on the HIP path ("f32" exact | "bf16")
+        self._cond_hip = None
+
+    def _cond_hip_ok(self, cond: torch.Tensor) -> bool:
+        if not cond.is_cuda:
+            return False
+        mods = (self.quantizer_encoding, self.cond_downsampling)
+        return not (torch.is_grad_enabled() and (cond.requires_grad or any(p.requires_grad for m in mods for p in m.parameters())))
 
     def fold_condition(self, cond, mask):
+        """QuantizerEncoding + ConditionDownSampler (reference :435-436); on ROCm at inference one HIP
+        call (flamed_cond_fold: three GEMMs with the quantizer encoding, GroupNorm/Mish/residual and
+        GroupNorm/ReLU applied in their operand loaders)."""
+        if self._cond_hip_ok(cond):
+            if self._cond_hip is None or self._cond_hip.dtype_name != self.cond_hip_dtype:
+                self._cond_hip = CondFoldHIP(self, self.cond_hip_dtype)
+            return self._cond_hip.fold(cond, mask)
         return self.cond_downsampling(self.quantizer_encoding(cond), mask)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        if self._cond_hip is not None:
+            self._cond_hip._sig = None  # load_state_dict copies in place: re-pack at the next call
+        super()._load_from_state_dict(*args, **kwargs)
 
     def compute_loss(self, x1, cond, spk, mask):
         """reference :414-432 (training objective; runs on torch ops under autograd)."""
@@ -442,3 +463,63 @@ class DenoiserHIP:
                                      ws.numel(), int(bool(self.den.hip_graph)), nat.stream_ptr(dev)),
                   "flamed_den_solve")
         return bufs["x"].clone()
+
+
+def cond_weight_list(pg: "ProbGenerator") -> List[torch.Tensor]:
+    """Weights in the order flamed_cond_load expects (include/flamed_hip.h)."""
+    cd = pg.cond_downsampling
+    rb = cd.resblocks[0].block.block
+    db = cd.downblocks[0]
+    return [pg.quantizer_encoding.quantizer_emb.weight, rb[0].weight, rb[0].bias, rb[1].weight, rb[1].bias,
+            db[0].weight, db[0].bias, db[1].weight, db[1].bias, cd.proj_out[0].weight, cd.proj_out[0].bias]
+
+
+class CondFoldHIP:
+    """Owns one flamed_cond_t handle (condition fold of a ProbGenerator on one device)."""
+
+    def __init__(self, pg: "ProbGenerator", dtype_name: str = "f32"):
+        self.pg = pg
+        self.dtype_name = dtype_name
+        self.code = nat.dtype_code(dtype_name)
+        self.handle = None
+        self._sig = None
+        self.ws = nat.Workspace()
+
+    def __del__(self):
+        try:
+            if self.handle is not None:
+                nat.lib().flamed_cond_destroy(self.handle)
+        except Exception:
+            pass
+
+    def _ensure(self, device):
+        params = cond_weight_list(self.pg)
+        sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(device),)
+        if sig == self._sig and self.handle is not None:
+            return
+        L = nat.lib()
+        if self.handle is None:
+            h = ctypes.c_void_p()
+            q, d = self.pg.quantizer_encoding.quantizer_emb.weight.shape
+            nat.check(L.flamed_cond_create(q, d, self.pg.target_dim, self.pg.n_stages, self.code, ctypes.byref(h)),
+                      "flamed_cond_create")
+            self.handle = h
+        keep = [p.detach().to(device=device, dtype=torch.float32).contiguous() for p in params]
+        arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
+        nat.check(L.flamed_cond_load(self.handle, arr, len(keep), nat.stream_ptr(device)), "flamed_cond_load")
+        self._keep = keep
+        self._sig = sig
+
+    def fold(self, cond: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        """cond (B, Q, T, D), mask (B, T, 1) True = valid -> (B, T, target_dim) fp32."""
+        dev = cond.device
+        self._ensure(dev)
+        B, Q, T, D = cond.shape
+        c = cond.to(torch.float32).contiguous()
+        m = mask.reshape(B, T).to(device=dev, dtype=torch.float32).contiguous()
+        out = torch.empty((B, T, self.pg.target_dim), dtype=torch.float32, device=dev)
+        L = nat.lib()
+        ws = self.ws.get(L.flamed_cond_workspace_size(self.handle, B, T), dev)
+        nat.check(L.flamed_cond_fold(self.handle, nat.ptr(c), nat.ptr(m), B, T, nat.ptr(out), nat.ptr(ws), ws.numel(),
+                                     nat.stream_ptr(dev)), "flamed_cond_fold")
+        return out

@@ -150,6 +150,25 @@ FLAMED_API int flamed_den_tune(flamed_den_t h, const char* key, int value);
  * live on another device. */
 FLAMED_API int flamed_den_device(flamed_den_t h);
 
+/* ============================ condition fold (once per utterance) ============================
+ * Replaces QuantizerEncoding (prob_generator.py:368-381) + ConditionDownSampler (:167-205, n_stages 1)
+ * of ProbGenerator.sample (:435-436), SURVEY.md §8(f) f1.  Weight order for flamed_cond_load (fp32 device
+ * tensors, prefix prob_generator.):
+ *   quantizer_encoding.quantizer_emb.weight,
+ *   cond_downsampling.resblocks.0.block.block.0.{weight,bias}, ...block.block.1.{weight,bias} (GroupNorm),
+ *   cond_downsampling.downblocks.0.0.{weight,bias}, cond_downsampling.downblocks.0.1.{weight,bias} (GroupNorm),
+ *   cond_downsampling.proj_out.0.{weight,bias}
+ * cond: (B, n_quantizers, T, cond_dim) as the reference receives it; mask: (B, T) fp32 (1 = valid frame);
+ * out: (B*T) x out_dim.  dtype FLAMED_F32 (exact fp32 MFMA) or FLAMED_BF16 GEMM operands. */
+enum { FLAMED_COND_W = 11 };
+typedef struct flamed_cond_s* flamed_cond_t;
+FLAMED_API int flamed_cond_create(int n_quantizers, int cond_dim, int out_dim, int n_stages, int dtype, flamed_cond_t* out);
+FLAMED_API int flamed_cond_destroy(flamed_cond_t h);
+FLAMED_API int flamed_cond_load(flamed_cond_t h, const float* const* weights, int n_weights, hipStream_t stream);
+FLAMED_API size_t flamed_cond_workspace_size(flamed_cond_t h, int B, int T);
+FLAMED_API int flamed_cond_fold(flamed_cond_t h, const float* cond, const float* mask, int B, int T, float* out, void* ws,
+                                size_t ws_bytes, hipStream_t stream);
+
 /* ==================== PVA duration / silence generators + length regulator ====================
  * Replaces ProbabilisticModule.forward (pva.py:221-238) inside the Euler loop of PVA.sample
  * (pva.py:97-109) and LengthRegulator.LR (pva.py:125-166, with tools.pad :299-317).

@@ -252,3 +252,38 @@ def test_velocity_path_boundaries_bf16(B, T, pg_bf16):
     # T <= 2: GroupNorm(H, H) over <= 2 frames per channel amplifies the bf16 rounding of the GEMM
     # operands (measured 1.2e-2 at B=1, T=2); SURVEY.md §8(c)'s bf16 bar 2e-2 applies there
     assert e < (BF16_VEL if T > 2 else 2e-2)
+
+
+@pytest.mark.parametrize("mode,tol", [("f32", 1e-5), ("bf16", 8e-3)])
+def test_cond_fold_golden(mode, tol, pg_f32):
+    """HIP condition fold (QuantizerEncoding + ConditionDownSampler, prob_generator.py:167-205, 368-381)
+    vs the reference's own output on padded lengths (golden prob_sample.cond_fold, lens 48/33)."""
+    pg, _ = pg_f32
+    g = golden("prob_sample")
+    lens = t32(g["lens"])
+    T = g["cond"].shape[2]
+    mask = ~(torch.arange(T)[None, :] >= lens[:, None]).unsqueeze(-1)
+    pg.cond_hip_dtype = mode
+    try:
+        with torch.inference_mode():
+            cf = pg.fold_condition(t32(g["cond"]).to(DEV), mask.to(DEV)).cpu()
+    finally:
+        pg.cond_hip_dtype = "f32"
+    e = rel_l2(cf, g["cond_fold"])
+    print(f"cond fold {mode} rel-L2 {e:.3e}")
+    assert cf.shape == g["cond_fold"].shape and e < tol
+
+
+@pytest.mark.parametrize("B,T", [(1, 400), (3, 257)])
+def test_cond_fold_vs_oracle(B, T, pg_f32):
+    pg, sd = pg_f32
+    gen = torch.Generator().manual_seed(B * 31 + T)
+    cond = torch.randn(B, 6, T, 384, generator=gen)
+    lens = torch.randint(T // 2, T + 1, (B,), generator=gen)
+    lens[0] = T
+    mask = ~(torch.arange(T)[None, :] >= lens[:, None]).unsqueeze(-1)
+    with torch.inference_mode():
+        cf = pg.fold_condition(cond.to(DEV), mask.to(DEV)).cpu()
+    e = rel_l2(cf, orc.cond_fold(sd, cond, mask))
+    print(f"cond fold B={B} T={T} f32 rel-L2 {e:.3e}")
+    assert e < 1e-5
