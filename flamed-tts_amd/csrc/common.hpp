@@ -119,6 +119,7 @@ struct Tune {
   int lnfold = 1;          // LayerNorm fold into mlp.0 / conv_out epilogues (bf16)
   int fold_big_rows = 6144;
   int graph_steps = 16;    // Euler steps per captured solve graph
+  int x16 = 0;             // large-M path: bf16 residual stream X and depthwise output D
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)
 Tune tune_snapshot(int* epoch);                       // process defaults + their epoch
@@ -243,6 +244,25 @@ template <> __device__ __forceinline__ void store_val4<bf16>(bf16* p, const floa
 }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Four / eight consecutive activations of type T (fp32 or bf16) as fp32 (16-B / 8-B / 16-B loads).
+template <typename T> __device__ __forceinline__ float4 ldx4(const T* p);
+template <> __device__ __forceinline__ float4 ldx4<float>(const float* p) { return ld4(p); }
+template <> __device__ __forceinline__ float4 ldx4<bf16>(const bf16* p) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const bf16x4 b = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(p));
+  return make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+}
+template <typename T> __device__ __forceinline__ void ldx8(const T* p, float* o);
+template <> __device__ __forceinline__ void ldx8<float>(const float* p, float* o) {
+  const float4 a = ld4(p), b = ld4(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+template <> __device__ __forceinline__ void ldx8<bf16>(const bf16* p, float* o) {
+  const bf16x8 b = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (float)b[j];
+}
 
 // ---- phase stamps (diagnostic build only: -DFL_STAMPS, libflamed_hip_stamps.so) ----
 // Thread 0 of every block writes s_memtime at numbered checkpoints into fl_stamp_buf[block][8]

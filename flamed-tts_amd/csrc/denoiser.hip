@@ -79,6 +79,7 @@ struct LoadLNMod {
   const float* __restrict__ lnw;
   const float* __restrict__ lnb;
   int kdim;  // K: columns staged per vector
+  const bf16* x16 = nullptr;  // large-M x16 path: the bf16 residual rows (normalise pass only; x unused)
   static constexpr int EPC = DTraits<DT>::EPC;
   static constexpr int kSrcBytes = 4;
   __device__ const char* src_row(int m) const { return reinterpret_cast<const char*>(x + (size_t)m * ld); }
@@ -206,10 +207,10 @@ struct LoadAdaY {
 // X = X + gate * (h + acc + b3), h = LN(X)(+affine) * (1 + sc) + sh recomputed from the same
 // stats the dwconv prologue used; emits LN partials of the new X.  Per-column vectors
 // [alpha, beta, gate] x 2 modulation rows + b3 are staged in LDS (kEVec = 8 floats per column).
-template <bool AFF>
+template <bool AFF, typename XT = float>  // XT: residual stream type (bf16 on the large-M x16 path)
 struct EpiConvNeXtResid {
   const float* __restrict__ b3;
-  float* X;
+  XT* X;
   int ld;
   const float* __restrict__ Sin;
   int NTin, twin;
@@ -229,7 +230,7 @@ struct EpiConvNeXtResid {
   static constexpr bool kPre = true;  // X[m][n] prefetched before the main loop
   static constexpr int kEVec = 9;  // fields x kEVecStride floats in LDS
   static constexpr int stat_rows(int BM) { return BM; }
-  __device__ float pre(int m, int n) const { return X[(size_t)m * ld + n]; }
+  __device__ float pre(int m, int n) const { return (float)X[(size_t)m * ld + n]; }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / mod.div, r1 = last / mod.div;
@@ -302,11 +303,11 @@ struct EpiConvNeXtResid {
   }
   static constexpr bool kStoreV = true;
   __device__ void store_v(int m, int n, float v, const float* vec, bool use, int bm, int bn) const {
-    X[(size_t)m * ld + n] = v;
+    store_val<XT>(X + (size_t)m * ld + n, v);
     if (ya) ya[(size_t)m * ld + n] = (bf16)(v * alpha_next(m, n, vec, use, bm, bn));
   }
   __device__ void store4_v(int m, int n, const float* v, const float* vec, bool use, int bm, int bn) const {
-    store_val4<float>(X + (size_t)m * ld + n, v);
+    store_val4<XT>(X + (size_t)m * ld + n, v);
     if (ya) {
       float y[4];
 #pragma unroll
@@ -314,16 +315,17 @@ struct EpiConvNeXtResid {
       store_val4<bf16>(ya + (size_t)m * ld + n, y);
     }
   }
-  __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
-  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(X + (size_t)m * ld + n, v); }
+  __device__ void store(int m, int n, float v) const { store_val<XT>(X + (size_t)m * ld + n, v); }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<XT>(X + (size_t)m * ld + n, v); }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(Sout)[(size_t)m * NTout + nt] = make_float2(mean, m2);
   }
 };
 
-struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged per column
+template <typename XT = float>
+struct EpiGatedResidT {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged per column
   const float* __restrict__ b;
-  float* X;
+  XT* X;
   int ld;
   const float* __restrict__ gate;
   int ms, div;
@@ -334,7 +336,7 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
   static constexpr bool kPre = true;  // X[m][n] prefetched before the main loop
   static constexpr int kEVec = 4;
   static constexpr int stat_rows(int) { return 0; }
-  __device__ float pre(int m, int n) const { return X[(size_t)m * ld + n]; }
+  __device__ float pre(int m, int n) const { return (float)X[(size_t)m * ld + n]; }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float*, float* vec) const {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / div, r1 = last / div;
@@ -353,8 +355,8 @@ struct EpiGatedResid {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged p
     }
     return x + gate[so.get() + (size_t)(m / div) * ms + n] * (acc + b[n]);
   }
-  __device__ void store(int m, int n, float v) const { X[(size_t)m * ld + n] = v; }
-  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(X + (size_t)m * ld + n, v); }
+  __device__ void store(int m, int n, float v) const { store_val<XT>(X + (size_t)m * ld + n, v); }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<XT>(X + (size_t)m * ld + n, v); }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(Sout)[(size_t)m * NTout + nt] = make_float2(mean, m2);
   }
@@ -487,12 +489,12 @@ constexpr int kDwCG = 64, kDwTC = 64;
 // the workgroups, half the halo re-read; measured slower at B = 64, 97 vs 82 us per launch,
 // profiles/r01_b64_bigpath.txt).  Below tn().dw_cg32_rows rows: narrow tn().dw_cg_small-channel groups.
 
-template <bool AFF, int KS, int TC, int CG = kDwCG>
-__global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restrict__ X, int H, const float* __restrict__ S,
+template <bool AFF, int KS, int TC, int CG = kDwCG, typename XT = float>  // XT: X and D type (bf16 on the x16 path)
+__global__ __launch_bounds__(256) void dwconv_stats_kernel(const XT* __restrict__ X, int H, const float* __restrict__ S,
                                                            int NT, int tw, float eps_ln, ModRef mod,
                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                            const float* __restrict__ dww, const float* __restrict__ dwb,
-                                                           float* __restrict__ D, float* __restrict__ GP, int T, int TS,
+                                                           XT* __restrict__ D, float* __restrict__ GP, int T, int TS,
                                                            int* __restrict__ gcnt, float* __restrict__ GNS) {
   constexpr int HALO = KS / 2, SR = TC + 2 * HALO, RG = 256 / CG, RPT = TC / RG, WIN = RPT + KS - 1;
   constexpr int C4 = CG / 4;                      // float4 chunks per staged row
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
     const int q = tid + j * 256;
     const int r = q / C4, c4 = q - r * C4;
     const int t = t0 - HALO + r;
-    xv[j] = (q < SR * C4 && t >= 0 && t < T) ? ld4(X + ((size_t)b * T + t) * H + c0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xv[j] = (q < SR * C4 && t >= 0 && t < T) ? ldx4<XT>(X + ((size_t)b * T + t) * H + c0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float w[KS];
 #pragma unroll
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(256) void dwconv_stats_kernel(const float* __restri
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int t = t0 + rg * RPT + q;
-      if (t < T) D[((size_t)b * T + t) * H + c] = vals[q];
+      if (t < T) store_val<XT>(D + ((size_t)b * T + t) * H + c, vals[q]);
     }
   };
   float cm = cn > 0.f ? cs / cn : 0.f, c2 = 0.f;
@@ -677,30 +679,31 @@ __global__ void gn_finalize_kernel(const float* __restrict__ GP, float* __restri
   GNS[((size_t)b * H + c) * 2 + 1] = 1.0f / sqrtf(m2 / (float)T + eps);
 }
 
-template <bool AFF>
+template <bool AFF, typename XT = float>
 // part 1: conv + partials (+ GroupNorm finalize fused in when gcnt is given); part 2: standalone
-// finalize (used only without counters).
-static int launch_dwconv_stats(const float* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw,
-                               const float* lnb, const float* dww, const float* dwb, float* D, float* GP, float* GNS,
+// finalize (used only without counters).  XT: type of X and D (bf16 on the large-M x16 path, which
+// always uses the 64-channel workgroups).
+static int launch_dwconv_stats(const XT* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw,
+                               const float* lnb, const float* dww, const float* dwb, XT* D, float* GP, float* GNS,
                                int B, int T, hipStream_t st, int part, int* gcnt) {
   FL_REQUIRE(H % kDwCG == 0 && H % 256 == 0, "dwconv: H=%d must be a multiple of 256", H);
   const int TC = ((size_t)B * T >= 8192 && tn().dw_tc_big == 128) ? 128 : kDwTC;
   const int TS = (T + TC - 1) / TC;
-  // fewer than g_dw_cg32_rows frames: 32-channel workgroups (twice the workgroups, half the serial work each)
-  const bool cg32 = (size_t)B * T < (size_t)tn().dw_cg32_rows;
+  // fewer than dw_cg32_rows frames: 32-channel workgroups (twice the workgroups, half the serial work each)
+  const bool cg32 = std::is_same<XT, float>::value && (size_t)B * T < (size_t)tn().dw_cg32_rows;
   if (part != 2) {
     if (TC == 128)
-      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, 128>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
-                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, 128, kDwCG, XT>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw,
+                         1e-6f, mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     else if (cg32 && tn().dw_cg_small == 16)
-      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 16>), dim3(H / 16, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
-                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 16, XT>), dim3(H / 16, TS, B), dim3(256), 0, st, X, H, S, NT, tw,
+                         1e-6f, mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     else if (cg32)
-      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 32>), dim3(H / 32, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
-                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, 32, XT>), dim3(H / 32, TS, B), dim3(256), 0, st, X, H, S, NT, tw,
+                         1e-6f, mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     else
-      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT, tw, 1e-6f,
-                         mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
+      hipLaunchKernelGGL((dwconv_stats_kernel<AFF, 31, kDwTC, kDwCG, XT>), dim3(H / kDwCG, TS, B), dim3(256), 0, st, X, H, S, NT,
+                         tw, 1e-6f, mod, lnw, lnb, dww, dwb, D, GP, T, TS, gcnt, GNS);
     FL_LAUNCH_CHECK();
   }
   if (part != 1 && !gcnt) {
@@ -720,6 +723,7 @@ struct LoadGN {
   const float* __restrict__ gnw;
   const float* __restrict__ gnb;
   int T;
+  const bf16* D16 = nullptr;  // large-M x16 path: bf16 depthwise output (normalise pass only; D unused)
   static constexpr int EPC = DTraits<DT>::EPC;
   static constexpr int kSrcBytes = 4;
   __device__ const char* src_row(int m) const { return reinterpret_cast<const char*>(D + (size_t)m * H); }
@@ -897,18 +901,19 @@ __global__ void cast_bf16x8_kernel(const float* __restrict__ src, int ld, bf16* 
   *reinterpret_cast<u32x4*>(dst + (size_t)m * K + c * 8) = pack_chunk<bf16>(v);
 }
 
-// A16 = GroupNorm(D) (LoadGN's arithmetic: (x - mean) * (rstd * gn_w) + gn_b)
-__global__ void gn_apply_bf16_kernel(LoadGN<bf16> al, bf16* __restrict__ dst, int M) {
+// A16 = GroupNorm(D) (LoadGN's arithmetic: (x - mean) * (rstd * gn_w) + gn_b); D fp32, or bf16 on the
+// x16 path (then written in place: each thread reads its 8 elements before storing them).
+template <typename DS>
+__global__ void gn_apply_bf16_kernel(LoadGN<bf16> al, const DS* src, bf16* dst, int M) {
   const int H = al.H, K8 = H / 8;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)M * K8) return;
   const int m = i / K8, k = (int)(i - (size_t)m * K8) * 8;
-  const float* x = al.D + (size_t)m * H + k;
+  float xv[8];
+  ldx8<DS>(src + (size_t)m * H + k, xv);
   const float* g = al.gns + ((size_t)(m / al.T) * H + k) * 2;
-  const float4 x0 = ld4(x), x1 = ld4(x + 4);
   const float4 g0 = ld4(g), g1 = ld4(g + 4), g2 = ld4(g + 8), g3 = ld4(g + 12);
   const float4 w0 = ld4(al.gnw + k), w1 = ld4(al.gnw + k + 4), b0 = ld4(al.gnb + k), b1 = ld4(al.gnb + k + 4);
-  const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
   const float mu[8] = {g0.x, g0.z, g1.x, g1.z, g2.x, g2.z, g3.x, g3.z};
   const float rs[8] = {g0.y, g0.w, g1.y, g1.w, g2.y, g2.w, g3.y, g3.w};
   const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
@@ -920,9 +925,11 @@ __global__ void gn_apply_bf16_kernel(LoadGN<bf16> al, bf16* __restrict__ dst, in
 }
 
 // A16 = LayerNorm(X) (+affine) * (1 + scale) + shift (LoadLNMod's arithmetic); 2 rows per workgroup,
-// the row statistics combined once per row from the producer's partials.
-template <bool AFF>
-__global__ __launch_bounds__(256) void lnmod_apply_bf16_kernel(LoadLNMod<bf16, AFF> al, bf16* __restrict__ dst, int M) {
+// the row statistics combined once per row from the producer's partials.  X fp32 (al.x) or the x16
+// path's bf16 rows (al.x16).
+template <bool AFF, typename XT>
+__global__ __launch_bounds__(256) void lnmod_apply_bf16_kernel(LoadLNMod<bf16, AFF> al, const XT* xs, bf16* __restrict__ dst,
+                                                               int M) {
   __shared__ float st[2][2];
   const int r = threadIdx.x >> 7, lt = threadIdx.x & 127;
   const int m = blockIdx.x * 2 + r;
@@ -934,12 +941,11 @@ __global__ __launch_bounds__(256) void lnmod_apply_bf16_kernel(LoadLNMod<bf16, A
   const size_t mo = (size_t)(m / md.div) * md.ms;
   const int K = al.kdim;
   for (int k = lt * 8; k < K; k += 128 * 8) {
-    const float* x = al.x + (size_t)m * al.ld + k;
-    const float4 x0 = ld4(x), x1 = ld4(x + 4);
+    float xv[8];
+    ldx8<XT>(xs + (size_t)m * al.ld + k, xv);
     const float4 c0 = ld4(md.sc + mo + k), c1 = ld4(md.sc + mo + k + 4), h0 = ld4(md.sh + mo + k), h1 = ld4(md.sh + mo + k + 4);
     float4 w0 = make_float4(1.f, 1.f, 1.f, 1.f), w1 = w0, b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
     if (AFF) { w0 = ld4(al.lnw + k); w1 = ld4(al.lnw + k + 4); b0 = ld4(al.lnb + k); b1 = ld4(al.lnb + k + 4); }
-    const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
     const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
@@ -963,14 +969,20 @@ static int big_prep(const LoadF32<bf16>& al, int M, int K, bf16* a16, hipStream_
 static int big_prep(const LoadGN<bf16>& al, int M, int K, bf16* a16, hipStream_t st) {
   FL_REQUIRE(K == al.H && K % 8 == 0, "big_prep(GN): K=%d", K);
   const size_t n = (size_t)M * (K / 8);
-  hipLaunchKernelGGL(gn_apply_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, al, a16, M);
+  if (al.D16)  // x16 path: bf16 depthwise output
+    hipLaunchKernelGGL(gn_apply_bf16_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, st, al, al.D16, a16, M);
+  else
+    hipLaunchKernelGGL(gn_apply_bf16_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, st, al, al.D, a16, M);
   FL_LAUNCH_CHECK();
   return kOk;
 }
 template <bool AFF>
 static int big_prep(const LoadLNMod<bf16, AFF>& al, int M, int K, bf16* a16, hipStream_t st) {
   FL_REQUIRE(K == al.kdim && K % 8 == 0, "big_prep(LN): K=%d", K);
-  hipLaunchKernelGGL(lnmod_apply_bf16_kernel<AFF>, dim3((M + 1) / 2), dim3(256), 0, st, al, a16, M);
+  if (al.x16)
+    hipLaunchKernelGGL((lnmod_apply_bf16_kernel<AFF, bf16>), dim3((M + 1) / 2), dim3(256), 0, st, al, al.x16, a16, M);
+  else
+    hipLaunchKernelGGL((lnmod_apply_bf16_kernel<AFF, float>), dim3((M + 1) / 2), dim3(256), 0, st, al, al.x, a16, M);
   FL_LAUNCH_CHECK();
   return kOk;
 }
@@ -1093,10 +1105,10 @@ struct DenCall {
   } while (0)
 
 struct DenWs {
-  float* X;    // residual stream, M x H
+  float* X;    // residual stream, M x H (bf16 rows on the x16 path)
   float* S0;   // LN partials, M x (H/64) x 2
   float* S1;
-  float* D;    // depthwise conv output, M x H fp32
+  float* D;    // depthwise conv output, M x H fp32 (bf16 on the x16 path)
   void* U;     // GEMM intermediate, M x H (DT)
   float* GP;   // GroupNorm chunk partials, B x TS x H x 3
   float* GNS;  // GroupNorm (mean, rstd), B x H x 2
@@ -1115,15 +1127,25 @@ static size_t den_slab_floats(const Den* d, int B, int T) {
   return ((M + 31) / 32) * (nmax / 64) * 4 * 32 * 64;
 }
 
+// Large-M bf16 residual stream (tune x16): X and the depthwise output D are stored as bf16 rows on the
+// large-M path (half the HBM bytes of the residual epilogues, the depthwise conv and the GroupNorm pass);
+// norms, statistics, GEMM accumulation and the Euler state stay fp32.
+static bool den_x16(const Den* d, int B, int T) {
+  const Tune& t = tn();
+  return d->dt == FLAMED_BF16 && t.x16 && t.big && (size_t)B * T >= (size_t)t.big_min_rows &&
+         !(t.bn32 && (size_t)B * T < (size_t)kTinyRows);
+}
+
 static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   size_t M = (size_t)B * T;
   size_t es = d->dt == FLAMED_BF16 ? 2 : 4;
+  const size_t xs = den_x16(d, B, T) ? 2 : 4;  // residual stream / depthwise output element size
   size_t NTmax = d->H / 32;  // LN row partials per row: H / BN, BN >= 32
   size_t TS = (T + 63) / 64;
   const size_t sl = den_slab_floats(d, B, T);
   const size_t a16 = (d->dt == FLAMED_BF16 && M >= (size_t)tn().big_min_rows) ? 2 * M * d->H : 0;  // large-M path range
   const size_t xa = d->fold ? 2 * M * d->H : 0;
-  size_t sizes[11] = {4 * M * d->H, 8 * M * NTmax, 8 * M * NTmax, 4 * M * d->H, es * M * d->H, 12 * B * TS * d->H,
+  size_t sizes[11] = {xs * M * d->H, 8 * M * NTmax, 8 * M * NTmax, xs * M * d->H, es * M * d->H, 12 * B * TS * d->H,
                       8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16, xa};
   size_t off = 0;
   void* ptrs[11];
@@ -1392,7 +1414,7 @@ namespace fl {
 // One velocity evaluation (+ Euler update when vout == nullptr).
 // `ctr` (optional): device step counter; when set the modulation rows are read at
 // mods + (*ctr) * B * MS and the last kernel increments it (graph replay of captured steps).
-template <typename DT>
+template <typename DT, typename XT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
                          const DenWs& w, int* ctr, hipStream_t st) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
@@ -1416,23 +1438,30 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   } a16_scope(w.A16);
   const int NT = H / BN;
   DT* U = reinterpret_cast<DT*>(w.U);
+  // residual stream X and depthwise output D: fp32, or bf16 rows on the large-M x16 path
+  constexpr bool X16 = std::is_same<XT, bf16>::value;
+  FL_REQUIRE(!X16 || big, "den_step: the bf16 residual stream runs on the large-M path only");
+  XT* X = reinterpret_cast<XT*>(w.X);
+  XT* Dx = reinterpret_cast<XT*>(w.D);
+  const bf16* X16p = X16 ? reinterpret_cast<const bf16*>(w.X) : nullptr;
+  const bf16* D16p = X16 ? reinterpret_cast<const bf16*>(w.D) : nullptr;
   const bool fold = std::is_same<DT, bf16>::value && d->fold && tu.lnfold && w.XA && (!big || M >= tu.fold_big_rows);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (tu.stamp_class >= 0) stamp_select(cls, st); TRY(x); if (tu.dup_class == (cls)) TRY(x); } while (0)
-  K_(0, (den_gemm<DT>(cfg, false, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStats{d->bin, w.X, H, w.S0, NT}, M, H, C, st)));
+  K_(0, (den_gemm<DT>(cfg, false, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStatsT<false, XT>{d->bin, X, H, w.S0, NT}, M, H, C, st)));
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div, so};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
-    K_(1, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
-    K_(2, (launch_dwconv_stats<true>(w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
-    K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T}, (const DT*)Bw.w2, H,
+    K_(1, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
+    K_(2, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
+    K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T, D16p}, (const DT*)Bw.w2, H,
                                         EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
     if (fold) {  // mlp.0 on x * alpha (written by conv_3's epilogue) with the LayerNorm in its epilogue
       K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
-                                          EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT,
+                                          EpiConvNeXtResid<true, XT>{Bw.b3, X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT,
                                                                  w.XA, Bw.lnmw, md + 4 * H},
                                           M, H, H, st)));
       K_(5, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.XA, H}, (const DT*)Bw.m0, H,
@@ -1440,24 +1469,24 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
                                           M, H, H, st)));
     } else {
       K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
-                                          EpiConvNeXtResid<true>{Bw.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
+                                          EpiConvNeXtResid<true, XT>{Bw.b3, X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
                                           M, H, H, st)));
-      K_(5, (den_gemm<DT>(cfg, true, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H}, (const DT*)Bw.m0, H,
+      K_(5, (den_gemm<DT>(cfg, true, LoadLNMod<DT, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H, X16p}, (const DT*)Bw.m0, H,
                                           EpiBiasAct<DT, 2>{Bw.mb0, U, H}, M, H, H, st)));
     }
     K_(6, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.m2, H,
-                                        EpiGatedResid{Bw.mb2, w.X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st)));
+                                        EpiGatedResidT<XT>{Bw.mb2, X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st)));
   }
   const float* mf = mods + (size_t)d->NB * 6 * H;
   ModRef mc{mf, mf + H, MS, mod_div, so};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div, so};
   const DenBlockW& F = d->fin;
-  K_(1, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 1, gcnt)));
-  K_(2, (launch_dwconv_stats<false>(w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, w.D, w.GP, w.GNS, B, T, st, 2, gcnt)));
-  K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  K_(1, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
+  K_(2, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
+  K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T, D16p}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   if (fold) {
     K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
-                                        EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT,
+                                        EpiConvNeXtResid<false, XT>{F.b3, X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT,
                                                                 w.XA, nullptr, mf + 4 * H},
                                         M, H, H, st)));
     K_(7, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.XA, H}, (const DT*)d->wout, H,
@@ -1465,9 +1494,9 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
                                         M, 3 * C, H, st)));
   } else {
     K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
-                                        EpiConvNeXtResid<false>{F.b3, w.X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
+                                        EpiConvNeXtResid<false, XT>{F.b3, X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
                                         M, H, H, st)));
-    K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H}, (const DT*)d->wout, H,
+    K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H, X16p}, (const DT*)d->wout, H,
                                         EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
   }
   {
@@ -1488,8 +1517,11 @@ static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, in
                     hipStream_t st, int* ctr = nullptr) {
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
-  if (d->dt == FLAMED_BF16) return den_step_impl<bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
-  return den_step_impl<float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+  if (d->dt == FLAMED_BF16) {
+    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+  }
+  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
 }
 
 // Steps per captured graph: the largest divisor of nfe that is <= tn().graph_steps (default 16; the

@@ -546,12 +546,12 @@ struct EpiBiasAct {
   __device__ void store_stats(int, int, float, float) const {}
 };
 
-// fp32 output (+ optional ReLU) + per-(row, N-tile) LayerNorm partials (mean, M2) for the
-// consumer's LayerNorm.
-template <bool RELU = false>
+// fp32 (or bf16: the large-M bf16 residual stream) output (+ optional ReLU) + per-(row, N-tile)
+// LayerNorm partials (mean, M2, of the fp32 values) for the consumer's LayerNorm.
+template <bool RELU = false, typename OT = float>
 struct EpiBiasStatsT {
   const float* __restrict__ bias;
-  float* __restrict__ out;
+  OT* __restrict__ out;
   int ldo;
   float* __restrict__ S;
   int NT;
@@ -562,8 +562,8 @@ struct EpiBiasStatsT {
     float v = acc + bias[n];
     return RELU ? fmaxf(v, 0.f) : v;
   }
-  __device__ void store(int m, int n, float v) const { out[(size_t)m * ldo + n] = v; }
-  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(out + (size_t)m * ldo + n, v); }
+  __device__ void store(int m, int n, float v) const { store_val<OT>(out + (size_t)m * ldo + n, v); }
+  __device__ void store4(int m, int n, const float* v) const { store_val4<OT>(out + (size_t)m * ldo + n, v); }
   __device__ void store_stats(int m, int nt, float mean, float m2) const {
     reinterpret_cast<float2*>(S)[(size_t)m * NT + nt] = make_float2(mean, m2);
   }

@@ -200,3 +200,30 @@ def test_cfg4_solve_256_graph_equals_eager(pg_bf16, cfg4):
     e = _solve(pg, x0, spk, 256, graph=False)
     assert torch.isfinite(a).all()
     assert torch.equal(a, e)
+
+
+@pytest.mark.parametrize("x16", [0, 1])
+def test_cfg2_large_m_residual_precision(pg_bf16, cfg2, x16):
+    """Large-M path with the fp32 (x16 0) or bf16 (x16 1) residual stream / depthwise output: velocity and
+    a 128-step solve of three utterances vs the oracle at the configs[2] shape."""
+    from flamed import _native as nat
+    pg, sd = pg_bf16
+    x0, spk = cfg2
+    L = nat.lib()
+    t = torch.tensor([[0.45]])
+    nat.check(L.flamed_tune(b"x16", x16), "tune")
+    try:
+        with torch.inference_mode():
+            v = pg.denoiser(x0.to(DEV), t.to(DEV), spk.to(DEV)).cpu()
+        a = _solve(pg, x0, spk, 128)
+        e = _solve(pg, x0, spk, 128, graph=False)
+    finally:
+        nat.check(L.flamed_tune(b"x16", 0), "tune")
+    ev = rel_l2(v, orc.denoiser_forward(sd, x0, t, spk))
+    print(f"configs[2] x16={x16} velocity rel-L2 {ev:.3e}")
+    assert ev < BF16_VEL
+    assert torch.equal(a, e)
+    for i in (0, 63):
+        es = rel_l2(a[i:i + 1], orc.euler_solve(sd, x0[i:i + 1], spk[i:i + 1], 128))
+        print(f"configs[2] x16={x16} utterance {i} 128-step rel-L2 {es:.3e}")
+        assert es < BF16_SOLVE
