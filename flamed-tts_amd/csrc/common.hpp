@@ -120,6 +120,7 @@ struct Tune {
   int fold_big_rows = 6144;
   int graph_steps = 16;    // Euler steps per captured solve graph
   int x16 = 0;             // large-M path: bf16 residual stream X and depthwise output D
+  int g8p_rows = 16384;    // large-M GEMMs from this many rows on 256 x 256 8-phase tiles (0 = off)
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)
 Tune tune_snapshot(int* epoch);                       // process defaults + their epoch

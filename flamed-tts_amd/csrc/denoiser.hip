@@ -13,6 +13,7 @@
 #include "flamed_hip.h"
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
+#include "gemm_8p.hpp"
 
 #include <mutex>
 #include <string>
@@ -231,6 +232,10 @@ struct EpiConvNeXtResid {
   static constexpr int kEVec = 9;  // fields x kEVecStride floats in LDS
   static constexpr int stat_rows(int BM) { return BM; }
   __device__ float pre(int m, int n) const { return (float)X[(size_t)m * ld + n]; }
+  __device__ void pre4(int m, int n, float* x) const {
+    const float4 v = ldx4<XT>(X + (size_t)m * ld + n);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float* st, float* vec) const {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / mod.div, r1 = last / mod.div;
@@ -337,6 +342,10 @@ struct EpiGatedResidT {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged 
   static constexpr int kEVec = 4;
   static constexpr int stat_rows(int) { return 0; }
   __device__ float pre(int m, int n) const { return (float)X[(size_t)m * ld + n]; }
+  __device__ void pre4(int m, int n, float* x) const {
+    const float4 v = ldx4<XT>(X + (size_t)m * ld + n);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  }
   __device__ bool prologue_v(int bm, int bn, int BM, int BN, int M, float*, float* vec) const {
     const int last = (bm + BM - 1 < M ? bm + BM - 1 : M - 1);
     const int r0 = bm / div, r1 = last / div;
@@ -988,6 +997,15 @@ static int big_prep(const LoadLNMod<bf16, AFF>& al, int M, int K, bf16* a16, hip
 }
 template <class EP>
 static int launch_big(const LoadPlain<bf16>& al, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  // 256 x 256 8-phase tiles once there are enough of them to fill the chip (gemm_8p.hpp; M = 25600:
+  // 855 vs 774 TF plain for the 128 x 128 ring, tools/probe_gemm.py; M = 6400: 440 vs 643 TF)
+  const int g8 = tn().g8p_rows;
+  if (g8 > 0 && M >= g8 && N % 256 == 0 && K % 128 == 0) {
+    // one 256 x 256 tile per CU at a time: use it only when the last round of tiles is well filled
+    // (conv_out's N = 768 at M = 25600 gives 300 tiles = 1.17 rounds: measured slower than the ring)
+    const size_t tiles = (size_t)((M + 255) / 256) * (N / 256), rounds = (tiles + 255) / 256;
+    if (tiles * 10 >= rounds * 256 * 7) return launch_gemm8p(al.p, al.ld, W, ldw, ep, M, N, K, st);
+  }
   if (tn().big_ns == 2) return launch_gemm_dma_fixed<128, 128, 2, true>(al, W, ldw, ep, M, N, K, st);
   return launch_gemm_dma_fixed<128, 128, 3, true>(al, W, ldw, ep, M, N, K, st);
 }

@@ -1,0 +1,328 @@
+// 256 x 256-tile bf16 GEMM for the MFMA-bound large-M regime (denoiser at B*T >= big_rows):
+// C[M][N] = A[M][K] . W[N][K]^T with A bf16 rows (LoadPlain) and any epilogue policy of gemm.hpp.
+//
+// Structure (cdna_hip_programming.md §5 "The 256^2 8-phase template"): 512 threads = 8 waves as
+// 2 (M) x 4 (N), each wave a 128 x 64 output block of 8 x 4 MFMA fragments (v_mfma_f32_16x16x32_bf16).
+// One K-tile = 64 deep: A 256 x 64 and W 256 x 64 bf16 (32 KB each) in a double-buffered LDS image
+// (128 KB).  Every operand byte travels by global_load_lds_dwordx4 (source-side XOR swizzle, lds_off<8>
+// reads), 16 KB "half-tiles" at a time: A_lo = the first 64 rows of each wave row's 128 (read by quadrant
+// Q0), A_hi = the last 64 (Q2), B_lo = the first 32 columns of each wave column's 64 (Q0, kept in
+// registers for Q3), B_hi = the other 32 (Q1).  A wave's 128 x 64 block is computed in four quadrant
+// phases per K-tile, 16 MFMAs each (Q0: A_lo x B_lo, Q1: A_lo x B_hi, Q2: A_hi x B_hi, Q3: A_hi x B_lo),
+// so each half-tile slot is read in exactly one phase:
+//   phase  1    2    3    4  |  5    6    7    8      (even K-tile in buffer 0, odd in buffer 1)
+//   reads  E.lo E.Bh E.Ah -  |  O.lo O.Bh O.Ah -
+//   loads  O.Bh O.Ah E'.Al E'.Bl | E'.Bh E'.Ah O'.Al O'.Bl     (E' = E + 2, O' = O + 2)
+//   waits               vm(4) |                vm(4)
+// Each phase: ds_reads of the phase's fragments, one half-tile of LDS-DMA (2 instructions per thread),
+// [counted vmcnt], s_barrier, lgkmcnt(0), 16 MFMAs at raised priority, s_barrier.  The two wave rows run
+// one barrier apart (the wr == 1 waves take one extra barrier up front), so one group's ds_reads overlap
+// the other's MFMAs.  Ordering rules (§5): a half-tile is read one phase after the wait that retires it
+// (the stagger needs that one barrier more), and restaged at least two phases after its last read — both
+// hold for every slot in the table above.  The wait counts are the DMA instructions issued after the
+// tile that must have landed (2 per later half-tile; fewer in the last iteration, when nothing follows).
+// Epilogue: the accumulators go through an fp32 LDS image of 256 x 128 (one column half at a time), read
+// back row-vectorised (16-B residual loads/stores, LayerNorm row partials of 128 columns over a half-wave).
+#pragma once
+#include "gemm.hpp"
+#include "gemm_dma.hpp"
+
+namespace fl {
+
+constexpr int k8pThreads = 512;
+
+template <class EP>
+struct G8Smem {
+  static constexpr int HALF = 16 * 1024;           // one half-tile: 128 rows x 128 B
+  static constexpr int BUF = 4 * HALF;             // one K-tile: A (32 KB) then W (32 KB)
+  static constexpr int ring = 2 * BUF;             // 128 KB
+  static constexpr int ctile = 256 * 128 * 4;      // epilogue image: 256 rows x 128 fp32 columns (128 KB)
+  static constexpr int body = ring > ctile ? ring : ctile;
+  static constexpr int e_stats = EP::stat_rows(256) * 2 * 4;
+  static constexpr int e_vec = kevec_of<EP>::value * kEVecStride * 4;  // per 128-column half (two copies)
+  static constexpr int bytes = (body + e_stats + 2 * e_vec + 15) / 16 * 16;
+};
+
+// tile row (A) / tile column (W) of row q in [0, 128) of half-tile h (0: lo, 1: hi)
+__device__ __forceinline__ int g8_arow(int h, int q) { return (q & 63) + ((q >> 6) << 7) + (h << 6); }
+__device__ __forceinline__ int g8_bcol(int h, int q) { return (q & 31) + ((q >> 5) << 6) + (h << 5); }
+
+// Four consecutive residual values of an epilogue with kPre: one vector load when the epilogue has pre4.
+template <class T, class = void> struct has_pre4 { static constexpr bool value = false; };
+template <class T>
+struct has_pre4<T, std::void_t<decltype(std::declval<const T&>().pre4(0, 0, (float*)nullptr))>> {
+  static constexpr bool value = true;
+};
+template <class EP>
+__device__ __forceinline__ void pre4(const EP& ep, int m, int n, float* x) {
+  if constexpr (has_pre4<EP>::value) {
+    ep.pre4(m, n, x);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = ep.pre(m, n + e);
+  }
+}
+
+template <class EP>
+__global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ W,
+                                                            int ldw, EP ep, int M, int N, int K) {
+  using SM = G8Smem<EP>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* e_stats = reinterpret_cast<float*>(smem + SM::body);
+  float* e_vec0 = e_stats + EP::stat_rows(256) * 2;
+  float* e_vec1 = e_vec0 + kevec_of<EP>::value * kEVecStride;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // XCD-aware tile order (guide §5 T1, bijective): the ~nwg/8 tiles one XCD receives are consecutive in
+  // row-major tile order, so an A row panel is fetched into one XCD's L2
+  int tx, ty;
+  {
+    const int gx = gridDim.x, nwg = gx * gridDim.y, id = blockIdx.y * gx + blockIdx.x;
+    const int xcd = id & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (id >> 3);
+    ty = wg / gx;
+    tx = wg - ty * gx;
+  }
+  const int bm = ty * 256, bn = tx * 256;
+  const int NT = K / 64;
+
+  // ---- per-lane DMA sources: wave w moves rows q = 16 w + 8 j + lane / 8 (j = 0, 1) of a half-tile;
+  // lane % 8 picks the 16-B chunk, XOR-swizzled on the source (lds_off<8> on the read, rule 21).  Kept as
+  // 32-bit element offsets from the (uniform) operand bases: 8 VGPRs instead of 8 pointers.
+  unsigned aoff[2][2], woff[2][2];  // [half][j]
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = wave * 16 + j * 8 + (lane >> 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ar = g8_arow(h, q), wn = g8_bcol(h, q);
+      const int m = bm + ar < M ? bm + ar : M - 1;
+      aoff[h][j] = (unsigned)m * (unsigned)lda + (unsigned)(((lane & 7) ^ ((ar >> 1) & 7)) << 3);
+      woff[h][j] = (unsigned)(bn + wn) * (unsigned)ldw + (unsigned)(((lane & 7) ^ ((wn >> 1) & 7)) << 3);
+    }
+  }
+  // A image rows are tile rows (byte r * 128 of the K-tile's A region); half-tile h row q lands at tile
+  // row g8_arow(h, q): the 8 rows of one instruction are consecutive there, so its 1 KB is contiguous.
+  auto issue = [&](int t, int which) __attribute__((always_inline)) {
+    // which: 0 A_lo, 1 B_lo, 2 B_hi, 3 A_hi
+    char* buf = smem + (t & 1) * SM::BUF;
+    const bool isA = which == 0 || which == 3;
+    const int h = (which == 2 || which == 3) ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q0 = wave * 16 + j * 8;  // first row of this instruction in the half-tile
+      if (isA) glds16(A + aoff[h][j] + (unsigned)t * 64u, buf + g8_arow(h, q0) * 128);
+      else glds16(W + woff[h][j] + (unsigned)t * 64u, buf + 2 * SM::HALF + g8_bcol(h, q0) * 128);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a[4][2], blo[2][2], bhi[2][2];
+  // fragment read addresses: row (wr*128 + i*16 + fr) / (wc*64 + j*16 + fr) at chunk kk*4 + fq; the lds_off
+  // swizzle ((row >> 1) & 7) reduces to (fr >> 1) & 7, so fragment i / j is +2048 B (an immediate offset)
+  const int swz = (fr >> 1) & 7;
+  const int lda0 = (wr * 128 + fr) * 128, ldb0 = 2 * SM::HALF + (wc * 64 + fr) * 128;
+  const int kc0 = ((fq ^ swz) & 7) << 4, kc1 = (((4 + fq) ^ swz) & 7) << 4;
+  auto read_a = [&](const char* ta, int i0) __attribute__((always_inline)) {
+    const char* p0 = ta + lda0 + kc0;
+    const char* p1 = ta + lda0 + kc1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a[i][0] = *reinterpret_cast<const u32x4*>(p0 + (i0 + i) * 2048);
+      a[i][1] = *reinterpret_cast<const u32x4*>(p1 + (i0 + i) * 2048);
+    }
+  };
+  auto read_b = [&](u32x4 (&b)[2][2], const char* tb, int j0) __attribute__((always_inline)) {
+    const char* p0 = tb + ldb0 + kc0;
+    const char* p1 = tb + ldb0 + kc1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      b[j][0] = *reinterpret_cast<const u32x4*>(p0 + (j0 + j) * 2048);
+      b[j][1] = *reinterpret_cast<const u32x4*>(p1 + (j0 + j) * 2048);
+    }
+  };
+  auto mfma_q = [&](int i0, int j0, const u32x4 (&b)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, a[i][kk]), __builtin_bit_cast(bf16x8, b[j][kk]), acc[i0 + i][j0 + j], 0, 0, 0);
+  };
+  auto bar = []() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one phase: reads (R), one half-tile of DMA (issued when `ld`), optional counted wait, barrier,
+  // lgkmcnt(0), MFMAs, barrier
+  auto mid = []() __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+  };
+  auto tail = []() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // ---- the epilogue's row statistics and per-column vectors (both 128-column halves) are staged first,
+  // outside the operand ring: its ordinary global loads complete before any LDS-DMA is in flight, and the
+  // accumulators are not yet live (staging them after the main loop spilled: 128 accumulators + staging)
+  constexpr bool EV = kevec_of<EP>::value > 0;
+  bool e_uv0 = false, e_uv1 = false;
+  if constexpr (EV) {
+    e_uv0 = ep.prologue_v(bm, bn, 256, 128, M, e_stats, e_vec0);
+    e_uv1 = ep.prologue_v(bm, bn + 128, 256, 128, M, e_stats, e_vec1);
+  } else {
+    ep.prologue(bm, 256, M, e_stats);
+  }
+
+  // ---- prologue: K-tile 0 whole, K-tile 1's A_lo / B_lo (the steady state's phase 7 / 8 loads)
+  issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
+  if (NT > 1) { issue(1, 0); issue(1, 1); }
+  if (NT > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+  if (wr == 1) bar();  // the second wave row runs one barrier behind
+
+  for (int t = 0; t < NT; t += 2) {
+    const char* E = smem + 0 * SM::BUF;
+    const char* O = smem + 1 * SM::BUF;
+    const bool e2 = t + 2 < NT, o2 = t + 3 < NT;  // NT is even: the odd K-tile t + 1 always exists
+    // phase 1: E.Q0 (A_lo x B_lo)
+    read_b(blo, E, 0);
+    read_a(E, 0);
+    issue(t + 1, 2);
+    mid(); mfma_q(0, 0, blo); tail();
+    // phase 2: E.Q1 (A_lo x B_hi)
+    read_b(bhi, E, 2);
+    issue(t + 1, 3);
+    mid(); mfma_q(0, 2, bhi); tail();
+    // phase 3: E.Q2 (A_hi x B_hi)
+    read_a(E, 4);
+    if (e2) issue(t + 2, 0);
+    mid(); mfma_q(4, 2, bhi); tail();
+    // phase 4: E.Q3 (A_hi x B_lo); wait: the odd K-tile has landed (E'.A_lo / B_lo may fly)
+    if (e2) issue(t + 2, 1);
+    if (e2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mid(); mfma_q(4, 0, blo); tail();
+    // phase 5: O.Q0
+    read_b(blo, O, 0);
+    read_a(O, 0);
+    if (e2) issue(t + 2, 2);
+    mid(); mfma_q(0, 0, blo); tail();
+    // phase 6: O.Q1
+    read_b(bhi, O, 2);
+    if (e2) issue(t + 2, 3);
+    mid(); mfma_q(0, 2, bhi); tail();
+    // phase 7: O.Q2
+    read_a(O, 4);
+    if (o2) issue(t + 3, 0);
+    mid(); mfma_q(4, 2, bhi); tail();
+    // phase 8: O.Q3; wait: the next even K-tile has landed (O'.A_lo / B_lo may fly)
+    if (o2) issue(t + 3, 1);
+    if (o2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    mid(); mfma_q(4, 0, blo); tail();
+  }
+  if (wr == 0) bar();  // realign the two wave rows: every LDS read of the main loop is complete after this
+  bar();
+
+  // ---- epilogue, one 128-column half at a time through a 256 x 128 fp32 image
+  float* ct = reinterpret_cast<float*>(smem);
+  auto cidx = [](int row, int col) __attribute__((always_inline)) { return row * 128 + (col ^ ((row & 3) << 4)); };
+  constexpr bool PRE = kpre_of<EP>::value;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int bnh = bn + h * 128;
+    if ((wc >> 1) == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ct[cidx(wr * 128 + i * 16 + fq * 4 + r, (wc & 1) * 64 + j * 16 + fr)] = acc[i][j][r];
+    }
+    const bool e_uv = h ? e_uv1 : e_uv0;
+    const float* e_vec = h ? e_vec1 : e_vec0;
+    __syncthreads();
+    constexpr int IT = 256 * 32 / k8pThreads, RPI = k8pThreads / 32;  // 16 rows per iteration
+    constexpr int U = 4;  // iterations whose residual loads are in flight together (16-B vector loads)
+#pragma unroll 1
+    for (int it0 = 0; it0 < IT; it0 += U) {
+      float xr[U][4];
+      if constexpr (PRE) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = (it0 + u) * RPI + (tid >> 5), c = (tid & 31) * 4;
+          pre4(ep, bm + row < M ? bm + row : M - 1, bnh + c, xr[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = (it0 + u) * RPI + (tid >> 5), c = (tid & 31) * 4;
+        const int m = bm + row < M ? bm + row : M - 1;
+        const float4 a4 = *reinterpret_cast<const float4*>(ct + cidx(row, c));
+        const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = bnh + c + e;
+          if constexpr (PRE) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bnh, xr[u][e]);
+          else if constexpr (EV) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bnh);
+          else v[e] = ep.value(m, n, av[e], e_stats, bm);
+        }
+        if constexpr (EP::kRowStats) {
+          float sum = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) sum += __shfl_xor(sum, o);
+          const float mean = sum * (1.0f / 128);
+          float q = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = v[e] - mean;
+            q += d * d;
+          }
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o);
+          if ((tid & 31) == 0 && bm + row < M) ep.store_stats(bm + row, bnh / 128, mean, q);
+        }
+        if (bm + row < M) store4(ep, bm + row, bnh + c, v, e_vec, e_uv, bm, bnh);
+      }
+    }
+    __syncthreads();  // the image is rewritten by the next half
+  }
+}
+
+// Shapes: N % 256 == 0, K % 128 == 0 (an even number of 64-deep K-tiles), any M (rows clamped / masked).
+template <class EP>
+inline int launch_gemm8p(const bf16* A, int lda, const bf16* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  FL_REQUIRE(M > 0 && N % 256 == 0 && K % 128 == 0, "gemm8p: unsupported shape M=%d N=%d K=%d", M, N, K);
+  using SM = G8Smem<EP>;
+  static_assert(SM::bytes <= 160 * 1024, "gemm8p: LDS");
+  auto kern = gemm8p_kernel<EP>;
+  FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
+  hipLaunchKernelGGL(kern, dim3(N / 256, (M + 255) / 256), dim3(k8pThreads), SM::bytes, st, A, lda, W, ldw, ep, M, N, K);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+}  // namespace fl

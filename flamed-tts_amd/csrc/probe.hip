@@ -4,6 +4,7 @@
 #include "flamed_diag.h"
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
+#include "gemm_8p.hpp"
 
 #include <vector>
 
@@ -145,6 +146,7 @@ static int probe_variant(int v, const bf16* A, const bf16* W, bf16* C, int M, in
     case 9: return probe_launch<32, 32, 3>(A, W, C, M, N, K, st);
     case 10: return launch_gemm_dma<32, 64>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 11: return launch_gemm_dma<32, 32>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
+    case 50: return launch_gemm8p(A, K, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 12: return launch_gemm_dma_fixed<128, 128, 3, true>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 13: return launch_gemm_dma_fixed<128, 128, 2, true>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);
     case 14: return launch_gemm_dma_fixed<256, 128, 3, true>(LoadPlain<bf16>{A, K}, W, K, EpiBiasAct<bf16, 0>{nullptr, C, N}, M, N, K, st);

@@ -1,0 +1,15 @@
+#!/bin/bash
+# B=64 variants on the 8-phase path: fold on/off; rocprof kernel trace of the default
+mkdir -p gpurun_out/r02i
+for v in "--x16 1" "--x16 1 --lnfold 0" "--x16 0 --lnfold 0"; do
+  tag=$(echo $v | tr -d ' -')
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary --no-peaks --batch 64 --steps 3 --warmup 1 $v > gpurun_out/r02i/b64_$tag.json 2>/dev/null || exit 1
+  python - gpurun_out/r02i/b64_$tag.json <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[1].split('/')[-1], "ms/solve", d["ms_per_step"], "step_us", d["step_us_graph"], " ".join(f"{k['name'][:10]}={k['us']}" for k in d["kernels"]))
+PY
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r02i/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-secondary --no-peaks --batch 64 --steps 1 --warmup 1 --x16 1 > $GRAFT_REPO_ROOT/gpurun_out/r02i/prof.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/gpurun_out/r02i/prof.log; exit 1; }
+echo prof ok

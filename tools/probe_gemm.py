@@ -17,9 +17,9 @@ VARIANTS = {0: "32x64s3", 9: "32x32s3", 10: "32x64dma", 11: "32x32dma", 1: "64x6
             27: "wsk16x64w8", 28: "wsk32x32w16", 29: "wsk16x32w8",
             30: "64x64sk2", 31: "64x64sk4", 32: "128x64sk2", 33: "128x64sk4", 34: "32x64sk2", 35: "32x64sk4",
             36: "64x32dma", 37: "32x32dma4", 38: "32x32k32dma8", 39: "32x32k32dma16", 40: "32x32dma8x", 41: "64x32dma4",
-            42: "32x32dma2", 43: "32x32dma8s", 44: "32x32dma4s", 45: "32x64dma4s", 46: "32x64dma4", 47: "32x32dma3"}
+            42: "32x32dma2", 43: "32x32dma8s", 44: "32x32dma4s", 45: "32x64dma4s", 46: "32x64dma4", 47: "32x32dma3", 50: "256x256x8p"}
 WSK = (22, 23, 24, 25, 26, 27, 28, 29)
-BIG = (3, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21)
+BIG = (3, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 50)
 
 
 VSEL = [int(x) for x in os.environ.get("PROBE_VARIANTS", "").split(",") if x]
@@ -57,7 +57,9 @@ def main():
                                                       ctypes.byref(us), st), "chk")
                         torch.cuda.synchronize()
                         err = (C.float() - ref).abs().max().item() / ref.abs().max().item()
-                        assert err < 2e-2, (name, err)
+                        rel = ((C.float() - ref).norm() / ref.norm()).item()
+                        if err >= 2e-2:
+                            row.append(f"[{name} WRONG max {err:.2e} rel {rel:.2e}]")
                 print(f"M={M:6d} K={K:5d} wbufs={wb:2d}: " + " ".join(row))
 
 
