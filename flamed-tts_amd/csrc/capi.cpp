@@ -81,6 +81,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"graph_steps", &Tune::graph_steps, 1, 1024, nullptr},
       {"x16", &Tune::x16, 0, 1, nullptr},
       {"g8p_rows", &Tune::g8p_rows, 0, 1 << 30, nullptr},
+      {"dwgn", &Tune::dwgn, 0, 1, nullptr},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(k.name, key) != 0) continue;

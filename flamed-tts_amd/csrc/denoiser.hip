@@ -722,6 +722,173 @@ static int launch_dwconv_stats(const XT* X, int H, const float* S, int NT, int t
   return kOk;
 }
 
+// Large-M path, one modulation row per utterance (sampling): the whole depthwise-conv + GroupNorm
+// sub-block (reference prob_generator.py:81-89) in one kernel per (utterance, 32 channels), writing
+// the normalised conv_2 A operand in bf16 directly (no D round trip, no separate GroupNorm pass).
+// grid (H/32, B), 256 threads = 16 channel pairs x 16 row groups; the conv runs on channel pairs in
+// packed fp32 (v_pk_fma_f32: two FMAs per lane per instruction, the VALU bound of this kernel).  The
+// LN row statistics of the whole utterance are combined into LDS once; the utterance is then walked in
+// 64-frame chunks: the LN+AdaLN-modulated rows (+-15 halo, zero padding at the edges) are staged in
+// LDS (double buffered, one barrier per chunk, rows padded to 40 floats so the two row groups of a
+// 32-lane LDS group hit disjoint banks), the k31 conv of 4 frames x 2 channels per thread is kept in
+// registers (NCH chunks: T <= 64 * NCH), each thread keeps shifted sums of its frames and the row
+// groups' (count, mean, M2) partials are combined once (Chan) into the GroupNorm(H,H) statistics over
+// all T frames.  The output pass applies LoadGN's arithmetic
+// (x - mean) * (rstd * gn_w) + gn_b to the register-resident values.  The X tiles of the next two
+// chunks are in flight while the current one is convolved.
+constexpr int kDgMaxT = 512;  // frames covered by the register-resident path (NCH <= 8)
+typedef float dg_f2 __attribute__((ext_vector_type(2)));
+template <bool AFF, int NCH, typename XT>
+__global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int H, const float* __restrict__ S, int NT, int tw,
+                                                   float eps_ln, ModRef mod, const float* __restrict__ lnw,
+                                                   const float* __restrict__ lnb, const float* __restrict__ dww,
+                                                   const float* __restrict__ dwb, const float* __restrict__ gnw,
+                                                   const float* __restrict__ gnb, bf16* __restrict__ A, int T) {
+  constexpr int KS = 31, HALO = KS / 2, CG = 32, NP = CG / 2, TC = 64, SR = TC + 2 * HALO, RG = 16, RPT = TC / RG;
+  constexpr int WIN = RPT + KS - 1, LDH = CG + 8;  // padded LDS row
+  constexpr int NTH = 256, C4 = CG / 4, NX = (SR * C4 + NTH - 1) / NTH;
+  __shared__ float hs[2][SR * LDH];
+  __shared__ float rs[NCH * TC * 2];
+  __shared__ float red[RG * CG * 3];
+  __shared__ float va[CG], vb[CG], gmu[CG], gsc[CG];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * CG, b = blockIdx.y;
+  const int pp = tid % NP, rg = tid / NP, c = c0 + 2 * pp;  // channels c, c + 1
+  const int nch = (T + TC - 1) / TC;
+  mod = mod.at();
+  float4 xv[2][NX];  // tiles of chunks ch and ch + 1 in flight
+  auto load_x = [&](float4* xs, int t0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int q = tid + j * NTH;
+      const int r = q / C4, c4 = q - r * C4;
+      const int t = t0 - HALO + r;
+      // unconditional load from a clamped row (rows outside the utterance are zeroed when staged): no
+      // branches around the loads, so the wait before staging chunk ch leaves chunk ch + 1's in flight
+      const int tc = min(max(t, 0), T - 1), c4c = q < SR * C4 ? c4 : 0;
+      xs[j] = ldx4<XT>(X + ((size_t)b * T + tc) * H + c0 + 4 * c4c);
+    }
+  };
+  load_x(xv[0], 0);
+  if (nch > 1) load_x(xv[1], TC);
+  for (int t = tid; t < T; t += NTH) row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rs[2 * t], rs[2 * t + 1]);
+  dg_f2 w[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) w[j] = *reinterpret_cast<const dg_f2*>(dww + (size_t)j * H + c);  // tap-major (KS, H) copy
+  const dg_f2 bias = *reinterpret_cast<const dg_f2*>(dwb + c);
+  if (tid < CG) {  // alpha/beta of the utterance's modulation row
+    const size_t mo = (((size_t)b * T) / mod.div) * mod.ms + c0 + tid;
+    const float sc1 = 1.0f + mod.sc[mo];
+    const float lw = AFF ? lnw[c0 + tid] : 1.0f, lb = AFF ? lnb[c0 + tid] : 0.0f;
+    va[tid] = lw * sc1;
+    vb[tid] = lb * sc1 + mod.sh[mo];
+  }
+  __syncthreads();
+  dg_f2 dv[NCH][RPT];
+  // GroupNorm partials of this thread's frames: shifted sums s1 = sum(x - K), s2 = sum((x - K)^2) with
+  // K = the thread's first conv output (a value of the data's own range, so no cancellation)
+  dg_f2 K = {0.f, 0.f}, s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch >= nch) break;
+    const int t0 = ch * TC;
+    float* h = hs[ch & 1];
+    float4* xc = xv[ch & 1];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int q = tid + j * NTH;
+      if (q < SR * C4) {
+        const int r = q / C4, c4 = q - r * C4;
+        const int t = t0 - HALO + r;
+        dg_f2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+        if (t >= 0 && t < T) {
+          const dg_f2 mean = rs[2 * t], rstd = rs[2 * t + 1];
+          const float4 a4 = *reinterpret_cast<const float4*>(va + 4 * c4), b4 = *reinterpret_cast<const float4*>(vb + 4 * c4);
+          lo = ((dg_f2{xc[j].x, xc[j].y} - mean) * rstd) * dg_f2{a4.x, a4.y} + dg_f2{b4.x, b4.y};
+          hi = ((dg_f2{xc[j].z, xc[j].w} - mean) * rstd) * dg_f2{a4.z, a4.w} + dg_f2{b4.z, b4.w};
+        }
+        *reinterpret_cast<float4*>(h + r * LDH + 4 * c4) = make_float4(lo.x, lo.y, hi.x, hi.y);
+      }
+    }
+    if (ch + 2 < nch) load_x(xc, t0 + 2 * TC);  // two chunks ahead, in flight during the next two convs
+    __syncthreads();  // h staged; the other buffer (chunk ch-1) is no longer read
+    dg_f2 win[WIN];
+#pragma unroll
+    for (int j = 0; j < WIN; ++j) win[j] = *reinterpret_cast<const dg_f2*>(h + (rg * RPT + j) * LDH + 2 * pp);
+    const int nv = T - (t0 + rg * RPT);  // valid frames of this thread in the chunk (may be <= 0)
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      dg_f2 a = bias;
+#pragma unroll
+      for (int j = 0; j < KS; ++j) a = __builtin_elementwise_fma(w[j], win[q + j], a);
+      dv[ch][q] = a;
+      if (ch == 0 && q == 0) K = a;
+      if (q < nv) {
+        const dg_f2 e = a - K;
+        s1 += e;
+        s2 = __builtin_elementwise_fma(e, e, s2);
+      }
+    }
+  }
+  {
+    int n = 0;  // frames this thread covered
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) n += max(0, min(RPT, T - (ch * TC + rg * RPT)));
+    const float fn = (float)n, inv = n > 0 ? 1.0f / fn : 0.f;
+    const dg_f2 m = K + s1 * inv, m2 = s2 - s1 * s1 * inv;
+    red[(rg * CG + 2 * pp) * 3 + 0] = fn;
+    red[(rg * CG + 2 * pp) * 3 + 1] = m.x;
+    red[(rg * CG + 2 * pp) * 3 + 2] = fmaxf(m2.x, 0.f);
+    red[(rg * CG + 2 * pp + 1) * 3 + 0] = fn;
+    red[(rg * CG + 2 * pp + 1) * 3 + 1] = m.y;
+    red[(rg * CG + 2 * pp + 1) * 3 + 2] = fmaxf(m2.y, 0.f);
+  }
+  __syncthreads();
+  if (tid < CG) {  // the row groups' partials, in order
+    float n = 0.f, m = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < RG; ++g) chan_combine(n, m, m2, red[(g * CG + tid) * 3], red[(g * CG + tid) * 3 + 1], red[(g * CG + tid) * 3 + 2]);
+    gmu[tid] = m;
+    gsc[tid] = (1.0f / sqrtf(m2 / (float)T + 1e-5f)) * gnw[c0 + tid];
+  }
+  __syncthreads();
+  const dg_f2 mu = {gmu[2 * pp], gmu[2 * pp + 1]}, sc = {gsc[2 * pp], gsc[2 * pp + 1]};
+  const dg_f2 sh = *reinterpret_cast<const dg_f2*>(gnb + c);
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 ob[NCH][RPT];  // all outputs converted first: the stores below then need no register waits
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const dg_f2 o = (dv[ch][q] - mu) * sc + sh;
+      ob[ch][q] = bf16x2{(bf16)o.x, (bf16)o.y};
+    }
+  bf16* ap = A + ((size_t)b * T + rg * RPT) * H + c;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+    for (int q = 0; q < RPT; ++q)
+      if (ch * TC + rg * RPT + q < T) *reinterpret_cast<bf16x2*>(ap + (size_t)(ch * TC + q) * H) = ob[ch][q];
+}
+
+template <bool AFF, typename XT>
+static int launch_dwgn(const XT* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw, const float* lnb,
+                       const float* dww, const float* dwb, const float* gnw, const float* gnb, bf16* A, int B, int T,
+                       hipStream_t st) {
+  FL_REQUIRE(H % 32 == 0 && T >= 1 && T <= kDgMaxT && mod.div % T == 0, "dwgn: H=%d T=%d div=%d", H, T, mod.div);
+  const int nch = (T + 63) / 64;
+  const dim3 g(H / 32, B), blk(256);
+#define FL_DWGN(N) hipLaunchKernelGGL((dwgn_kernel<AFF, N, XT>), g, blk, 0, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, A, T)
+  if (nch <= 2) FL_DWGN(2);
+  else if (nch <= 4) FL_DWGN(4);
+  else if (nch <= 6) FL_DWGN(6);
+  else if (nch == 7) FL_DWGN(7);
+  else FL_DWGN(8);
+#undef FL_DWGN
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
 // conv_2 A operand: GroupNorm applied on the fly, A = (D - mean) * (rstd * gn_w) + gn_b, with
 // [mean, rstd*gn_w] per (utterance, channel) staged in LDS for the <= 2 utterances of the tile.
 template <typename DT>
@@ -1464,6 +1631,8 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   const bf16* X16p = X16 ? reinterpret_cast<const bf16*>(w.X) : nullptr;
   const bf16* D16p = X16 ? reinterpret_cast<const bf16*>(w.D) : nullptr;
   const bool fold = std::is_same<DT, bf16>::value && d->fold && tu.lnfold && w.XA && (!big || M >= tu.fold_big_rows);
+  // whole-utterance depthwise conv + GroupNorm (launch_dwgn): large M, one modulation row per utterance
+  const bool dwgn = big && tu.dwgn && T <= kDgMaxT && mod_div % T == 0 && H % 64 == 0;
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (tu.stamp_class >= 0) stamp_select(cls, st); TRY(x); if (tu.dup_class == (cls)) TRY(x); } while (0)
@@ -1473,10 +1642,15 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div, so};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
-    K_(1, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
-    K_(2, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
-    K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T, D16p}, (const DT*)Bw.w2, H,
-                                        EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    if (dwgn) {  // large M: conv + GroupNorm in one kernel, conv_2 on the normalised bf16 rows
+      K_(1, (launch_dwgn<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, w.A16, B, T, st)));
+      K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.A16, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    } else {
+      K_(1, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
+      K_(2, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
+      K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T, D16p}, (const DT*)Bw.w2, H,
+                                          EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    }
     if (fold) {  // mlp.0 on x * alpha (written by conv_3's epilogue) with the LayerNorm in its epilogue
       K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)Bw.w3, H,
                                           EpiConvNeXtResid<true, XT>{Bw.b3, X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT,
@@ -1499,9 +1673,14 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   ModRef mc{mf, mf + H, MS, mod_div, so};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div, so};
   const DenBlockW& F = d->fin;
-  K_(1, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
-  K_(2, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
-  K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T, D16p}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  if (dwgn) {
+    K_(1, (launch_dwgn<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, F.gnw, F.gnb, w.A16, B, T, st)));
+    K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.A16, H}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  } else {
+    K_(1, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
+    K_(2, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
+    K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T, D16p}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  }
   if (fold) {
     K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                         EpiConvNeXtResid<false, XT>{F.b3, X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT,

@@ -172,12 +172,15 @@ def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
     ({"dw_cg": 16}, 2, 300), ({"dw_cg32": 0}, 1, 131), ({"dma_ns": 8}, 1, 400), ({"dma_ns": 4, "dma": 2}, 1, 250),
     ({"lnfold": 0}, 1, 400), ({"lnfold": 0}, 17, 500), ({"lnfold": 0, "big": 0}, 5, 400),
     ({"g8p_rows": 0}, 41, 400), ({"x16": 1}, 41, 400), ({"x16": 1, "lnfold": 0}, 41, 400), ({"x16": 1}, 5, 400),
+    ({"dwgn": 0}, 41, 400), ({"dwgn": 0, "x16": 1}, 41, 400), ({"dwgn": 1}, 30, 64), ({"dwgn": 1}, 12, 130),
+    ({"dwgn": 1}, 4, 512), ({"dwgn": 1}, 4, 513), ({"dwgn": 1, "x16": 1}, 7, 333),
 ])
 def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     """Every GEMM main-loop / tile / pipeline variant behind flamed_tune computes the same velocity (vs the
     oracle, bf16 tolerance): register-staged vs LDS-DMA, 32- vs 64-wide small tiles, mid-M, large-M ring
     depth, depthwise T-chunk, the 256 x 256 8-phase tiles (B*T = 16,400) vs the 128 x 128 ring, and the
-    large-M bf16 residual stream (x16)."""
+    large-M bf16 residual stream (x16), and the whole-utterance depthwise conv + GroupNorm kernel (dwgn:
+    1, 2, 3 and 8 frame chunks; T = 513 falls back to the chunked conv + GroupNorm pass)."""
     from flamed import _native as nat
     pg, sd = pg_bf16
     g = torch.Generator().manual_seed(B * 7 + T)
@@ -187,7 +190,7 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     ref = orc.denoiser_forward(sd, x, t, c)
     L = nat.lib()
     defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536, "dma_ns": 3, "lnfold": 1,
-                "g8p_rows": 16384, "x16": 0}
+                "g8p_rows": 16384, "x16": 0, "dwgn": 1}
     try:
         for k, v in knobs.items():
             nat.check(L.flamed_tune(k.encode(), v), "tune")
