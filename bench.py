@@ -71,6 +71,7 @@ def parse():
     ap.add_argument("--x16", type=int, default=None, help="flamed_tune x16 (large-M bf16 residual stream)")
     ap.add_argument("--g8p-rows", type=int, default=None, help="flamed_tune g8p_rows (256x256 8-phase GEMM tiles from this many rows; 0 off)")
     ap.add_argument("--dwgn", type=int, default=None, help="flamed_tune dwgn (large-M whole-utterance depthwise conv + GroupNorm kernel)")
+    ap.add_argument("--dwgn-small", type=int, default=None, help="flamed_tune dwgn_small (small-M one-workgroup depthwise conv + GroupNorm)")
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
@@ -360,7 +361,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")

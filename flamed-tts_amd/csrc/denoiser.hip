@@ -889,6 +889,177 @@ static int launch_dwgn(const XT* X, int H, const float* S, int NT, int tw, ModRe
   return kOk;
 }
 
+// Small-M path (B*T below the large-M threshold, T <= 576, one modulation row per utterance): the
+// depthwise-conv + GroupNorm sub-block (prob_generator.py:81-89) of one utterance and 8 channels in
+// one workgroup, so no cross-workgroup hand-off is needed for the GroupNorm statistics.  grid
+// (H/8, B), 256 threads = 4 channel pairs x 64 row groups of RPT consecutive frames (RPT odd: the
+// row groups of a 32-lane LDS group then hit disjoint banks).  All T (+-15 halo) LN+AdaLN-modulated
+// rows are staged in LDS at once, the conv runs in packed fp32 on channel pairs with its outputs in
+// registers (X rows and the producer's LN partials of all the thread's staged frames are loaded
+// before any is used), the GroupNorm statistics are two exact passes (sum, then sum of squared deviations: wave shuffles
+// + one LDS exchange each, fixed order), and the normalised bf16 conv_2 operand is written with
+// LoadGN's arithmetic (x - mean) * (rstd * gn_w) + gn_b.  conv_2 then runs as a plain bf16 GEMM on the
+// LDS-DMA loop.
+template <bool AFF, int RPT>
+__global__ __launch_bounds__(256) void dwgn_small_kernel(const float* __restrict__ X, int H, const float* __restrict__ S, int NT,
+                                                         int tw, float eps_ln, ModRef mod, const float* __restrict__ lnw,
+                                                         const float* __restrict__ lnb, const float* __restrict__ dww,
+                                                         const float* __restrict__ dwb, const float* __restrict__ gnw,
+                                                         const float* __restrict__ gnb, bf16* __restrict__ A, int T) {
+  constexpr int KS = 31, HALO = KS / 2, CG = 8, WIN = RPT + KS - 1, MAXR = 64 * RPT + 2 * HALO;
+  static_assert(RPT % 2 == 1, "odd RPT keeps the window reads conflict-free");
+  __shared__ float hs[MAXR * CG];
+  __shared__ dg_f2 red[2][4][4];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * CG, b = blockIdx.y;
+  const int p = tid & 3, rg = tid >> 2, c = c0 + 2 * p;
+  FL_STAMP(0);
+  mod = mod.at();
+  // this thread's staged rows r = tid, tid + 256, ... (frame r - HALO): X loads issued first (clamped
+  // rows, zeroed when staged), so they are in flight during the row-statistics pass
+  constexpr int NSR = (MAXR + 255) / 256;
+  float4 xv[NSR][2];
+#pragma unroll
+  for (int i = 0; i < NSR; ++i) {
+    const int t = min(max(tid + 256 * i - HALO, 0), T - 1);
+    const float* xr = X + ((size_t)b * T + t) * H + c0;
+    xv[i][0] = ld4(xr);
+    xv[i][1] = ld4(xr + 4);
+  }
+  // LN row statistics of this thread's staged frames, combined from the producer's partials; with
+  // NT <= 16 the partials of all its frames are loaded before any is reduced (one latency, not NSR)
+  float rmean[NSR], rrstd[NSR];
+  if (NT <= 16) {
+    float2 q[NSR][16];
+#pragma unroll
+    for (int i = 0; i < NSR; ++i) {
+      const int t = min(max(tid + 256 * i - HALO, 0), T - 1);
+      const float2* pp = reinterpret_cast<const float2*>(S) + (size_t)(b * T + t) * NT;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) q[i][k] = k < NT ? pp[k] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < NSR; ++i) {
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sm += q[i][k].x;
+      const float mean = sm / (float)NT;
+      float m2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < NT) { const float d = q[i][k].x - mean; m2 += q[i][k].y + (float)tw * d * d; }
+      rmean[i] = mean;
+      rrstd[i] = 1.0f / sqrtf(m2 / (float)(NT * tw) + eps_ln);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NSR; ++i) {
+      const int t = min(max(tid + 256 * i - HALO, 0), T - 1);
+      row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rmean[i], rrstd[i]);
+    }
+  }
+  FL_STAMP(1);
+  float va[CG], vb[CG];  // per-channel alpha/beta of the 8 staged channels
+  {
+    const size_t mo = (((size_t)b * T) / mod.div) * mod.ms + c0;
+#pragma unroll
+    for (int e = 0; e < CG; ++e) {
+      const float sc1 = 1.0f + mod.sc[mo + e];
+      const float lw = AFF ? lnw[c0 + e] : 1.0f, lb = AFF ? lnb[c0 + e] : 0.0f;
+      va[e] = lw * sc1;
+      vb[e] = lb * sc1 + mod.sh[mo + e];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NSR; ++i) {
+    const int r = tid + 256 * i, t = r - HALO;
+    if (r >= T + 2 * HALO) break;
+    float o[CG];
+#pragma unroll
+    for (int e = 0; e < CG; ++e) o[e] = 0.f;
+    if (t >= 0 && t < T) {
+      const float mean = rmean[i], rstd = rrstd[i];
+      const float xs[CG] = {xv[i][0].x, xv[i][0].y, xv[i][0].z, xv[i][0].w, xv[i][1].x, xv[i][1].y, xv[i][1].z, xv[i][1].w};
+#pragma unroll
+      for (int e = 0; e < CG; ++e) o[e] = ((xs[e] - mean) * rstd) * va[e] + vb[e];
+    }
+    *reinterpret_cast<float4*>(hs + r * CG) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(hs + r * CG + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+  dg_f2 w[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) w[j] = *reinterpret_cast<const dg_f2*>(dww + (size_t)j * H + c);
+  const dg_f2 bias = *reinterpret_cast<const dg_f2*>(dwb + c);
+  __syncthreads();
+  FL_STAMP(2);
+  dg_f2 win[WIN];
+#pragma unroll
+  for (int j = 0; j < WIN; ++j) win[j] = *reinterpret_cast<const dg_f2*>(hs + (rg * RPT + j) * CG + 2 * p);
+  dg_f2 dv[RPT];
+  const int nv = T - rg * RPT;  // valid frames of this thread (may be <= 0); rows past T are discarded
+  dg_f2 s = {0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    dg_f2 a = bias;
+#pragma unroll
+    for (int j = 0; j < KS; ++j) a = __builtin_elementwise_fma(w[j], win[q + j], a);
+    dv[q] = a;
+    if (q < nv) s += a;
+  }
+  auto block_sum = [&](dg_f2 v, int slot) __attribute__((always_inline)) -> dg_f2 {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {
+      v.x += __shfl_xor(v.x, o);
+      v.y += __shfl_xor(v.y, o);
+    }
+    if ((tid & 63) < 4) red[slot][tid >> 6][p] = v;
+    __syncthreads();
+    return ((red[slot][0][p] + red[slot][1][p]) + red[slot][2][p]) + red[slot][3][p];
+  };
+  FL_STAMP(3);
+  const float invT = 1.0f / (float)T;
+  const dg_f2 mean = block_sum(s, 0) * invT;
+  dg_f2 s2 = {0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < RPT; ++q)
+    if (q < nv) { const dg_f2 e = dv[q] - mean; s2 = __builtin_elementwise_fma(e, e, s2); }
+  const dg_f2 m2 = block_sum(s2, 1);
+  const dg_f2 sc = dg_f2{1.0f / sqrtf(m2.x * invT + 1e-5f), 1.0f / sqrtf(m2.y * invT + 1e-5f)} * *reinterpret_cast<const dg_f2*>(gnw + c);
+  const dg_f2 sh = *reinterpret_cast<const dg_f2*>(gnb + c);
+  FL_STAMP(4);
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 ob[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const dg_f2 o = (dv[q] - mean) * sc + sh;
+    ob[q] = bf16x2{(bf16)o.x, (bf16)o.y};
+  }
+  bf16* ap = A + ((size_t)b * T + rg * RPT) * H + c;
+#pragma unroll
+  for (int q = 0; q < RPT; ++q)
+    if (q < nv) *reinterpret_cast<bf16x2*>(ap + (size_t)q * H) = ob[q];
+  FL_STAMP(5);
+}
+
+constexpr int kDgSmallMaxT = 576;  // 64 row groups x RPT <= 9
+template <bool AFF>
+static int launch_dwgn_small(const float* X, int H, const float* S, int NT, int tw, ModRef mod, const float* lnw, const float* lnb,
+                             const float* dww, const float* dwb, const float* gnw, const float* gnb, bf16* A, int B, int T,
+                             hipStream_t st) {
+  FL_REQUIRE(H % 8 == 0 && T >= 1 && T <= kDgSmallMaxT && mod.div % T == 0 && NT <= 32, "dwgn_small: H=%d T=%d div=%d NT=%d", H, T,
+             mod.div, NT);
+  const dim3 g(H / 8, B), blk(256);
+#define FL_DWGNS(R) hipLaunchKernelGGL((dwgn_small_kernel<AFF, R>), g, blk, 0, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, A, T)
+  if (T <= 64) FL_DWGNS(1);
+  else if (T <= 192) FL_DWGNS(3);
+  else if (T <= 320) FL_DWGNS(5);
+  else if (T <= 448) FL_DWGNS(7);
+  else FL_DWGNS(9);
+#undef FL_DWGNS
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
 // conv_2 A operand: GroupNorm applied on the fly, A = (D - mean) * (rstd * gn_w) + gn_b, with
 // [mean, rstd*gn_w] per (utterance, channel) staged in LDS for the <= 2 utterances of the tile.
 template <typename DT>
@@ -1633,6 +1804,9 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   const bool fold = std::is_same<DT, bf16>::value && d->fold && tu.lnfold && w.XA && (!big || M >= tu.fold_big_rows);
   // whole-utterance depthwise conv + GroupNorm (launch_dwgn): large M, one modulation row per utterance
   const bool dwgn = big && tu.dwgn && T <= kDgMaxT && mod_div % T == 0 && H % 64 == 0;
+  // small M (bf16): the same sub-block in one workgroup per (utterance, 8 channels), bf16 operand in D's space
+  const bool dwgn_s = std::is_same<DT, bf16>::value && !big && !X16 && tu.dwgn_small && T <= kDgSmallMaxT && mod_div % T == 0;
+  bf16* const As = reinterpret_cast<bf16*>(w.D);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (tu.stamp_class >= 0) stamp_select(cls, st); TRY(x); if (tu.dup_class == (cls)) TRY(x); } while (0)
@@ -1645,6 +1819,9 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     if (dwgn) {  // large M: conv + GroupNorm in one kernel, conv_2 on the normalised bf16 rows
       K_(1, (launch_dwgn<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, w.A16, B, T, st)));
       K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.A16, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
+    } else if (dwgn_s) {
+      K_(1, (launch_dwgn_small<true>((const float*)w.X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, As, B, T, st)));
+      K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)As, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
     } else {
       K_(1, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
       K_(2, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
@@ -1676,6 +1853,9 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   if (dwgn) {
     K_(1, (launch_dwgn<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, F.gnw, F.gnb, w.A16, B, T, st)));
     K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.A16, H}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
+  } else if (dwgn_s) {
+    K_(1, (launch_dwgn_small<false>((const float*)w.X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, F.gnw, F.gnb, As, B, T, st)));
+    K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)As, H}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   } else {
     K_(1, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
     K_(2, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));

@@ -174,13 +174,16 @@ def test_velocity_large_m_bf16(per_frame_t, pg_bf16):
     ({"g8p_rows": 0}, 41, 400), ({"x16": 1}, 41, 400), ({"x16": 1, "lnfold": 0}, 41, 400), ({"x16": 1}, 5, 400),
     ({"dwgn": 0}, 41, 400), ({"dwgn": 0, "x16": 1}, 41, 400), ({"dwgn": 1}, 30, 64), ({"dwgn": 1}, 12, 130),
     ({"dwgn": 1}, 4, 512), ({"dwgn": 1}, 4, 513), ({"dwgn": 1, "x16": 1}, 7, 333),
+    ({"dwgn_small": 0}, 1, 400), ({"dwgn_small": 0}, 2, 300), ({"dwgn_small": 1}, 1, 577), ({"dwgn_small": 1}, 1, 449),
+    ({"dwgn_small": 1}, 3, 130), ({"dwgn_small": 1}, 1, 64), ({"dwgn_small": 1, "lnfold": 0}, 1, 250),
 ])
 def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     """Every GEMM main-loop / tile / pipeline variant behind flamed_tune computes the same velocity (vs the
     oracle, bf16 tolerance): register-staged vs LDS-DMA, 32- vs 64-wide small tiles, mid-M, large-M ring
     depth, depthwise T-chunk, the 256 x 256 8-phase tiles (B*T = 16,400) vs the 128 x 128 ring, and the
     large-M bf16 residual stream (x16), and the whole-utterance depthwise conv + GroupNorm kernel (dwgn:
-    1, 2, 3 and 8 frame chunks; T = 513 falls back to the chunked conv + GroupNorm pass)."""
+    1, 2, 3 and 8 frame chunks; T = 513 falls back to the chunked conv + GroupNorm pass) and its small-M
+    form (one workgroup per utterance x 8 channels, RPT = 1..9; T = 577 falls back)."""
     from flamed import _native as nat
     pg, sd = pg_bf16
     g = torch.Generator().manual_seed(B * 7 + T)
@@ -190,7 +193,7 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     ref = orc.denoiser_forward(sd, x, t, c)
     L = nat.lib()
     defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536, "dma_ns": 3, "lnfold": 1,
-                "g8p_rows": 16384, "x16": 0, "dwgn": 1}
+                "g8p_rows": 16384, "x16": 0, "dwgn": 1, "dwgn_small": 1}
     try:
         for k, v in knobs.items():
             nat.check(L.flamed_tune(k.encode(), v), "tune")

@@ -19,7 +19,7 @@ import yaml  # noqa: E402
 from flamed import _native as nat  # noqa: E402
 
 NAMES = {0: ("proj_in", ["prologue", "mainloop", "splitk", "epi+stats", ""]),
-         1: ("dwconv+gn", ["stats/vec/X loads", "LN+mod->LDS", "conv+D write", "partials", "gn finalize"]),
+         1: ("dwconv+gn", ["X/partials loads+LN stats", "LN+mod->LDS", "conv", "GN sums (2 passes)", "normalise+store"]),
          3: ("conv2(GN)", ["prologue", "mainloop", "splitk", "epi+stats", ""]),
          4: ("conv3 resid", ["prologue", "mainloop", "splitk", "epi+stats", ""]),
          5: ("mlp0(LN)", ["prologue", "mainloop", "splitk", "epi+stats", ""]),
