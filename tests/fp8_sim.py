@@ -20,17 +20,25 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from _common import seeded, orc  # noqa: E402  (checker only)
 
-NAMES = ["proj_in", "conv_2", "conv_3", "mlp.0", "mlp.2", "conv_out"]
+# FP8_SET=big4: only the four 1024x1024 GEMMs per block (conv_2, conv_3, mlp.0, mlp.2), what the HIP fp8
+# path quantizes; proj_in (K = 256) and conv_out stay bf16
+BIG4 = os.environ.get("FP8_SET", "") == "big4"
+NAMES = ["conv_2", "conv_3", "mlp.0", "mlp.2"] if BIG4 else ["proj_in", "conv_2", "conv_3", "mlp.0", "mlp.2", "conv_out"]
 E4M3 = torch.float8_e4m3fn
 
 
-def mx_q(x: torch.Tensor, dim: int) -> torch.Tensor:
-    """MX-fp8 fake-quantisation of x along `dim` (blocks of 32; the dim must be a multiple of 32)."""
+def mx_q(x: torch.Tensor, dim: int, ceil: bool = False) -> torch.Tensor:
+    """MX-fp8 fake-quantisation of x along `dim` (blocks of 32; the dim must be a multiple of 32).
+    floor (OCP MX spec): 2^(floor(log2 amax) - 8), the block maximum lands in [256, 512) and saturates at 448;
+    ceil (what the HIP kernels use): 2^ceil(log2(amax / 448)), no element saturates."""
     xt = x.movedim(dim, -1)
     shp = xt.shape
     b = xt.reshape(*shp[:-1], shp[-1] // 32, 32)
     amax = b.abs().amax(-1, keepdim=True)
-    e = torch.floor(torch.log2(amax.clamp_min(2.0 ** -126))) - 8
+    if ceil:
+        e = torch.ceil(torch.log2(amax.clamp_min(2.0 ** -126) / 448.0))
+    else:
+        e = torch.floor(torch.log2(amax.clamp_min(2.0 ** -126))) - 8
     s = torch.exp2(e)
     q = (b / s).clamp(-448, 448).to(E4M3).float() * s
     q = torch.where(amax > 0, q, torch.zeros_like(q))
@@ -40,8 +48,8 @@ def mx_q(x: torch.Tensor, dim: int) -> torch.Tensor:
 def quant_w(w, recipe):
     if recipe == "bf16":
         return w.to(torch.bfloat16).float()
-    if recipe == "mxfp8":
-        return mx_q(w, 1)  # (N, K[, taps]): blocks along the input-channel dim
+    if recipe.startswith("mxfp8"):
+        return mx_q(w, 1, recipe.endswith("c"))  # (N, K[, taps]): blocks along the input-channel dim
     s = w.reshape(w.shape[0], -1).abs().amax(1).clamp_min(1e-12) / 448.0
     shp = (-1,) + (1,) * (w.dim() - 1)
     return (w / s.view(shp)).to(E4M3).float() * s.view(shp)
@@ -50,8 +58,8 @@ def quant_w(w, recipe):
 def quant_a(a, recipe, dim):
     if recipe == "bf16":
         return a.to(torch.bfloat16).float()
-    if recipe == "mxfp8":
-        return mx_q(a, dim)
+    if recipe.startswith("mxfp8"):
+        return mx_q(a, dim, recipe.endswith("c"))
     return a.clamp(-448, 448).to(E4M3).float()
 
 
@@ -66,10 +74,11 @@ class Quantized:
         r = self.recipe
 
         def conv(x_, w, b=None, stride=1, padding=0, dilation=1, groups=1):
-            return self.conv0(quant_a(x_, r, 1) if groups == 1 else x_, w, b, stride, padding, dilation, groups)
+            q = groups == 1 and (w.shape[-1] == 1 or not BIG4)
+            return self.conv0(quant_a(x_, r, 1) if q else x_, w, b, stride, padding, dilation, groups)
 
         def lin(sd_, p, x_):
-            q = any(p.endswith(n) for n in ("proj_in", "mlp.0", "mlp.2"))
+            q = any(p.endswith(n) for n in (("mlp.0", "mlp.2") if BIG4 else ("proj_in", "mlp.0", "mlp.2")))
             return self.lin0(sd_, p, quant_a(x_, r, -1) if q else x_)
         orc.F.conv1d, orc._lin = conv, lin
         return self
@@ -96,7 +105,7 @@ def main():
     c = torch.randn(1, 256, generator=g)
     refs_v = {tv: orc.denoiser_forward(sd, x0, torch.tensor([[tv]]), c) for tv in (0.1, 0.5, 0.9)}
     refs_s = {n: orc.euler_solve(sd, x0, c, n) for n in (128, 256)}
-    for recipe in ("bf16", "mxfp8", "fp8-chan"):
+    for recipe in os.environ.get("FP8_RECIPES", "bf16,mxfp8,mxfp8c,fp8-chan").split(","):
         sdq = quantized_sd(sd, recipe)
         with Quantized(recipe):
             ev = [rel(orc.denoiser_forward(sdq, x0, torch.tensor([[tv]]), c), r) for tv, r in refs_v.items()]

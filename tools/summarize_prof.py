@@ -18,9 +18,9 @@ from collections import defaultdict
 
 CLASSES = [
     ("proj_in_gemm", [r"LoadF32.*EpiBiasStatsT", r"LoadF32I.*EpiBiasStatsT"]),
-    ("lnmod_dwconv_gnpartials", [r"dwconv_stats_kernel"]),
+    ("lnmod_dwconv_gnpartials", [r"dwconv_stats_kernel", r"dwgn_small_kernel", r"dwgn_kernel"]),
     ("gn_finalize", [r"gn_finalize_kernel"]),
-    ("gnapply_conv2_gemm_gelu", [r"LoadGN"]),
+    ("gnapply_conv2_gemm_gelu", [r"LoadGN", r"EpiBiasActIDF16bLi1E", r"EpiBiasAct<bf16, 1>"]),
     ("conv3_gemm_gated_resid", [r"EpiConvNeXtResid"]),
     ("lnmod_mlp0_gemm_silu", [r"LoadLNMod<[^>]*true>", r"LoadLNModI\w+Lb1E", r"EpiLNFold<[^>]*bf16", r"EpiLNFoldIDF16b"]),
     ("mlp2_gemm_gated_resid", [r"EpiGatedResid"]),
