@@ -27,6 +27,7 @@ import torch.nn as nn
 from torch.nn.utils import weight_norm
 
 from flamed import _native as nat
+from flamed import ops
 from .alias_free_torch import Activation1d
 from .quantize import ResidualVQ
 from .transformer import TransformerEncoder
@@ -165,7 +166,7 @@ class FACodecEncoder(nn.Module):
         if self._use_hip(x):
             if self._hip is None or self._hip.dtype_name != self.hip_dtype:
                 self._hip = EncoderHIP(self, self.hip_dtype)
-            return self._hip.encode(x)
+            return ops.enc_encode(self._hip.oid, x)
         return self.block(x)
 
     def inference(self, x):
@@ -304,7 +305,7 @@ class FACodecDecoder(nn.Module):
         if self._use_hip(x):
             if self._hip is None or self._hip.dtype_name != self.hip_dtype:
                 self._hip = FacDecoderHIP(self, self.hip_dtype)
-            return self._hip.decode(x, speaker_embedding)
+            return ops.fac_decode(self._hip.oid, x, speaker_embedding)
         gamma, beta = self.timbre_linear(speaker_embedding).unsqueeze(2).chunk(2, 1)
         h = self.timbre_norm(x.transpose(1, 2)).transpose(1, 2)
         return self.model(h * gamma + beta)
@@ -343,6 +344,7 @@ class FacDecoderHIP:
         self._keep = []
         self.ws = nat.Workspace()
         self._bufs = {}
+        self.oid = ops.register(self)  # torch.ops.flamed_hip.fac_decode / enc_encode
 
     def __del__(self):
         try:
@@ -425,6 +427,7 @@ class EncoderHIP:
         self._keep = []
         self.ws = nat.Workspace()
         self._bufs = {}
+        self.oid = ops.register(self)  # torch.ops.flamed_hip.fac_decode / enc_encode
 
     def __del__(self):
         try:
@@ -433,24 +436,32 @@ class EncoderHIP:
         except Exception:
             pass
 
+    def _ensure_created(self):
+        if self.handle is None:
+            h = ctypes.c_void_p()
+            ups = (ctypes.c_int * len(self.enc.up_ratios))(*self.enc.up_ratios)
+            nat.check(nat.lib().flamed_enc_create(self.enc.ngf, len(self.enc.up_ratios), ups, self.enc.out_channels,
+                                                  nat.dtype_code(self.dtype_name), ctypes.byref(h)), "flamed_enc_create")
+            self.handle = h
+
     def _ensure(self, dev):
         params = enc_weight_list(self.enc)
         sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(dev),)
         if sig == self._sig:
             return
         L = nat.lib()
-        if self.handle is None:
-            h = ctypes.c_void_p()
-            ups = (ctypes.c_int * len(self.enc.up_ratios))(*self.enc.up_ratios)
-            nat.check(L.flamed_enc_create(self.enc.ngf, len(self.enc.up_ratios), ups, self.enc.out_channels,
-                                          nat.dtype_code(self.dtype_name), ctypes.byref(h)), "flamed_enc_create")
-            self.handle = h
+        self._ensure_created()
         keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
         arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
         nat.check(L.flamed_enc_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_enc_load")
         self._keep = keep
         self._sig = sig
         self._bufs = {}
+
+    def out_len(self, n: int) -> int:
+        """Frames the encoder produces from n samples (the strided conv chain; needs the handle)."""
+        self._ensure_created()
+        return int(nat.lib().flamed_enc_out_len(self.handle, n))
 
     def encode(self, x):
         if x.dim() != 3 or x.shape[1] != 1:

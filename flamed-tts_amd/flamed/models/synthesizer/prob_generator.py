@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from flamed import _native as nat
+from flamed import ops
 from flamed.utils.conv import GemmConv1d
 
 
@@ -248,7 +249,7 @@ class SimpleMLPAdaLN(nn.Module):
 
     def forward(self, x, t, c):
         if self._use_hip(x):
-            return self.hip().velocity(x, t, c)
+            return ops.den_velocity(self.hip().oid, x, t, c)
         y = self.time_embed(t) + self.cond_embed(c).unsqueeze(1)
         h = self.proj_in(x)
         for blk in self.res_blocks:
@@ -290,7 +291,7 @@ class ProbGenerator(nn.Module):
         if self._cond_hip_ok(cond):
             if self._cond_hip is None or self._cond_hip.dtype_name != self.cond_hip_dtype:
                 self._cond_hip = CondFoldHIP(self, self.cond_hip_dtype)
-            return self._cond_hip.fold(cond, mask)
+            return ops.cond_fold(self._cond_hip.oid, cond, mask)
         return self.cond_downsampling(self.quantizer_encoding(cond), mask)
 
     def _load_from_state_dict(self, *args, **kwargs):
@@ -318,7 +319,7 @@ class ProbGenerator(nn.Module):
         ts = torch.linspace(0, 1, nfe + 1, device=cond.device)
         xt = torch.randn((b, l, self.target_dim)).to(cond.device) * temperature + cond
         if self.denoiser._use_hip(xt):
-            xt = self.denoiser.hip().solve(xt, ts, spk, nfe)
+            xt = ops.den_solve(self.denoiser.hip().oid, xt, ts, spk, nfe)
         else:
             delta_t = 1 / nfe
             for i in range(1, len(ts)):
@@ -359,6 +360,7 @@ class DenoiserHIP:
         self.ws = nat.Workspace()
         self.ada_ws = nat.Workspace()
         self._solve_bufs = {}
+        self.oid = ops.register(self)  # torch.ops.flamed_hip.den_* carry this id
 
     def __del__(self):
         try:
@@ -484,6 +486,7 @@ class CondFoldHIP:
         self.handle = None
         self._sig = None
         self.ws = nat.Workspace()
+        self.oid = ops.register(self)  # torch.ops.flamed_hip.cond_fold
 
     def __del__(self):
         try:

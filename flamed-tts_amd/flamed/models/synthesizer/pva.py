@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from flamed import _native as nat
+from flamed import ops
 from flamed.utils.tools import pad
 
 
@@ -144,6 +145,11 @@ class LengthRegulator(nn.Module):
 
 
 def hip_length_regulate(x, phone, sil, src_lens, max_len, log_domain=False):
+    """torch.ops.flamed_hip.length_regulate (max_len None/0 = the batch's longest utterance)."""
+    return ops.length_regulate(x, phone, sil, src_lens, int(max_len) if max_len else 0, bool(log_domain))
+
+
+def hip_length_regulate_impl(x, phone, sil, src_lens, max_len, log_domain=False):
     """HIP length regulator: phase 1 (repeats + prefix sums), one host read of the lengths (the
     reference's .tolist() sync, pva.py:158), phase 2 (gather)."""
     L_ = nat.lib()
@@ -199,7 +205,7 @@ class PVA(nn.Module):
         dur_t = torch.randn((b, l)).to(x.device) * temperature
         sil_t = torch.randn((b, l)).to(x.device) * temperature
         if _hip_ok(x, self):
-            return self.hip().flow(x, src_mask, dur_t, sil_t, ts, nfe)
+            return ops.pva_flow(self.hip().oid, x, src_mask, dur_t, sil_t, ts, nfe)
         delta_t = 1 / nfe
         for i in range(1, len(ts)):
             dur_t = dur_t + delta_t * self.duration_generator(dur_t, x, ts[i - 1], src_mask)
@@ -241,6 +247,7 @@ class PvaHIP:
         self._keep = []
         self.ws = nat.Workspace()
         self._bufs = {}
+        self.oid = ops.register(self)  # torch.ops.flamed_hip.pva_flow
 
     def __del__(self):
         try:

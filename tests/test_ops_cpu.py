@@ -1,0 +1,72 @@
+"""torch.library layer (flamed/ops.py): every HIP entry point the modules dispatch to is a
+registered `flamed_hip::*` custom op with a schema and a fake (meta) implementation, so FakeTensor shape
+propagation and torch.compile tracing see them.  CPU only: no op body runs here."""
+import types
+
+import pytest
+import torch
+from torch._subclasses.fake_tensor import FakeTensorMode
+from torch.fx.experimental.symbolic_shapes import ShapeEnv
+
+import _common  # noqa: F401  (sys.path)
+from flamed import ops
+
+
+def test_every_op_is_registered_with_a_schema():
+    for name in ops.OPS:
+        op = getattr(torch.ops.flamed_hip, name)
+        schema = str(op.default._schema)
+        assert schema.startswith(f"flamed_hip::{name}("), schema
+
+
+def test_modules_dispatch_through_the_ops():
+    import inspect
+    from flamed.models.synthesizer import prob_generator, pva
+    from flamed.models.facodec import facodec
+    src = inspect.getsource(prob_generator) + inspect.getsource(pva) + inspect.getsource(facodec)
+    for name in ops.OPS:
+        assert f"ops.{name}(" in src, name
+
+
+class _Owner:  # weak-referenceable stand-in for a HIP owner object
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def _dummy_owner(**kw):
+    o = _Owner(**kw)
+    return o, ops.register(o)
+
+
+def test_fake_shapes():
+    pg, pid = _dummy_owner(pg=types.SimpleNamespace(target_dim=256))
+    dec, did = _dummy_owner(dec=types.SimpleNamespace(hop_length=200))
+    enc, eid = _dummy_owner(enc=types.SimpleNamespace(out_channels=256), out_len=lambda n: n // 200)
+    with FakeTensorMode(shape_env=ShapeEnv()):
+        x = torch.empty(2, 50, 256)
+        v = torch.ops.flamed_hip.den_velocity(1, x, torch.empty(1, 1), torch.empty(2, 256))
+        assert v.shape == (2, 50, 256) and v.dtype == torch.float32
+        s = torch.ops.flamed_hip.den_solve(1, x, torch.empty(129), torch.empty(2, 256), 128)
+        assert s.shape == (2, 50, 256)
+        c = torch.ops.flamed_hip.cond_fold(pid, torch.empty(2, 4, 50, 64), torch.empty(2, 50, 1, dtype=torch.bool))
+        assert c.shape == (2, 50, 256)
+        d, si = torch.ops.flamed_hip.pva_flow(1, torch.empty(2, 9, 256), torch.empty(2, 9, dtype=torch.bool),
+                                              torch.empty(2, 9), torch.empty(2, 9), torch.empty(33), 32)
+        assert d.shape == (2, 9) and si.shape == (2, 9)
+        out, tl = torch.ops.flamed_hip.length_regulate(torch.empty(2, 9, 256), torch.empty(2, 9), torch.empty(2, 9),
+                                                       torch.empty(2, dtype=torch.int64), 40, False)
+        assert out.shape == (2, 40, 256) and tl.shape == (2,) and tl.dtype == torch.int64
+        out, _ = torch.ops.flamed_hip.length_regulate(torch.empty(2, 9, 256), torch.empty(2, 9), torch.empty(2, 9),
+                                                      torch.empty(2, dtype=torch.int64), 0, True)
+        assert isinstance(out.shape[1], torch.SymInt)  # data-dependent length (the reference's .tolist())
+        w = torch.ops.flamed_hip.fac_decode(did, torch.empty(1, 256, 40), torch.empty(1, 256))
+        assert w.shape == (1, 1, 8000)
+        e = torch.ops.flamed_hip.enc_encode(eid, torch.empty(1, 1, 48000))
+        assert e.shape == (1, 256, 240)
+
+
+def test_dead_owner_raises():
+    o, oid = _dummy_owner()
+    del o
+    with pytest.raises(RuntimeError, match="no live HIP owner"):
+        ops.owner(oid)
