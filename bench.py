@@ -270,24 +270,39 @@ def secondary_measurements(dev, nfe):
 
 
 def long_form(pg, dev, args, C, T=2400, nfe=256):
-    """BASELINE configs[4] shape at bf16: 30 s utterances (2400 frames), nsteps-denoiser=256, B = 1 and 16
-    (the fp8 projections of that config are not built)."""
+    """BASELINE configs[4]: 30 s utterances (2400 frames), nsteps-denoiser=256, B = 1 and 16, on the bench's
+    handle (bf16) and on an fp8 handle (MX-fp8 conv_2/conv_3/mlp.0/mlp.2 on the large-M path, which B = 16
+    (38,400 rows) takes and B = 1 (2,400 rows) does not: there the fp8 handle computes in bf16).  The fp8
+    row also reports the rel-L2 between its solve and the bf16 one (same inputs)."""
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
     hip = pg.denoiser.hip()
-    out = {"frames": T, "nfe": nfe, "dtype": args.dtype, "note": "bf16 GEMM operands (fp8 not built)"}
+    hip8 = DenoiserHIP(pg.denoiser, "fp8")
+    out = {"frames": T, "nfe": nfe, "dtype": args.dtype}
     ts = torch.linspace(0, 1, nfe + 1, device=dev)
+    fp8 = {"dtype": "mx-fp8 e4m3 (pointwise H x H GEMMs, B*T >= 16384 rows) + bf16",
+           "note": "OCP MX: e8m0 scale per 32 input channels of weights and activations, scale = 2^ceil(log2(amax/448))"}
     for B in (1, 16):
         g = torch.Generator().manual_seed(args.seed + 2)
         x0 = (torch.randn(B, T, C, generator=g) * 0.3 + torch.randn(B, T, C, generator=g)).to(dev)
         spk = torch.randn(B, C, generator=g).to(dev)
-        with torch.inference_mode():
-            hip.solve(x0, ts, spk, nfe)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            hip.solve(x0, ts, spk, nfe)
-            torch.cuda.synchronize()
-            sec = time.perf_counter() - t0
-        out[f"B{B}"] = {"ms_per_solve": round(sec * 1e3, 3), "latent_frames_per_s": round(B * T / sec, 1),
-                        "rtf_denoiser": round(sec / (B * T * 200 / 16000.0), 6)}
+        sols = {}
+        for name, h in (("bf16", hip), ("fp8", hip8)):
+            with torch.inference_mode():
+                h.solve(x0, ts, spk, nfe)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sols[name] = h.solve(x0, ts, spk, nfe)
+                torch.cuda.synchronize()
+                sec = time.perf_counter() - t0
+            row = {"ms_per_solve": round(sec * 1e3, 3), "latent_frames_per_s": round(B * T / sec, 1),
+                   "rtf_denoiser": round(sec / (B * T * 200 / 16000.0), 6)}
+            if name == "bf16":
+                out[f"B{B}"] = row
+            else:
+                row["fp8_active"] = B * T >= 16384
+                row["rel_l2_vs_bf16"] = float((sols["fp8"] - sols["bf16"]).norm() / sols["bf16"].norm())
+                fp8[f"B{B}"] = row
+    out["fp8"] = fp8
     return out
 
 

@@ -1307,6 +1307,110 @@ __global__ __launch_bounds__(256) void lnmod_apply_bf16_kernel(LoadLNMod<bf16, A
   }
 }
 
+// ---- MX-fp8 operands (fp8 handles, large M; gemm_8p.hpp): the same normalise passes writing e4m3 rows +
+// the scale image.  A thread's 8 consecutive columns; the 4 lanes of one 32-column block combine their
+// maxima with two shuffles (lane groups of 4 are 32-column aligned: K / 8 = 128 lanes per row).
+__device__ __forceinline__ void store_f8x8(const float* o, unsigned char* dst, unsigned char* sc, int m, int k, int K) {
+  float am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(o[j]));
+  am = fmaxf(am, __shfl_xor(am, 1));
+  am = fmaxf(am, __shfl_xor(am, 2));
+  const int e = mx_exp(am);
+  const float inv = mx_inv(e);
+  const uint2 q = make_uint2(pack4_fp8(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv),
+                             pack4_fp8(o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv));
+  *reinterpret_cast<uint2*>(dst + (size_t)m * K + k) = q;
+  if ((k & 31) == 0) sc[mx_a_index(m, k >> 5, K)] = (unsigned char)(e + 127);
+}
+
+template <typename DS>
+__global__ void gn_apply_f8_kernel(LoadGN<bf16> al, const DS* src, unsigned char* dst, unsigned char* sc, int M) {
+  const int H = al.H, K8 = H / 8;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)M * K8) return;  // M * K8 is a multiple of 64: whole waves leave
+  const int m = i / K8, k = (int)(i - (size_t)m * K8) * 8;
+  float xv[8];
+  ldx8<DS>(src + (size_t)m * H + k, xv);
+  const float* g = al.gns + ((size_t)(m / al.T) * H + k) * 2;
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (xv[j] - g[2 * j]) * (g[2 * j + 1] * al.gnw[k + j]) + al.gnb[k + j];
+  store_f8x8(o, dst, sc, m, k, H);
+}
+
+template <bool AFF, typename XT>
+__global__ __launch_bounds__(256) void lnmod_apply_f8_kernel(LoadLNMod<bf16, AFF> al, const XT* xs, unsigned char* dst,
+                                                             unsigned char* sc, int M) {
+  __shared__ float st[2][2];
+  const int r = threadIdx.x >> 7, lt = threadIdx.x & 127;
+  const int m = blockIdx.x * 2 + r;
+  if (lt == 0 && m < M) row_stats_from_partials(al.S, m, al.NT, al.tw, al.eps, st[r][0], st[r][1]);
+  __syncthreads();
+  if (m >= M) return;  // a whole 128-lane row half-block (two waves) leaves together
+  const float mean = st[r][0], rstd = st[r][1];
+  const ModRef md = al.mod.at();
+  const size_t mo = (size_t)(m / md.div) * md.ms;
+  const int K = al.kdim;
+  for (int k = lt * 8; k < K; k += 128 * 8) {
+    float xv[8], o[8];
+    ldx8<XT>(xs + (size_t)m * al.ld + k, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s1 = 1.0f + md.sc[mo + k + j];
+      const float wv = AFF ? al.lnw[k + j] : 1.0f, bv = AFF ? al.lnb[k + j] : 0.0f;
+      o[j] = ((xv[j] - mean) * rstd) * (wv * s1) + (bv * s1 + md.sh[mo + k + j]);
+    }
+    store_f8x8(o, dst, sc, m, k, K);
+  }
+}
+
+static int f8_prep(const LoadGN<bf16>& al, int M, unsigned char* a8, unsigned char* s8, hipStream_t st) {
+  const size_t n = (size_t)M * (al.H / 8);
+  if (al.D16)
+    hipLaunchKernelGGL(gn_apply_f8_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, st, al, al.D16, a8, s8, M);
+  else
+    hipLaunchKernelGGL(gn_apply_f8_kernel<float>, dim3((n + 255) / 256), dim3(256), 0, st, al, al.D, a8, s8, M);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+template <bool AFF>
+static int f8_prep(const LoadLNMod<bf16, AFF>& al, int M, unsigned char* a8, unsigned char* s8, hipStream_t st) {
+  FL_REQUIRE(al.kdim % 1024 == 0, "f8_prep(LN): K=%d", al.kdim);
+  if (al.x16)
+    hipLaunchKernelGGL((lnmod_apply_f8_kernel<AFF, bf16>), dim3((M + 1) / 2), dim3(256), 0, st, al, al.x16, a8, s8, M);
+  else
+    hipLaunchKernelGGL((lnmod_apply_f8_kernel<AFF, float>), dim3((M + 1) / 2), dim3(256), 0, st, al, al.x, a8, s8, M);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+// fp32 weight W[N][K] -> e4m3 rows + the W scale image (mx_b_index): one thread per (row, 32-block).
+__global__ void quant_w_f8_kernel(const float* __restrict__ src, int N, int K, unsigned char* __restrict__ dst,
+                                  unsigned char* __restrict__ sc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, KB = K / 32;
+  if (i >= N * KB) return;
+  const int n = i / KB, kb = i - n * KB;
+  const float* p = src + (size_t)n * K + kb * 32;
+  float v[32], am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; j += 4) {
+    const float4 f = ld4(p + j);
+    v[j] = f.x; v[j + 1] = f.y; v[j + 2] = f.z; v[j + 3] = f.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 32; ++j) am = fmaxf(am, fabsf(v[j]));
+  const int e = mx_exp(am);
+  const float inv = mx_inv(e);
+  unsigned q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = pack4_fp8(v[4 * j] * inv, v[4 * j + 1] * inv, v[4 * j + 2] * inv, v[4 * j + 3] * inv);
+  u32x4* d = reinterpret_cast<u32x4*>(dst + (size_t)n * K + kb * 32);
+  d[0] = u32x4{q[0], q[1], q[2], q[3]};
+  d[1] = u32x4{q[4], q[5], q[6], q[7]};
+  sc[mx_b_index(n, kb, K)] = (unsigned char)(e + 127);
+}
+
 static int big_prep(const LoadF32<bf16>& al, int M, int K, bf16* a16, hipStream_t st) {
   const size_t n = (size_t)M * (K / 8);
   hipLaunchKernelGGL(cast_bf16x8_kernel, dim3((n + 255) / 256), dim3(256), 0, st, al.p, al.ld, a16, M, K);
@@ -1391,11 +1495,15 @@ static int den_gemm(GemmCfg c, bool wide_a, const AL& al, const DT* W, int ldw, 
 
 struct DenBlockW {
   const void* w2; const void* w3; const void* m0; const void* m2;  // DT (H x H)
+  // fp8 handles: e4m3 copies + W scale images of w2, w3, m0, m2 (the final layer: w2, w3)
+  const unsigned char* q[4] = {nullptr, nullptr, nullptr, nullptr};
+  const unsigned char* qs[4] = {nullptr, nullptr, nullptr, nullptr};
   const float *b2, *b3, *mb0, *mb2, *lnw, *lnb, *lnmw, *lnmb, *dww, *dwb, *gnw, *gnb;
 };
 
 struct Den {
-  int C, H, NB, KS, S, dt;  // dt: 0 f32, 1 bf16
+  int C, H, NB, KS, S, dt;  // dt: 0 f32, 1 bf16 (also for fp8 handles)
+  bool f8 = false;          // FLAMED_FP8 handle: bf16 everywhere + MX-fp8 conv_2/conv_3/mlp.0/mlp.2 at large M
   int MS;                   // mods row stride: MS0 modulation floats + the LayerNorm-fold tables (bf16)
   int MS0;                  // (6 NB + 5) H: shift/scale/gate vectors of every adaLN_modulation
   int fold = 0;             // row holds fold tables [wa, wb] per LN-consuming GEMM (mlp.0 x NB, conv_out)
@@ -1531,9 +1639,14 @@ FLAMED_API int flamed_den_create(int C, int H, int n_blocks, int kernel, int spk
   FL_REQUIRE(C > 0 && C % 64 == 0 && H % 256 == 0 && H <= 1024 && n_blocks >= 1 && spk_dim % 64 == 0,
              "flamed_den_create: unsupported dims C=%d H=%d S=%d", C, H, spk_dim);
   FL_REQUIRE(kernel == 31, "flamed_den_create: only convnext kernel_size=31 is specialised (got %d)", kernel);
-  FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16, "flamed_den_create: dtype must be FLAMED_F32 or FLAMED_BF16");
+  FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16 || dtype == FLAMED_FP8,
+             "flamed_den_create: dtype must be FLAMED_F32, FLAMED_BF16 or FLAMED_FP8");
+  FL_REQUIRE(dtype != FLAMED_FP8 || (H % 256 == 0 && H <= kMxMaxK), "flamed_den_create: fp8 needs H %% 256 == 0, H <= %d", kMxMaxK);
   Den* d = new Den();
-  d->C = C; d->H = H; d->NB = n_blocks; d->KS = kernel; d->S = spk_dim; d->dt = dtype;
+  d->C = C; d->H = H; d->NB = n_blocks; d->KS = kernel; d->S = spk_dim;
+  d->dt = dtype == FLAMED_FP8 ? FLAMED_BF16 : dtype;
+  d->f8 = dtype == FLAMED_FP8;
+  dtype = d->dt;
   d->MS0 = (6 * n_blocks + 5) * H;
   d->fold = dtype == FLAMED_BF16;
   d->MS = d->MS0 + (d->fold ? n_blocks * 2 * H + 2 * 3 * C : 0);
@@ -1619,6 +1732,8 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   for (int i = 0; i <= NB; ++i) o_dw[i] = take(4ull * KS * H);
   const size_t n_vec = 1 + 11ull * NB + 5;  // H-wide vectors: proj_in bias, 11 per block, 5 final
   const size_t o_vec = take(4ull * (n_vec * H + C));
+  const size_t q_bytes = (size_t)H * H + mx_scale_bytes(H, H);  // one fp8 matrix + its scale image
+  const size_t o_q = d->f8 ? take(q_bytes * (4ull * NB + 2)) : 0;
   if (d->dev) { FL_HIP(hipFree(d->dev)); d->dev = nullptr; }
   FL_HIP(hipMalloc(&d->dev, off));
   d->dev_bytes = off;
@@ -1626,6 +1741,16 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   auto cpy = [&](size_t o, const float* src, size_t n) -> int {
     hipLaunchKernelGGL(copy_kernel_f32, dim3((n + 255) / 256), dim3(256), 0, st, src, reinterpret_cast<float*>(base + o), n);
     FL_LAUNCH_CHECK();
+    return kOk;
+  };
+  auto quant = [&](int slot, const float* src, const unsigned char** q, const unsigned char** qs) -> int {
+    if (!d->f8) return kOk;
+    unsigned char* p = reinterpret_cast<unsigned char*>(base + o_q + (size_t)slot * q_bytes);
+    const int nb = H * (H / 32);
+    hipLaunchKernelGGL(quant_w_f8_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, src, H, H, p, p + (size_t)H * H);
+    FL_LAUNCH_CHECK();
+    *q = p;
+    *qs = p + (size_t)H * H;
     return kOk;
   };
   auto cast = [&](size_t o, const float* src, size_t n) -> int {
@@ -1665,6 +1790,8 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     TRY(cast(ob + 2 * es * H * H, bw[14], (size_t)H * H));
     TRY(cast(ob + 3 * es * H * H, bw[16], (size_t)H * H));
     B.w2 = base + ob; B.w3 = base + ob + es * H * H; B.m0 = base + ob + 2 * es * H * H; B.m2 = base + ob + 3 * es * H * H;
+    TRY(quant(4 * i + 0, bw[8], &B.q[0], &B.qs[0])); TRY(quant(4 * i + 1, bw[10], &B.q[1], &B.qs[1]));
+    TRY(quant(4 * i + 2, bw[14], &B.q[2], &B.qs[2])); TRY(quant(4 * i + 3, bw[16], &B.q[3], &B.qs[3]));
     hipLaunchKernelGGL(taps_t_kernel, dim3((H * KS + 255) / 256), dim3(256), 0, st, bw[4], reinterpret_cast<float*>(base + o_dw[i]), H, KS);
     FL_LAUNCH_CHECK();
     B.dww = reinterpret_cast<float*>(base + o_dw[i]);
@@ -1684,6 +1811,7 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     TRY(cast(o_fin, fw[6], (size_t)H * H)); TRY(vec(fw[7], H, &F.b2));
     TRY(cast(o_fin + es * H * H, fw[8], (size_t)H * H)); TRY(vec(fw[9], H, &F.b3));
     F.w2 = base + o_fin; F.w3 = base + o_fin + es * H * H;
+    TRY(quant(4 * NB + 0, fw[6], &F.q[0], &F.qs[0])); TRY(quant(4 * NB + 1, fw[8], &F.q[1], &F.qs[1]));
     size_t n = (size_t)C * H * 3;
     if (d->dt == FLAMED_BF16)
       hipLaunchKernelGGL(stack_taps_kernel<bf16>, dim3((n + 255) / 256), dim3(256), 0, st, fw[10], reinterpret_cast<bf16*>(base + o_out), C, H, 3);
@@ -1801,9 +1929,17 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   XT* Dx = reinterpret_cast<XT*>(w.D);
   const bf16* X16p = X16 ? reinterpret_cast<const bf16*>(w.X) : nullptr;
   const bf16* D16p = X16 ? reinterpret_cast<const bf16*>(w.D) : nullptr;
-  const bool fold = std::is_same<DT, bf16>::value && d->fold && tu.lnfold && w.XA && (!big || M >= tu.fold_big_rows);
+  // fp8 handle at large M: MX-fp8 conv_2 / conv_3 / mlp.0 / mlp.2 on the 256 x 256 tiles, their A operands
+  // written as e4m3 + scales by the normalise passes and by the conv_2 / mlp.0 epilogues (no LayerNorm
+  // fold, no dwgn: their producers write bf16)
+  const bool f8 = std::is_same<DT, bf16>::value && d->f8 && big && tu.g8p_rows > 0 && M >= tu.g8p_rows;
+  const bool fold = std::is_same<DT, bf16>::value && d->fold && tu.lnfold && w.XA && (!big || M >= tu.fold_big_rows) && !f8;
   // whole-utterance depthwise conv + GroupNorm (launch_dwgn): large M, one modulation row per utterance
-  const bool dwgn = big && tu.dwgn && T <= kDgMaxT && mod_div % T == 0 && H % 64 == 0;
+  const bool dwgn = big && tu.dwgn && T <= kDgMaxT && mod_div % T == 0 && H % 64 == 0 && !f8;
+  unsigned char* const A8 = reinterpret_cast<unsigned char*>(w.A16);  // fp8 operands: e4m3 rows, then scales
+  unsigned char* const A8s = f8 ? A8 + (size_t)M * H : nullptr;
+  unsigned char* const U8 = reinterpret_cast<unsigned char*>(w.U);
+  unsigned char* const U8s = f8 ? U8 + (size_t)M * H : nullptr;
   // small M (bf16): the same sub-block in one workgroup per (utterance, 8 channels), bf16 operand in D's space
   const bool dwgn_s = std::is_same<DT, bf16>::value && !big && !X16 && tu.dwgn_small && T <= kDgSmallMaxT && mod_div % T == 0;
   bf16* const As = reinterpret_cast<bf16*>(w.D);
@@ -1816,6 +1952,20 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     const float* md = mods + (size_t)i * 6 * H;
     ModRef mc{md, md + H, MS, mod_div, so};
     ModRef mm{md + 3 * H, md + 4 * H, MS, mod_div, so};
+    if (f8) {
+      K_(1, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
+      K_(2, (launch_dwconv_stats<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
+      K_(3, f8_prep(LoadGN<bf16>{w.D, H, w.GNS, Bw.gnw, Bw.gnb, T, D16p}, M, A8, A8s, st));
+      K_(3, launch_gemm8p_f8(A8, A8s, H, Bw.q[0], Bw.qs[0], H, EpiBiasActF8<1>{Bw.b2, U8, U8s, H}, M, H, H, st));
+      K_(4, launch_gemm8p_f8(U8, U8s, H, Bw.q[1], Bw.qs[1], H,
+                             EpiConvNeXtResid<true, XT>{Bw.b3, X, H, w.S0, NT, BN, 1e-6f, mc, md + 2 * H, Bw.lnw, Bw.lnb, w.S1, NT},
+                             M, H, H, st));
+      K_(5, f8_prep(LoadLNMod<bf16, true>{w.X, H, w.S1, NT, BN, 1e-6f, mm, Bw.lnmw, Bw.lnmb, H, X16p}, M, A8, A8s, st));
+      K_(5, launch_gemm8p_f8(A8, A8s, H, Bw.q[2], Bw.qs[2], H, EpiBiasActF8<2>{Bw.mb0, U8, U8s, H}, M, H, H, st));
+      K_(6, launch_gemm8p_f8(U8, U8s, H, Bw.q[3], Bw.qs[3], H,
+                             EpiGatedResidT<XT>{Bw.mb2, X, H, md + 5 * H, MS, mod_div, w.S0, NT, so}, M, H, H, st));
+      continue;
+    }
     if (dwgn) {  // large M: conv + GroupNorm in one kernel, conv_2 on the normalised bf16 rows
       K_(1, (launch_dwgn<true, XT>(X, H, w.S0, NT, BN, mc, Bw.lnw, Bw.lnb, Bw.dww, Bw.dwb, Bw.gnw, Bw.gnb, w.A16, B, T, st)));
       K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.A16, H}, (const DT*)Bw.w2, H, EpiBiasAct<DT, 1>{Bw.b2, U, H}, M, H, H, st)));
@@ -1850,7 +2000,12 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   ModRef mc{mf, mf + H, MS, mod_div, so};
   ModRef mo{mf + 3 * H, mf + 4 * H, MS, mod_div, so};
   const DenBlockW& F = d->fin;
-  if (dwgn) {
+  if (f8) {
+    K_(1, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 1, gcnt)));
+    K_(2, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
+    K_(3, f8_prep(LoadGN<bf16>{w.D, H, w.GNS, F.gnw, F.gnb, T, D16p}, M, A8, A8s, st));
+    K_(3, launch_gemm8p_f8(A8, A8s, H, F.q[0], F.qs[0], H, EpiBiasActF8<1>{F.b2, U8, U8s, H}, M, H, H, st));
+  } else if (dwgn) {
     K_(1, (launch_dwgn<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, F.gnw, F.gnb, w.A16, B, T, st)));
     K_(3, (den_gemm<DT>(cfg, false, LoadPlain<DT>{(const DT*)w.A16, H}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   } else if (dwgn_s) {
@@ -1861,7 +2016,13 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     K_(2, (launch_dwconv_stats<false, XT>(X, H, w.S0, NT, BN, mc, nullptr, nullptr, F.dww, F.dwb, Dx, w.GP, w.GNS, B, T, st, 2, gcnt)));
     K_(3, (den_gemm<DT>(cfg, true, LoadGN<DT>{w.D, H, w.GNS, F.gnw, F.gnb, T, D16p}, (const DT*)F.w2, H, EpiBiasAct<DT, 1>{F.b2, U, H}, M, H, H, st)));
   }
-  if (fold) {
+  if (f8) {
+    K_(4, launch_gemm8p_f8(U8, U8s, H, F.q[1], F.qs[1], H,
+                           EpiConvNeXtResid<false, XT>{F.b3, X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT},
+                           M, H, H, st));
+    K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H, X16p}, (const DT*)d->wout, H,
+                                        EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
+  } else if (fold) {
     K_(4, (den_gemm<DT>(cfg, false, LoadPlain<DT>{U, H}, (const DT*)F.w3, H,
                                         EpiConvNeXtResid<false, XT>{F.b3, X, H, w.S0, NT, BN, 1e-6f, mc, mf + 2 * H, nullptr, nullptr, w.S1, NT,
                                                                 w.XA, nullptr, mf + 4 * H},

@@ -23,6 +23,19 @@
 // tile that must have landed (2 per later half-tile; fewer in the last iteration, when nothing follows).
 // Epilogue: the accumulators go through an fp32 LDS image of 256 x 128 (one column half at a time), read
 // back row-vectorised (16-B residual loads/stores, LayerNorm row partials of 128 columns over a half-wave).
+//
+// MX-fp8 variant (F8 = true; BASELINE configs[4] "fp8 pointwise projections"): A and W are OCP e4m3 bytes
+// with one e8m0 scale per 32-element K block of every row (both operands), and each quadrant runs 8
+// v_mfma_scale_f32_16x16x128_f8f6f4 (2x the K of the bf16 form per MFMA, twice its cycles: 2x bf16 per
+// clock).  A K-tile is 128 elements = the same 128-B rows, so the DMA ring, the swizzle and the fragment
+// reads are byte-for-byte the bf16 ones.  Lane group g (lanes 16 g .. 16 g + 15) reads chunks g and 4 + g
+// of its row — instruction K [16 g, +16) in VGPRs 0-3, [64 + 16 g, +16) in VGPRs 4-7 (measured,
+// tools/probe_mx.py) — and passes the scale of K block g, which the hardware applies to instruction K
+// [32 g, 32 g + 32) = memory bytes [32 g, 32 g + 32) of the K-tile row: an MX block is 32 contiguous
+// elements.  The scales of the tile's 256 rows / columns over all of K (256 x K / 32 bytes each; K <= 1024)
+// are staged in LDS before the main loop, in the order the fragment reads want (mx_a_index / mx_b_index:
+// a lane reads its 8 A-row scales with one ds_read_b64 and its 4 W-column scales with one ds_read_b32 per
+// K-tile, picked by the MFMA's op_sel byte).
 #pragma once
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
@@ -31,7 +44,9 @@ namespace fl {
 
 constexpr int k8pThreads = 512;
 
-template <class EP>
+constexpr int kMxMaxK = 1024;  // fp8 path: largest K whose scales are staged whole (256 x K/32 B per operand)
+
+template <class EP, bool F8 = false>
 struct G8Smem {
   static constexpr int HALF = 16 * 1024;           // one half-tile: 128 rows x 128 B
   static constexpr int BUF = 4 * HALF;             // one K-tile: A (32 KB) then W (32 KB)
@@ -40,12 +55,49 @@ struct G8Smem {
   static constexpr int body = ring > ctile ? ring : ctile;
   static constexpr int e_stats = EP::stat_rows(256) * 2 * 4;
   static constexpr int e_vec = kevec_of<EP>::value * kEVecStride * 4;  // per 128-column half (two copies)
-  static constexpr int bytes = (body + e_stats + 2 * e_vec + 15) / 16 * 16;
+  static constexpr int mx = F8 ? 2 * 256 * (kMxMaxK / 32) : 0;          // A then W scale bytes
+  static constexpr int bytes = (body + e_stats + 2 * e_vec + mx + 15) / 16 * 16;
 };
+
+// Position of the e8m0 scale of (row m, K block kb) of an fp8 A operand with K columns: per 256-row tile
+// a contiguous 256 x K/32-byte image, ordered [kb][row half][row % 16][row % 128 / 16] (a lane's 8
+// fragment rows are 8 consecutive bytes).  Rows are padded to a multiple of 256.
+__host__ __device__ __forceinline__ size_t mx_a_index(int m, int kb, int K) {
+  const int r = m & 255;
+  return (size_t)(m >> 8) * (size_t)(8 * K) + (size_t)(((kb * 2 + (r >> 7)) << 7) + ((r & 15) << 3) + ((r & 127) >> 4));
+}
+// ... of (column n, K block kb) of an fp8 W: per 256-column tile [kb][column quarter][n % 16][n % 64 / 16].
+__host__ __device__ __forceinline__ size_t mx_b_index(int n, int kb, int K) {
+  const int c = n & 255;
+  return (size_t)(n >> 8) * (size_t)(8 * K) + (size_t)(((kb * 4 + (c >> 6)) << 6) + ((c & 15) << 2) + ((c & 63) >> 4));
+}
+// Bytes of the scale image of an fp8 operand of `rows` rows (or W columns) and K columns.
+inline size_t mx_scale_bytes(size_t rows, int K) { return (rows + 255) / 256 * 256 * (size_t)(K / 32); }
+
+// MX block exponent of the HIP recipe: the smallest e with amax * 2^-e <= 448 (no element saturates;
+// e = ceil(log2(amax / 448)), tests/fp8_sim.py "mxfp8c"), clamped to the e8m0 range.
+__device__ __forceinline__ int mx_exp(float amax) {
+  const unsigned u = __float_as_uint(amax);
+  const int be = (int)((u >> 23) & 0xff);
+  if (be == 0) return -127;  // zero / denormal block: any scale represents it
+  int e = be - 127 - 8;      // amax * 2^-e in [256, 512)
+  if (amax * __uint_as_float((unsigned)(127 - e) << 23) > 448.f) ++e;
+  return e < -126 ? -126 : (e > 127 ? 127 : e);
+}
+__device__ __forceinline__ float mx_inv(int e) { return __uint_as_float((unsigned)(127 - e) << 23); }  // 2^-e
+// Four values (already scaled into [-448, 448]) -> four e4m3 bytes, v[0] in the low byte.
+__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
 
 // tile row (A) / tile column (W) of row q in [0, 128) of half-tile h (0: lo, 1: hi)
 __device__ __forceinline__ int g8_arow(int h, int q) { return (q & 63) + ((q >> 6) << 7) + (h << 6); }
 __device__ __forceinline__ int g8_bcol(int h, int q) { return (q & 31) + ((q >> 5) << 6) + (h << 5); }
+
+// Epilogues whose output is the next GEMM's MX-fp8 operand (EP::kF8Out; store_f8 hook).
+template <class T, class = void> struct kf8out_of { static constexpr bool value = false; };
+template <class T> struct kf8out_of<T, std::void_t<decltype(T::kF8Out)>> { static constexpr bool value = T::kF8Out; };
 
 // Four consecutive residual values of an epilogue with kPre: one vector load when the epilogue has pre4.
 template <class T, class = void> struct has_pre4 { static constexpr bool value = false; };
@@ -63,14 +115,47 @@ __device__ __forceinline__ void pre4(const EP& ep, int m, int n, float* x) {
   }
 }
 
-template <class EP>
-__global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restrict__ A, int lda, const bf16* __restrict__ W,
-                                                            int ldw, EP ep, int M, int N, int K) {
-  using SM = G8Smem<EP>;
+// Bias + activation (EpiBiasAct<bf16, ACT>'s arithmetic) written as the next GEMM's MX-fp8 A operand:
+// e4m3 rows (row stride ldo bytes) + the scale image (mx_a_index with K = ldo).  gemm8p epilogues only.
+template <int ACT>
+struct EpiBiasActF8 {
+  static constexpr bool kF8Out = true;
+  const float* __restrict__ bias;
+  unsigned char* __restrict__ out;
+  unsigned char* __restrict__ sc;
+  int ldo;
+  static constexpr bool kRowStats = false;
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {}
+  __device__ float value(int, int n, float acc, const float*, int) const {
+    float v = acc + bias[n];
+    if constexpr (ACT == 1) v = gelu_fast(v);
+    if constexpr (ACT == 2) v = silu(v);
+    return v;
+  }
+  __device__ void store(int, int, float) const {}
+  __device__ void store_stats(int, int, float, float) const {}
+  __device__ void store_f8(int m, int n, unsigned packed, int e, bool lead) const {
+    *reinterpret_cast<unsigned*>(out + (size_t)m * ldo + n) = packed;
+    if (lead) sc[mx_a_index(m, n >> 5, ldo)] = (unsigned char)(e + 127);
+  }
+};
+
+// A / W: bf16 (F8 = false) or e4m3 bytes with scale images SA / SW (F8 = true); lda / ldw in elements.
+template <class EP, bool F8 = false>
+__global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restrict__ Av, int lda, const void* __restrict__ Wv,
+                                                            int ldw, EP ep, int M, int N, int K,
+                                                            const unsigned char* __restrict__ SA,
+                                                            const unsigned char* __restrict__ SW) {
+  using SM = G8Smem<EP, F8>;
+  constexpr int ES = F8 ? 1 : 2;  // bytes per element
+  const char* A = reinterpret_cast<const char*>(Av);
+  const char* W = reinterpret_cast<const char*>(Wv);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* e_stats = reinterpret_cast<float*>(smem + SM::body);
   float* e_vec0 = e_stats + EP::stat_rows(256) * 2;
   float* e_vec1 = e_vec0 + kevec_of<EP>::value * kEVecStride;
+  unsigned char* mxs = reinterpret_cast<unsigned char*>(e_vec1 + kevec_of<EP>::value * kEVecStride);  // F8 scales
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -89,11 +174,11 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
     tx = wg - ty * gx;
   }
   const int bm = ty * 256, bn = tx * 256;
-  const int NT = K / 64;
+  const int NT = K * ES / 128;  // 128-B K-tiles
 
   // ---- per-lane DMA sources: wave w moves rows q = 16 w + 8 j + lane / 8 (j = 0, 1) of a half-tile;
   // lane % 8 picks the 16-B chunk, XOR-swizzled on the source (lds_off<8> on the read, rule 21).  Kept as
-  // 32-bit element offsets from the (uniform) operand bases: 8 VGPRs instead of 8 pointers.
+  // 32-bit byte offsets from the (uniform) operand bases: 8 VGPRs instead of 8 pointers.
   unsigned aoff[2][2], woff[2][2];  // [half][j]
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -102,8 +187,8 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
     for (int h = 0; h < 2; ++h) {
       const int ar = g8_arow(h, q), wn = g8_bcol(h, q);
       const int m = bm + ar < M ? bm + ar : M - 1;
-      aoff[h][j] = (unsigned)m * (unsigned)lda + (unsigned)(((lane & 7) ^ ((ar >> 1) & 7)) << 3);
-      woff[h][j] = (unsigned)(bn + wn) * (unsigned)ldw + (unsigned)(((lane & 7) ^ ((wn >> 1) & 7)) << 3);
+      aoff[h][j] = (unsigned)m * (unsigned)(lda * ES) + (unsigned)(((lane & 7) ^ ((ar >> 1) & 7)) << 4);
+      woff[h][j] = (unsigned)(bn + wn) * (unsigned)(ldw * ES) + (unsigned)(((lane & 7) ^ ((wn >> 1) & 7)) << 4);
     }
   }
   // A image rows are tile rows (byte r * 128 of the K-tile's A region); half-tile h row q lands at tile
@@ -116,8 +201,8 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int q0 = wave * 16 + j * 8;  // first row of this instruction in the half-tile
-      if (isA) glds16(A + aoff[h][j] + (unsigned)t * 64u, buf + g8_arow(h, q0) * 128);
-      else glds16(W + woff[h][j] + (unsigned)t * 64u, buf + 2 * SM::HALF + g8_bcol(h, q0) * 128);
+      if (isA) glds16(A + aoff[h][j] + (unsigned)t * 128u, buf + g8_arow(h, q0) * 128);
+      else glds16(W + woff[h][j] + (unsigned)t * 128u, buf + 2 * SM::HALF + g8_bcol(h, q0) * 128);
     }
   };
 
@@ -151,15 +236,46 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
       b[j][1] = *reinterpret_cast<const u32x4*>(p1 + (j0 + j) * 2048);
     }
   };
+  // F8: this lane's scale words of the current K-tile (A rows i = 0..7 as two words, W columns j = 0..3)
+  unsigned sa_w[2] = {0u, 0u}, sw_w = 0u;
+  auto read_s = [&](int t) __attribute__((always_inline)) {
+    if constexpr (F8) {
+      const int kb = t * 4 + fq;
+      const uint2 v = *reinterpret_cast<const uint2*>(mxs + ((kb * 2 + wr) << 7) + (fr << 3));
+      sa_w[0] = v.x;
+      sa_w[1] = v.y;
+      sw_w = *reinterpret_cast<const unsigned*>(mxs + 256 * (kMxMaxK / 32) + ((kb * 4 + wc) << 6) + (fr << 2));
+    }
+  };
   auto mfma_q = [&](int i0, int j0, const u32x4 (&b)[2][2]) __attribute__((always_inline)) {
+    if constexpr (F8) {
+      typedef int i32x8 __attribute__((ext_vector_type(8)));
+      auto cat = [](const u32x4& lo, const u32x4& hi) __attribute__((always_inline)) {
+        return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      };
+      const unsigned sa = i0 ? sa_w[1] : sa_w[0];
+      // op_sel picks the byte of the scale word: A row i0 + i -> byte i, W column j0 + j -> byte j0 + j
+#define FL_MXQ(I, J, JB)                                                                                           \
+  acc[i0 + I][j0 + J] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat(a[I][0], a[I][1]), cat(b[J][0], b[J][1]), \
+                                                                         acc[i0 + I][j0 + J], 0, 0, I, sa, JB, sw_w)
+      if (j0 == 0) {
+        FL_MXQ(0, 0, 0); FL_MXQ(0, 1, 1); FL_MXQ(1, 0, 0); FL_MXQ(1, 1, 1);
+        FL_MXQ(2, 0, 0); FL_MXQ(2, 1, 1); FL_MXQ(3, 0, 0); FL_MXQ(3, 1, 1);
+      } else {
+        FL_MXQ(0, 0, 2); FL_MXQ(0, 1, 3); FL_MXQ(1, 0, 2); FL_MXQ(1, 1, 3);
+        FL_MXQ(2, 0, 2); FL_MXQ(2, 1, 3); FL_MXQ(3, 0, 2); FL_MXQ(3, 1, 3);
+      }
+#undef FL_MXQ
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, a[i][kk]), __builtin_bit_cast(bf16x8, b[j][kk]), acc[i0 + i][j0 + j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j)
+            acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, a[i][kk]), __builtin_bit_cast(bf16x8, b[j][kk]), acc[i0 + i][j0 + j], 0, 0, 0);
+    }
   };
   auto bar = []() __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
@@ -193,6 +309,16 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
   } else {
     ep.prologue(bm, 256, M, e_stats);
   }
+  if constexpr (F8) {  // the tile's A-row and W-column scale images (8 * K bytes each), before any DMA
+    const int n16 = K / 2;  // 16-B pieces per image (8 K bytes)
+    const u32x4* sa = reinterpret_cast<const u32x4*>(SA + (size_t)ty * (size_t)(8 * K));
+    const u32x4* sw = reinterpret_cast<const u32x4*>(SW + (size_t)tx * (size_t)(8 * K));
+    for (int q = tid; q < n16; q += k8pThreads) {
+      reinterpret_cast<u32x4*>(mxs)[q] = sa[q];
+      reinterpret_cast<u32x4*>(mxs + 256 * (kMxMaxK / 32))[q] = sw[q];
+    }
+    __syncthreads();
+  }
 
   // ---- prologue: K-tile 0 whole, K-tile 1's A_lo / B_lo (the steady state's phase 7 / 8 loads)
   issue(0, 0); issue(0, 1); issue(0, 2); issue(0, 3);
@@ -207,6 +333,7 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
     const char* O = smem + 1 * SM::BUF;
     const bool e2 = t + 2 < NT, o2 = t + 3 < NT;  // NT is even: the odd K-tile t + 1 always exists
     // phase 1: E.Q0 (A_lo x B_lo)
+    read_s(t);
     read_b(blo, E, 0);
     read_a(E, 0);
     issue(t + 1, 2);
@@ -225,6 +352,7 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mid(); mfma_q(4, 0, blo); tail();
     // phase 5: O.Q0
+    read_s(t + 1);
     read_b(blo, O, 0);
     read_a(O, 0);
     if (e2) issue(t + 2, 2);
@@ -290,6 +418,15 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const bf16* __restri
           else if constexpr (EV) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bnh);
           else v[e] = ep.value(m, n, av[e], e_stats, bm);
         }
+        if constexpr (kf8out_of<EP>::value) {  // MX-fp8 output: 8 lanes = one 32-column block of the row
+          float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+#pragma unroll
+          for (int o = 1; o < 8; o <<= 1) am = fmaxf(am, __shfl_xor(am, o));
+          const int e = mx_exp(am);
+          const float inv = mx_inv(e);
+          if (bm + row < M) ep.store_f8(bm + row, bnh + c, pack4_fp8(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv), e, (tid & 7) == 0);
+          continue;
+        }
         if constexpr (EP::kRowStats) {
           float sum = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
@@ -318,9 +455,28 @@ inline int launch_gemm8p(const bf16* A, int lda, const bf16* W, int ldw, const E
   FL_REQUIRE(M > 0 && N % 256 == 0 && K % 128 == 0, "gemm8p: unsupported shape M=%d N=%d K=%d", M, N, K);
   using SM = G8Smem<EP>;
   static_assert(SM::bytes <= 160 * 1024, "gemm8p: LDS");
-  auto kern = gemm8p_kernel<EP>;
+  auto kern = gemm8p_kernel<EP, false>;
   FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
-  hipLaunchKernelGGL(kern, dim3(N / 256, (M + 255) / 256), dim3(k8pThreads), SM::bytes, st, A, lda, W, ldw, ep, M, N, K);
+  hipLaunchKernelGGL(kern, dim3(N / 256, (M + 255) / 256), dim3(k8pThreads), SM::bytes, st, (const void*)A, lda, (const void*)W, ldw,
+                     ep, M, N, K, (const unsigned char*)nullptr, (const unsigned char*)nullptr);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+// MX-fp8: A (M x K e4m3, row stride lda bytes) with scale image SA (mx_a_index, rows padded to 256), W
+// (N x K e4m3) with SW (mx_b_index).  Shapes: N % 256 == 0, K % 256 == 0 (an even number of 128-deep
+// K-tiles), K <= kMxMaxK.
+template <class EP>
+inline int launch_gemm8p_f8(const unsigned char* A, const unsigned char* SA, int lda, const unsigned char* W,
+                            const unsigned char* SW, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  FL_REQUIRE(M > 0 && N % 256 == 0 && K % 256 == 0 && K <= kMxMaxK && A && SA && W && SW,
+             "gemm8p_f8: unsupported shape M=%d N=%d K=%d", M, N, K);
+  using SM = G8Smem<EP, true>;
+  static_assert(SM::bytes <= 160 * 1024, "gemm8p_f8: LDS");
+  auto kern = gemm8p_kernel<EP, true>;
+  FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
+  hipLaunchKernelGGL(kern, dim3(N / 256, (M + 255) / 256), dim3(k8pThreads), SM::bytes, st, (const void*)A, lda, (const void*)W, ldw,
+                     ep, M, N, K, SA, SW);
   FL_LAUNCH_CHECK();
   return kOk;
 }

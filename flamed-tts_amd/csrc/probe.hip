@@ -303,6 +303,34 @@ FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, 
   return rc;
 }
 
+// One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3) on a 16 x 128 A, 16 x 128 B (row n = output
+// column), e8m0 scales sa / sb [16][4]: lane l holds row l % 16 and the 32 bytes of "lane group" l / 16;
+// mode 0: bytes [32 g, 32 g + 32) of the row, mode 1: chunks g and 4 + g (K [16 g, 16 g + 16) and
+// [64 + 16 g, ...)); the lane passes the scale byte sa[row][g].  C[16][16] (row m, column n).
+__global__ void mx_probe_kernel(const unsigned char* A, const unsigned char* B, const unsigned char* sa,
+                                const unsigned char* sb, float* C, int mode) {
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
+  const int l = threadIdx.x, r = l & 15, g = l >> 4;
+  const int c0 = mode == 0 ? 2 * g : g, c1 = mode == 0 ? 2 * g + 1 : 4 + g;
+  const u32x4 a0 = *reinterpret_cast<const u32x4*>(A + r * 128 + c0 * 16), a1 = *reinterpret_cast<const u32x4*>(A + r * 128 + c1 * 16);
+  const u32x4 b0 = *reinterpret_cast<const u32x4*>(B + r * 128 + c0 * 16), b1 = *reinterpret_cast<const u32x4*>(B + r * 128 + c1 * 16);
+  const i32x8 av = {(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+  const i32x8 bv = {(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+  const int sca = sa[r * 4 + g], scb = sb[r * 4 + g];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc, 0, 0, 0, sca, 0, scb);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) C[(g * 4 + e) * 16 + r] = acc[e];
+}
+
+FLAMED_API int flamed_probe_mx(const void* A, const void* B, const void* sa, const void* sb, float* C, int mode, hipStream_t st) {
+  FL_REQUIRE(A && B && sa && sb && C, "flamed_probe_mx: null args");
+  hipLaunchKernelGGL(mx_probe_kernel, dim3(1), dim3(64), 0, st, (const unsigned char*)A, (const unsigned char*)B,
+                     (const unsigned char*)sa, (const unsigned char*)sb, C, mode);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
 FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t st) {
   FL_REQUIRE(us_out && reps > 0 && blocks > 0, "flamed_probe_empty: bad args");
   auto body = [&](hipStream_t s) -> int {

@@ -74,11 +74,13 @@ DIAG_SIGNATURES = {
     "flamed_probe_empty": (c_int, [c_int, c_int, ctypes.POINTER(c_float), P]),
     "flamed_probe_gemm_pf": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
+    "flamed_probe_mx": (c_int, [P, P, P, P, P, c_int, P]),
     "flamed_stamp_buffer": (c_int, [P]),
 }
 
-FLAMED_F32, FLAMED_BF16 = 0, 1
-DTYPES = {"f32": FLAMED_F32, "fp32": FLAMED_F32, "float32": FLAMED_F32, "bf16": FLAMED_BF16, "bfloat16": FLAMED_BF16}
+FLAMED_F32, FLAMED_BF16, FLAMED_FP8 = 0, 1, 2
+DTYPES = {"f32": FLAMED_F32, "fp32": FLAMED_F32, "float32": FLAMED_F32, "bf16": FLAMED_BF16, "bfloat16": FLAMED_BF16,
+          "fp8": FLAMED_FP8}  # fp8: denoiser handles only (MX-fp8 pointwise GEMMs at large M, bf16 elsewhere)
 
 
 def lib():

@@ -31,6 +31,12 @@ FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream
 FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, int wbufs, int pf_blocks, const void* A,
                                     const void* W, void* C, float* us_out, hipStream_t stream);
 
+/* flamed_probe_mx: one block-scaled MX-fp8 MFMA (16x16x128, e4m3, e8m0 scales) in lane layout `mode`
+ * (0: a lane's 32 bytes are K [32g, 32g+32) of its row, 1: K [16g, 16g+16) and [64+16g, 64+16g+16));
+ * A, B 16 x 128 bytes, sa, sb 16 x 4, C 16 x 16 fp32 = sum_k A[m][k] sa B[n][k] sb. */
+FLAMED_API int flamed_probe_mx(const void* A, const void* B, const void* sa, const void* sb, float* C, int mode,
+                               hipStream_t stream);
+
 /* libflamed_hip_stamps.so only: device buffer of blocks x 8 u64 into which the denoiser kernels of
  * class `flamed_tune("stamp_class", c)` write s_memtime at their phase boundaries (eager steps). */
 FLAMED_API int flamed_stamp_buffer(void* buf);

@@ -30,7 +30,11 @@ extern "C" {
 
 #define FLAMED_API __attribute__((visibility("default")))
 
-enum { FLAMED_F32 = 0, FLAMED_BF16 = 1 };
+/* Compute dtypes.  FLAMED_FP8 (denoiser handles only): FLAMED_BF16 everywhere, plus MX-fp8 (OCP e4m3 with
+ * one e8m0 scale per 32 input channels, weights and activations) for the four H x H pointwise GEMMs of
+ * every block (conv_2, conv_3, mlp.0, mlp.2; BASELINE configs[4]) on the large-M path (B*T >= the
+ * g8p_rows knob, default 16384); below it the handle computes exactly as FLAMED_BF16. */
+enum { FLAMED_F32 = 0, FLAMED_BF16 = 1, FLAMED_FP8 = 2 };
 
 FLAMED_API const char* flamed_last_error(void);
 FLAMED_API int flamed_version(void);
