@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=400, help="latent frames per utterance (80 Hz)")
     ap.add_argument("--nfe", type=int, default=128)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"], help="denoiser handle dtype (fp8: MX-fp8 pointwise GEMMs at large M)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -1308,22 +1308,7 @@ __global__ __launch_bounds__(256) void lnmod_apply_bf16_kernel(LoadLNMod<bf16, A
 }
 
 // ---- MX-fp8 operands (fp8 handles, large M; gemm_8p.hpp): the same normalise passes writing e4m3 rows +
-// the scale image.  A thread's 8 consecutive columns; the 4 lanes of one 32-column block combine their
-// maxima with two shuffles (lane groups of 4 are 32-column aligned: K / 8 = 128 lanes per row).
-__device__ __forceinline__ void store_f8x8(const float* o, unsigned char* dst, unsigned char* sc, int m, int k, int K) {
-  float am = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(o[j]));
-  am = fmaxf(am, __shfl_xor(am, 1));
-  am = fmaxf(am, __shfl_xor(am, 2));
-  const int e = mx_exp(am);
-  const float inv = mx_inv(e);
-  const uint2 q = make_uint2(pack4_fp8(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv),
-                             pack4_fp8(o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv));
-  *reinterpret_cast<uint2*>(dst + (size_t)m * K + k) = q;
-  if ((k & 31) == 0) sc[mx_a_index(m, k >> 5, K)] = (unsigned char)(e + 127);
-}
-
+// the scale image through store_f8x8.
 template <typename DS>
 __global__ void gn_apply_f8_kernel(LoadGN<bf16> al, const DS* src, unsigned char* dst, unsigned char* sc, int M) {
   const int H = al.H, K8 = H / 8;
@@ -1383,32 +1368,6 @@ static int f8_prep(const LoadLNMod<bf16, AFF>& al, int M, unsigned char* a8, uns
     hipLaunchKernelGGL((lnmod_apply_f8_kernel<AFF, float>), dim3((M + 1) / 2), dim3(256), 0, st, al, al.x, a8, s8, M);
   FL_LAUNCH_CHECK();
   return kOk;
-}
-
-// fp32 weight W[N][K] -> e4m3 rows + the W scale image (mx_b_index): one thread per (row, 32-block).
-__global__ void quant_w_f8_kernel(const float* __restrict__ src, int N, int K, unsigned char* __restrict__ dst,
-                                  unsigned char* __restrict__ sc) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, KB = K / 32;
-  if (i >= N * KB) return;
-  const int n = i / KB, kb = i - n * KB;
-  const float* p = src + (size_t)n * K + kb * 32;
-  float v[32], am = 0.f;
-#pragma unroll
-  for (int j = 0; j < 32; j += 4) {
-    const float4 f = ld4(p + j);
-    v[j] = f.x; v[j + 1] = f.y; v[j + 2] = f.z; v[j + 3] = f.w;
-  }
-#pragma unroll
-  for (int j = 0; j < 32; ++j) am = fmaxf(am, fabsf(v[j]));
-  const int e = mx_exp(am);
-  const float inv = mx_inv(e);
-  unsigned q[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) q[j] = pack4_fp8(v[4 * j] * inv, v[4 * j + 1] * inv, v[4 * j + 2] * inv, v[4 * j + 3] * inv);
-  u32x4* d = reinterpret_cast<u32x4*>(dst + (size_t)n * K + kb * 32);
-  d[0] = u32x4{q[0], q[1], q[2], q[3]};
-  d[1] = u32x4{q[4], q[5], q[6], q[7]};
-  sc[mx_b_index(n, kb, K)] = (unsigned char)(e + 127);
 }
 
 static int big_prep(const LoadF32<bf16>& al, int M, int K, bf16* a16, hipStream_t st) {

@@ -95,6 +95,19 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
 __device__ __forceinline__ int g8_arow(int h, int q) { return (q & 63) + ((q >> 6) << 7) + (h << 6); }
 __device__ __forceinline__ int g8_bcol(int h, int q) { return (q & 31) + ((q >> 5) << 6) + (h << 5); }
 
+// One block-scaled MX-fp8 MFMA accumulating in place (D == C, tied): the builtin's destination is not tied
+// to its accumulator input, and at 2 waves / SIMD the untied form spills the 256 x 256 tile's 128
+// accumulators.  A scale byte IB / JB of the scale word: op_sel bit = byte & 1, op_sel_hi bit = byte >> 1.
+typedef int mx_i32x8 __attribute__((ext_vector_type(8)));
+template <int IB, int JB>
+__device__ __forceinline__ void mx_mfma_inplace(f32x4& acc, const mx_i32x8& a, const mx_i32x8& b, unsigned sa, unsigned sb) {
+  if constexpr (IB == 0 && JB == 0)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]" : "+v"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+  else
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[%5,%6,0] op_sel_hi:[%7,%8,0]"
+                 : "+v"(acc) : "v"(a), "v"(b), "v"(sa), "v"(sb), "i"(IB & 1), "i"(JB & 1), "i"(IB >> 1), "i"(JB >> 1));
+}
+
 // Epilogues whose output is the next GEMM's MX-fp8 operand (EP::kF8Out; store_f8 hook).
 template <class T, class = void> struct kf8out_of { static constexpr bool value = false; };
 template <class T> struct kf8out_of<T, std::void_t<decltype(T::kF8Out)>> { static constexpr bool value = T::kF8Out; };
@@ -113,6 +126,48 @@ __device__ __forceinline__ void pre4(const EP& ep, int m, int n, float* x) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[e] = ep.pre(m, n + e);
   }
+}
+
+// A producer thread's 8 consecutive columns of row m (K columns) -> e4m3 + the block scale; the 4 lanes
+// of one 32-column block (consecutive lanes, 32-column aligned) combine their maxima with two shuffles.
+__device__ __forceinline__ void store_f8x8(const float* o, unsigned char* dst, unsigned char* sc, int m, int k, int K) {
+  float am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(o[j]));
+  am = fmaxf(am, __shfl_xor(am, 1));
+  am = fmaxf(am, __shfl_xor(am, 2));
+  const int e = mx_exp(am);
+  const float inv = mx_inv(e);
+  const uint2 q = make_uint2(pack4_fp8(o[0] * inv, o[1] * inv, o[2] * inv, o[3] * inv),
+                             pack4_fp8(o[4] * inv, o[5] * inv, o[6] * inv, o[7] * inv));
+  *reinterpret_cast<uint2*>(dst + (size_t)m * K + k) = q;
+  if ((k & 31) == 0) sc[mx_a_index(m, k >> 5, K)] = (unsigned char)(e + 127);
+}
+
+// fp32 weight W[N][K] -> e4m3 rows + the W scale image (mx_b_index): one thread per (row, 32-block).
+static __global__ void quant_w_f8_kernel(const float* __restrict__ src, int N, int K, unsigned char* __restrict__ dst,
+                                  unsigned char* __restrict__ sc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, KB = K / 32;
+  if (i >= N * KB) return;
+  const int n = i / KB, kb = i - n * KB;
+  const float* p = src + (size_t)n * K + kb * 32;
+  float v[32], am = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; j += 4) {
+    const float4 f = ld4(p + j);
+    v[j] = f.x; v[j + 1] = f.y; v[j + 2] = f.z; v[j + 3] = f.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 32; ++j) am = fmaxf(am, fabsf(v[j]));
+  const int e = mx_exp(am);
+  const float inv = mx_inv(e);
+  unsigned q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = pack4_fp8(v[4 * j] * inv, v[4 * j + 1] * inv, v[4 * j + 2] * inv, v[4 * j + 3] * inv);
+  u32x4* d = reinterpret_cast<u32x4*>(dst + (size_t)n * K + kb * 32);
+  d[0] = u32x4{q[0], q[1], q[2], q[3]};
+  d[1] = u32x4{q[4], q[5], q[6], q[7]};
+  sc[mx_b_index(n, kb, K)] = (unsigned char)(e + 127);
 }
 
 // Bias + activation (EpiBiasAct<bf16, ACT>'s arithmetic) written as the next GEMM's MX-fp8 A operand:
@@ -212,7 +267,12 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 a[4][2], blo[2][2], bhi[2][2];
+  u32x4 a[4][2], blo[2][2], bhi[2][2];  // bf16: fragment i / j, 16-B chunk kk
+  // F8: the same two chunks read straight into the halves of the MFMA's 8-dword operand (no copies into
+  // fresh register tuples: the fp8 loop otherwise spills at 2 waves / SIMD)
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  typedef int i32x8 __attribute__((ext_vector_type(8)));
+  i32x8 a8[4], blo8[2], bhi8[2];
   // fragment read addresses: row (wr*128 + i*16 + fr) / (wc*64 + j*16 + fr) at chunk kk*4 + fq; the lds_off
   // swizzle ((row >> 1) & 7) reduces to (fr >> 1) & 7, so fragment i / j is +2048 B (an immediate offset)
   const int swz = (fr >> 1) & 7;
@@ -223,23 +283,38 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
     const char* p1 = ta + lda0 + kc1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      a[i][0] = *reinterpret_cast<const u32x4*>(p0 + (i0 + i) * 2048);
-      a[i][1] = *reinterpret_cast<const u32x4*>(p1 + (i0 + i) * 2048);
+      if constexpr (F8) {
+        a8[i].lo = *reinterpret_cast<const i32x4*>(p0 + (i0 + i) * 2048);
+        a8[i].hi = *reinterpret_cast<const i32x4*>(p1 + (i0 + i) * 2048);
+      } else {
+        a[i][0] = *reinterpret_cast<const u32x4*>(p0 + (i0 + i) * 2048);
+        a[i][1] = *reinterpret_cast<const u32x4*>(p1 + (i0 + i) * 2048);
+      }
     }
   };
-  auto read_b = [&](u32x4 (&b)[2][2], const char* tb, int j0) __attribute__((always_inline)) {
+  auto read_b = [&](int hi, const char* tb, int j0) __attribute__((always_inline)) {  // hi: into bhi (else blo)
     const char* p0 = tb + ldb0 + kc0;
     const char* p1 = tb + ldb0 + kc1;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      b[j][0] = *reinterpret_cast<const u32x4*>(p0 + (j0 + j) * 2048);
-      b[j][1] = *reinterpret_cast<const u32x4*>(p1 + (j0 + j) * 2048);
+      if constexpr (F8) {
+        i32x8(&b)[2] = hi ? bhi8 : blo8;
+        b[j].lo = *reinterpret_cast<const i32x4*>(p0 + (j0 + j) * 2048);
+        b[j].hi = *reinterpret_cast<const i32x4*>(p1 + (j0 + j) * 2048);
+      } else {
+        u32x4(&b)[2][2] = hi ? bhi : blo;
+        b[j][0] = *reinterpret_cast<const u32x4*>(p0 + (j0 + j) * 2048);
+        b[j][1] = *reinterpret_cast<const u32x4*>(p1 + (j0 + j) * 2048);
+      }
     }
   };
   // F8: this lane's scale words of the current K-tile (A rows i = 0..7 as two words, W columns j = 0..3)
   unsigned sa_w[2] = {0u, 0u}, sw_w = 0u;
   auto read_s = [&](int t) __attribute__((always_inline)) {
     if constexpr (F8) {
+      // the scale words are MFMA operands of the previous K-tile's (inline-asm, hazard-unaware) MFMAs:
+      // wait out the longest MFMA read-after-issue window before overwriting them
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
       const int kb = t * 4 + fq;
       const uint2 v = *reinterpret_cast<const uint2*>(mxs + ((kb * 2 + wr) << 7) + (fr << 3));
       sa_w[0] = v.x;
@@ -247,17 +322,12 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
       sw_w = *reinterpret_cast<const unsigned*>(mxs + 256 * (kMxMaxK / 32) + ((kb * 4 + wc) << 6) + (fr << 2));
     }
   };
-  auto mfma_q = [&](int i0, int j0, const u32x4 (&b)[2][2]) __attribute__((always_inline)) {
+  auto mfma_q = [&](int i0, int j0, int hi) __attribute__((always_inline)) {  // hi: B fragments from bhi
     if constexpr (F8) {
-      typedef int i32x8 __attribute__((ext_vector_type(8)));
-      auto cat = [](const u32x4& lo, const u32x4& hi) __attribute__((always_inline)) {
-        return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-      };
+      const i32x8(&b8)[2] = hi ? bhi8 : blo8;
       const unsigned sa = i0 ? sa_w[1] : sa_w[0];
       // op_sel picks the byte of the scale word: A row i0 + i -> byte i, W column j0 + j -> byte j0 + j
-#define FL_MXQ(I, J, JB)                                                                                           \
-  acc[i0 + I][j0 + J] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat(a[I][0], a[I][1]), cat(b[J][0], b[J][1]), \
-                                                                         acc[i0 + I][j0 + J], 0, 0, I, sa, JB, sw_w)
+#define FL_MXQ(I, J, JB) mx_mfma_inplace<I, JB>(acc[i0 + I][j0 + J], a8[I], b8[J], sa, sw_w)
       if (j0 == 0) {
         FL_MXQ(0, 0, 0); FL_MXQ(0, 1, 1); FL_MXQ(1, 0, 0); FL_MXQ(1, 1, 1);
         FL_MXQ(2, 0, 0); FL_MXQ(2, 1, 1); FL_MXQ(3, 0, 0); FL_MXQ(3, 1, 1);
@@ -267,6 +337,7 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
       }
 #undef FL_MXQ
     } else {
+      const u32x4(&b)[2][2] = hi ? bhi : blo;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -334,45 +405,48 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
     const bool e2 = t + 2 < NT, o2 = t + 3 < NT;  // NT is even: the odd K-tile t + 1 always exists
     // phase 1: E.Q0 (A_lo x B_lo)
     read_s(t);
-    read_b(blo, E, 0);
+    read_b(0, E, 0);
     read_a(E, 0);
     issue(t + 1, 2);
-    mid(); mfma_q(0, 0, blo); tail();
+    mid(); mfma_q(0, 0, 0); tail();
     // phase 2: E.Q1 (A_lo x B_hi)
-    read_b(bhi, E, 2);
+    read_b(1, E, 2);
     issue(t + 1, 3);
-    mid(); mfma_q(0, 2, bhi); tail();
+    mid(); mfma_q(0, 2, 1); tail();
     // phase 3: E.Q2 (A_hi x B_hi)
     read_a(E, 4);
     if (e2) issue(t + 2, 0);
-    mid(); mfma_q(4, 2, bhi); tail();
+    mid(); mfma_q(4, 2, 1); tail();
     // phase 4: E.Q3 (A_hi x B_lo); wait: the odd K-tile has landed (E'.A_lo / B_lo may fly)
     if (e2) issue(t + 2, 1);
     if (e2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    mid(); mfma_q(4, 0, blo); tail();
+    mid(); mfma_q(4, 0, 0); tail();
     // phase 5: O.Q0
     read_s(t + 1);
-    read_b(blo, O, 0);
+    read_b(0, O, 0);
     read_a(O, 0);
     if (e2) issue(t + 2, 2);
-    mid(); mfma_q(0, 0, blo); tail();
+    mid(); mfma_q(0, 0, 0); tail();
     // phase 6: O.Q1
-    read_b(bhi, O, 2);
+    read_b(1, O, 2);
     if (e2) issue(t + 2, 3);
-    mid(); mfma_q(0, 2, bhi); tail();
+    mid(); mfma_q(0, 2, 1); tail();
     // phase 7: O.Q2
     read_a(O, 4);
     if (o2) issue(t + 3, 0);
-    mid(); mfma_q(4, 2, bhi); tail();
+    mid(); mfma_q(4, 2, 1); tail();
     // phase 8: O.Q3; wait: the next even K-tile has landed (O'.A_lo / B_lo may fly)
     if (o2) issue(t + 3, 1);
     if (o2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    mid(); mfma_q(4, 0, blo); tail();
+    mid(); mfma_q(4, 0, 0); tail();
   }
   if (wr == 0) bar();  // realign the two wave rows: every LDS read of the main loop is complete after this
   bar();
+  // F8: the last MFMAs were inline asm (the compiler's hazard recognizer does not see them): the XDL
+  // write -> VALU / DS read window of a 16-pass MFMA (18 wait states) before the epilogue reads acc
+  if constexpr (F8) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
   // ---- epilogue, one 128-column half at a time through a 256 x 128 fp32 image
   float* ct = reinterpret_cast<float*>(smem);

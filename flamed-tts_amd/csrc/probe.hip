@@ -331,6 +331,35 @@ FLAMED_API int flamed_probe_mx(const void* A, const void* B, const void* sa, con
   return kOk;
 }
 
+// fp32 rows -> MX-fp8 A operand through the product's producer path (store_f8x8).
+__global__ void quant_a_f8_probe_kernel(const float* A, int M, int K, unsigned char* dst, unsigned char* sc) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K8 = K / 8;
+  if (i >= (size_t)M * K8) return;
+  const int m = i / K8, k = (int)(i - (size_t)m * K8) * 8;
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = A[(size_t)m * K + k + j];
+  store_f8x8(o, dst, sc, m, k, K);
+}
+
+FLAMED_API int flamed_probe_mx_gemm(const float* A, const float* W, int M, int N, int K, float* C, hipStream_t st) {
+  FL_REQUIRE(A && W && C && M > 0 && N % 256 == 0 && K % 512 == 0 && K <= kMxMaxK, "flamed_probe_mx_gemm: bad args");
+  const size_t a8 = (size_t)M * K, as = mx_scale_bytes(M, K), w8 = (size_t)N * K, wsb = mx_scale_bytes(N, K);
+  unsigned char* buf = nullptr;
+  FL_HIP(hipMalloc(&buf, a8 + as + w8 + wsb));
+  unsigned char *A8 = buf, *AS = buf + a8, *W8 = AS + as, *WS = W8 + w8;
+  FL_HIP(hipMemsetAsync(AS, 0, as, st));  // padded rows: unused scales stay finite
+  const size_t na = (size_t)M * (K / 8);
+  hipLaunchKernelGGL(quant_a_f8_probe_kernel, dim3((na + 255) / 256), dim3(256), 0, st, A, M, K, A8, AS);
+  const int nb = N * (K / 32);
+  hipLaunchKernelGGL(quant_w_f8_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, W, N, K, W8, WS);
+  int rc = launch_gemm8p_f8(A8, AS, K, W8, WS, K, EpiBiasAct<float, 0>{nullptr, C, N}, M, N, K, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(buf);
+  return rc;
+}
+
 FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t st) {
   FL_REQUIRE(us_out && reps > 0 && blocks > 0, "flamed_probe_empty: bad args");
   auto body = [&](hipStream_t s) -> int {

@@ -75,6 +75,7 @@ DIAG_SIGNATURES = {
     "flamed_probe_gemm_pf": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_mx": (c_int, [P, P, P, P, P, c_int, P]),
+    "flamed_probe_mx_gemm": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "flamed_stamp_buffer": (c_int, [P]),
 }
 

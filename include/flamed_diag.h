@@ -37,6 +37,11 @@ FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, 
 FLAMED_API int flamed_probe_mx(const void* A, const void* B, const void* sa, const void* sb, float* C, int mode,
                                hipStream_t stream);
 
+/* flamed_probe_mx_gemm: C[M][N] fp32 = MX-fp8(A[M][K]) . MX-fp8(W[N][K])^T through the product's fp8 pieces
+ * (store_f8x8 producer, quant_w_f8_kernel, the 256x256 block-scaled GEMM); N % 256 == 0, K % 512 == 0,
+ * K <= 1024.  Synchronous (allocates and frees its own scratch). */
+FLAMED_API int flamed_probe_mx_gemm(const float* A, const float* W, int M, int N, int K, float* C, hipStream_t stream);
+
 /* libflamed_hip_stamps.so only: device buffer of blocks x 8 u64 into which the denoiser kernels of
  * class `flamed_tune("stamp_class", c)` write s_memtime at their phase boundaries (eager steps). */
 FLAMED_API int flamed_stamp_buffer(void* buf);

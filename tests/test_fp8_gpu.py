@@ -7,9 +7,13 @@ on the large-M path; everything else is the bf16 path.  Two checks per case:
   * against the fp32 oracle, under a looser tolerance: velocity rel-L2 <= 8e-2
     (tests/fp8_sim.py "mxfp8c" on the same four GEMMs: 4.5e-2), solve rel-L2 <= 5e-2 (sim: 2.7e-2 at
     128 and 256 steps);
-  * against the oracle with the same MX quantization emulated (fp8_sim.Quantized): much closer (<= 2e-2
-    and < 1/3 of the fp32 error), which pins the kernel's quantization to the stated recipe (layout,
-    scales, rounding) rather than just "some 8-bit error".
+  * the MX-fp8 GEMM itself (producer quantization + weight packing + block-scaled 256x256 kernel, through
+    flamed_probe_mx_gemm) against torch's e4m3 quantization of the same recipe followed by an fp64 matmul:
+    rel-L2 <= 2e-4 (measured 4.7e-5: the scaled MFMA's internal summation, 1.7e-5 for one 128-K
+    instruction in tools/probe_mx.py; the quantization itself is 3.8e-2), which pins layout, scales and
+    rounding.  (A whole-network
+    comparison against an emulated oracle cannot be tight: bf16-level input differences flip e4m3
+    rounding decisions, ~6 % steps, and the flips compound through 20 GEMMs.)
 
 Small cases force the fp8 path at 1,600 rows with the per-handle knob g8p_rows; the configs[4] case runs
 at its real size (B = 16, T = 2400 = 38,400 rows) with the default knobs.
@@ -55,24 +59,41 @@ def _inputs(seed, B, T):
     return x, t, c
 
 
-def _emulated_velocity(sd, x, t, c):
+@pytest.mark.parametrize("M", [512, 1000])
+def test_mx_gemm_matches_recipe(M):
+    from flamed import _native as nat
     sim = _sim()
-    sdq = sim.quantized_sd(sd, "mxfp8c")
-    with sim.Quantized("mxfp8c"):
-        return orc.denoiser_forward(sdq, x, t, c)
+    N, K = 1024, 1024
+    g = torch.Generator().manual_seed(M)
+    # rows of varied magnitude (the blocks' scales differ) and a few outliers per row
+    A = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-6, 6, (M, 1), generator=g).float())
+    A[:, ::97] *= 20
+    W = torch.randn(N, K, generator=g) * 0.03
+    ref = sim.mx_q(A.double(), 1, True) @ sim.mx_q(W.double(), 1, True).T
+    Ad, Wd = A.to(DEV), W.to(DEV)
+    Cd = torch.empty(M, N, device=DEV)
+    nat.check(nat.diag_lib().flamed_probe_mx_gemm(nat.ptr(Ad), nat.ptr(Wd), M, N, K, nat.ptr(Cd), nat.stream_ptr(DEV)),
+              "flamed_probe_mx_gemm")
+    e = rel_l2(Cd.cpu().double(), ref)
+    e_plain = rel_l2(Cd.cpu().double(), A.double() @ W.double().T)
+    print(f"MX-fp8 GEMM M={M}: vs recipe {e:.3e}, vs unquantized {e_plain:.3e}")
+    assert e < 2e-4, e
+    assert e_plain > 1e-2  # it did quantize
 
 
 def test_fp8_velocity_small(pg8):
     pg, sd = pg8
     x, t, c = _inputs(11, 2, 800)
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
     with torch.inference_mode():
         v = pg.denoiser(x.to(DEV), t.to(DEV), c.to(DEV)).cpu()
-    e32 = rel_l2(v, orc.denoiser_forward(sd, x, t, c))
-    e8 = rel_l2(v, _emulated_velocity(sd, x, t, c))
-    print(f"fp8 velocity B=2 T=800: vs fp32 {e32:.3e}, vs MX emulation {e8:.3e}")
+        vb = DenoiserHIP(pg.denoiser, "bf16").velocity(x.to(DEV), t.to(DEV), c.to(DEV)).cpu()
+    ref = orc.denoiser_forward(sd, x, t, c)
+    e32, eb = rel_l2(v, ref), rel_l2(vb, ref)
+    print(f"fp8 velocity B=2 T=800: vs fp32 {e32:.3e} (bf16 handle: {eb:.3e})")
     assert torch.isfinite(v).all()
     assert e32 < FP8_VEL, e32
-    assert e8 < 2e-2 and e8 < e32 / 3, (e8, e32)
+    assert e32 > 3 * eb  # the fp8 GEMMs ran (an fp8 handle below g8p_rows computes exactly as bf16)
 
 
 def test_fp8_solve_small(pg8):
