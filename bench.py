@@ -224,6 +224,22 @@ def secondary_measurements(dev, nfe):
             cmask = torch.ones(Bc, 400, 1, dtype=torch.bool, device=dev)
             ms = _time_ms(lambda: pg.fold_condition(cond, cmask), dev)
             out[f"cond_fold_B{Bc}"] = {"ms": round(ms, 3), "frames": Bc * 400, "dtype": pg.cond_hip_dtype}
+        # prior transformer stack (HIP, exact fp32, graph-captured) vs the same modules on torch-ROCm ops,
+        # at the headline utterance: ~247 phonemes -> 400 target frames behind a 240-frame (3 s) prompt
+        pr = m.prior_generator
+        Lp, Tp, Pp = 247, 400, 240
+        ids = torch.randint(1, 300, (1, Lp), generator=g).to(dev)
+        smask = torch.zeros(1, Lp, dtype=torch.bool, device=dev)
+        xlr = torch.randn(1, Tp, 192, generator=g).to(dev)
+        tmask = torch.zeros(1, Tp, dtype=torch.bool, device=dev)
+        tl = torch.tensor([Tp], device=dev)
+        pcodes = torch.randint(0, 1024, (1, 6, Pp), generator=g).to(dev)
+        row = {"phonemes": Lp, "frames": Tp, "prompt_frames": Pp, "dtype": "f32 (exact MFMA)"}
+        row["encode_ms"] = round(_time_ms(lambda: pr.hip().encode(ids, smask), dev), 3)
+        row["decode_ms"] = round(_time_ms(lambda: pr.hip().decode(xlr, tmask, pcodes, Pp), dev), 3)
+        row["torch_encode_ms"] = round(_time_ms(lambda: pr.encoder(ids, smask), dev), 3)
+        row["torch_decode_ms"] = round(_time_ms(lambda: pr._decode(pr.bridge(xlr), tl, tmask, pcodes, Pp), dev), 3)
+        out["prior_transformer"] = row
         # end to end: Flamed.sample_batch (prior transformer + PVA + cond fold + denoiser) + decode, with
         # both reference RTF definitions (synthesize.py:209-217 prompt mode incl. decode; :293-303
         # metadata mode, decode excluded)

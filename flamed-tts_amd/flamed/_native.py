@@ -64,6 +64,13 @@ SIGNATURES = {
     "flamed_enc_out_len": (c_int, [P, c_int]),
     "flamed_enc_workspace_size": (c_size_t, [P, c_int, c_int]),
     "flamed_enc_encode": (c_int, [P, P, c_int, c_int, P, P, c_size_t, c_int, P]),
+    "flamed_prior_create": (c_int, [ctypes.POINTER(c_int), c_int, ctypes.POINTER(P)]),
+    "flamed_prior_destroy": (c_int, [P]),
+    "flamed_prior_num_weights": (c_int, [P]),
+    "flamed_prior_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_prior_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int]),
+    "flamed_prior_encode": (c_int, [P, P, P, c_int, c_int, P, P, P, c_size_t, c_int, P]),
+    "flamed_prior_decode": (c_int, [P, P, P, P, c_int, c_int, c_int, P, P, P, P, c_size_t, c_int, P]),
 }
 
 # include/flamed_diag.h: probes in libflamed_diag.so, phase stamps in libflamed_hip_stamps.so (tools only)

@@ -4,7 +4,7 @@ Every hot-path entry point the modules dispatch to on ROCm is registered as a Py
 `flamed_hip` namespace, so the calls are visible to the dispatcher: `torch.compile` (dynamo traces them
 as single opaque nodes instead of graph-breaking on ctypes), FakeTensor / meta shape propagation, and
 `torch.library.opcheck`.  The ops are thin: the work is done by the per-module owner objects
-(`DenoiserHIP`, `CondFoldHIP`, `PvaHIP`, `FacDecoderHIP`, `EncoderHIP`), which own the native handles and
+(`DenoiserHIP`, `CondFoldHIP`, `PvaHIP`, `FacDecoderHIP`, `EncoderHIP`, `PriorHIP`), which own the native handles and
 their device-resident weight arenas.  An owner is passed to an op by an integer id (custom-op schemas
 take tensors and scalars only); the registry holds weak references, so a dropped module frees its handle.
 
@@ -16,6 +16,8 @@ take tensors and scalars only); the registry holds weak references, so a dropped
   flamed_hip::length_regulate(x, pd, sd, lens, max_len, log_domain)  LengthRegulator.LR  pva.py:125-166
   flamed_hip::fac_decode(id, x, spk)               FACodecDecoder.inference        facodec.py:630-638
   flamed_hip::enc_encode(id, x)                    FACodecEncoder.forward          facodec.py:158-243
+  flamed_hip::prior_encode(id, texts, mask)        Encoder.forward (prior)         prior_generator.py:152-153
+  flamed_hip::prior_decode(id, x, mask, prompts, P) bridge + decoders + head       prior_generator.py:165-188
 
 None of the ops has an autograd formula: the modules route autograd (training) to their torch ops
 before reaching here, exactly as the reference trains.  There is no CPU kernel: the ops are registered
@@ -137,4 +139,31 @@ def _(oid, x):
     return x.new_empty((B, o.enc.out_channels, o.out_len(n)), dtype=torch.float32)
 
 
-OPS = ("den_velocity", "den_solve", "cond_fold", "pva_flow", "length_regulate", "fac_decode", "enc_encode")
+# ---------------------------------------------------------------- prior transformer stack
+
+@torch.library.custom_op("flamed_hip::prior_encode", mutates_args=())
+def prior_encode(oid: int, texts: Tensor, src_mask: Tensor) -> Tensor:
+    return owner(oid).encode(texts, src_mask)
+
+
+@prior_encode.register_fake
+def _(oid, texts, src_mask):
+    B, n = texts.shape
+    return texts.new_empty((B, n, owner(oid).pg.encoder.d_model), dtype=torch.float32)
+
+
+@torch.library.custom_op("flamed_hip::prior_decode", mutates_args=())
+def prior_decode(oid: int, x: Tensor, tgt_mask: Tensor, prompts: Tensor, prompts_len: int) -> Tuple[Tensor, Tensor]:
+    return owner(oid).decode(x, tgt_mask, prompts, prompts_len)
+
+
+@prior_decode.register_fake
+def _(oid, x, tgt_mask, prompts, prompts_len):
+    B, T, _ = x.shape
+    pg = owner(oid).pg
+    nq, D, V1 = len(pg.prior_decoder), pg.shared_decoder.d_model, pg.head.weight.shape[0]
+    return x.new_empty((B, nq, T, D)), x.new_empty((B, V1, nq, T))
+
+
+OPS = ("den_velocity", "den_solve", "cond_fold", "pva_flow", "length_regulate", "fac_decode", "enc_encode",
+       "prior_encode", "prior_decode")

@@ -255,6 +255,43 @@ FLAMED_API size_t flamed_enc_workspace_size(flamed_enc_t h, int B, int n);
 FLAMED_API int flamed_enc_encode(flamed_enc_t h, const float* wav, int B, int n, float* out, void* ws, size_t ws_bytes,
                                  int use_graph, hipStream_t stream);
 
+/* ======================= prior transformer stack (once per utterance) =======================
+ * Replaces the transformer parts of PriorGenerator.sample (prior_generator.py:141-196, SURVEY.md §8(f)
+ * f2): Encoder (module/transformer/Models.py:33-100) before the PVA, and bridge + shared Decoder +
+ * six prompt-prefixed Decoders (Models.py:103-171, PreEncoding prior_generator.py:12-26) + head after
+ * it.  FFTBlock = post-norm MultiHeadAttention (SubLayers.py:8-57) + conv FFN (:60-95).  Exact fp32.
+ * dims (17 + n_q ints): n_symbols, enc {hidden, heads, conv_filter, k0, k1, layers, max_seq_len},
+ *   dec {hidden, heads, conv_filter, k0, k1, shared_layers, max_seq_len}, vocab_size, n_q,
+ *   decoder_layers[n_q].  Head widths 32 or 48; hidden 192 / 256 / 384.
+ * Weight order for flamed_prior_load (fp32 device tensors, prefix prior_generator.; one FFT layer =
+ *   slf_attn.{w_qs,w_ks,w_vs}.{weight,bias}, slf_attn.fc.{weight,bias}, slf_attn.layer_norm.{weight,bias},
+ *   pos_ffn.w_1.{weight,bias}, pos_ffn.w_2.{weight,bias}, pos_ffn.layer_norm.{weight,bias}):
+ *   encoder.src_word_emb.weight, encoder.position_enc, encoder.layer_stack.* layers,
+ *   bridge.{weight,bias}, code_embedding.weight, shared_decoder.position_enc, shared_decoder layers,
+ *   pre_encode.{prompt_emb,target_emb,quantizer_emb.weight},
+ *   for each q: prior_decoder.q.position_enc, prior_decoder.q layers; head.{weight,bias}.
+ * Everything is copied / packed into the handle's arena (q/k/v concatenated, conv taps tap-major,
+ * head zero-padded to a multiple of 64 rows). */
+typedef struct flamed_prior_s* flamed_prior_t;
+FLAMED_API int flamed_prior_create(const int* dims, int n_dims, flamed_prior_t* out);
+FLAMED_API int flamed_prior_destroy(flamed_prior_t h);
+FLAMED_API int flamed_prior_num_weights(flamed_prior_t h);
+FLAMED_API int flamed_prior_load(flamed_prior_t h, const float* const* weights, int n_weights, hipStream_t stream);
+/* Workspace for an encode of (B, L) and a decode of (B, T) targets behind P prompt frames. */
+FLAMED_API size_t flamed_prior_workspace_size(flamed_prior_t h, int B, int L, int T, int P);
+/* texts (B, L) int64, src_mask (B, L) uint8 (1 = padding), out (B, L, enc hidden) fp32.  pos: NULL for
+ * the loaded encoder.position_enc (L <= max_seq_len), else an (L, hidden) table (Models.py:83-86). */
+FLAMED_API int flamed_prior_encode(flamed_prior_t h, const int64_t* texts, const uint8_t* src_mask, int B, int L,
+                                   const float* pos, float* out, void* ws, size_t ws_bytes, int use_graph,
+                                   hipStream_t stream);
+/* x (B, T, enc hidden) length-regulated encoder output, tgt_mask (B, T) uint8 (1 = padding), prompts
+ * (B, n_q, P) int64 codes; embs (B, n_q, T, dec hidden) = prior embeddings, logits (B, vocab+1, n_q, T)
+ * masked as the reference.  pos: NULL for the loaded decoder tables (P + T <= max_seq_len), else a
+ * (P + T, hidden) table used by every decoder. */
+FLAMED_API int flamed_prior_decode(flamed_prior_t h, const float* x, const uint8_t* tgt_mask, const int64_t* prompts,
+                                   int B, int T, int P, const float* pos, float* embs, float* logits, void* ws,
+                                   size_t ws_bytes, int use_graph, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -459,3 +459,115 @@ def decoder_vq(sd: SD, x: torch.Tensor, n_q=(1, 2, 3)):
         codes.append(ir)
     spk = timbre_encoder(sd, x.transpose(1, 2)).transpose(1, 2).mean(dim=2)
     return torch.cat(codes, dim=0), spk
+
+
+# --------------------------------------------------------------------------------------------
+# Prior transformer stack   (flamed/models/synthesizer/prior_generator.py, module/transformer/*.py)
+# --------------------------------------------------------------------------------------------
+
+def sinusoid_table(n_position: int, d_hid: int) -> torch.Tensor:
+    """Models.py:10-30 — angle pos / 10000^(2*(j//2)/d) in float64, sin on even j, cos on odd j, then
+    float32.  (n_position, d_hid)."""
+    pos = np.arange(n_position, dtype=np.float64)[:, None]
+    j = np.arange(d_hid)[None, :]
+    t = pos / np.power(10000, 2 * (j // 2) / d_hid)
+    t[:, 0::2] = np.sin(t[:, 0::2])
+    t[:, 1::2] = np.cos(t[:, 1::2])
+    return torch.from_numpy(t).float()
+
+
+def fft_block(sd: SD, p: str, x: torch.Tensor, mask: torch.Tensor, n_head: int) -> torch.Tensor:
+    """FFTBlock.forward, Layers.py:21-30: post-norm MultiHeadAttention (SubLayers.py:29-57; scaled
+    dot product with the key-padding mask set to -inf, Modules.py:14-25), masked_fill, then the conv
+    FFN (SubLayers.py:85-95: Conv1d k0 -> ReLU -> Conv1d k1, + residual, LayerNorm), masked_fill.
+    x (B, n, D), mask (B, n) True = padding."""
+    B, n, D = x.shape
+    dk = D // n_head
+    a = p + ".slf_attn."
+
+    def heads(name):
+        return F.linear(x, sd[a + name + ".weight"], sd[a + name + ".bias"]).view(B, n, n_head, dk) \
+            .permute(2, 0, 1, 3).reshape(n_head * B, n, dk)
+
+    q, k, v = heads("w_qs"), heads("w_ks"), heads("w_vs")
+    att = torch.bmm(q, k.transpose(1, 2)) / float(np.power(dk, 0.5))
+    att = att.masked_fill(mask.unsqueeze(1).expand(-1, n, -1).repeat(n_head, 1, 1), -np.inf)
+    o = torch.bmm(torch.softmax(att, dim=2), v).view(n_head, B, n, dk).permute(1, 2, 0, 3).reshape(B, n, D)
+    o = F.linear(o, sd[a + "fc.weight"], sd[a + "fc.bias"])
+    x = F.layer_norm(o + x, (D,), sd[a + "layer_norm.weight"], sd[a + "layer_norm.bias"], 1e-5)
+    x = x.masked_fill(mask.unsqueeze(-1), 0)
+    f = p + ".pos_ffn."
+    w1, w2 = sd[f + "w_1.weight"], sd[f + "w_2.weight"]
+    h = F.conv1d(x.transpose(1, 2), w1, sd[f + "w_1.bias"], padding=(w1.shape[-1] - 1) // 2)
+    h = F.conv1d(F.relu(h), w2, sd[f + "w_2.bias"], padding=(w2.shape[-1] - 1) // 2).transpose(1, 2)
+    x = F.layer_norm(h + x, (D,), sd[f + "layer_norm.weight"], sd[f + "layer_norm.bias"], 1e-5)
+    return x.masked_fill(mask.unsqueeze(-1), 0)
+
+
+def _n_layers(sd: SD, p: str) -> int:
+    n = 0
+    while f"{p}.layer_stack.{n}.slf_attn.fc.weight" in sd:
+        n += 1
+    return n
+
+
+def prior_encoder(sd: SD, texts: torch.Tensor, src_mask: torch.Tensor, p: str = "prior_generator.encoder",
+                  n_head: int = 4) -> torch.Tensor:
+    """Encoder.forward (eval), Models.py:73-100: src_word_emb(ids) + position table, FFT blocks."""
+    B, n = texts.shape
+    pe = sd[p + ".position_enc"][0]
+    pos = sinusoid_table(n, pe.shape[-1]) if n > pe.shape[0] - 1 else pe[:n]
+    x = F.embedding(texts, sd[p + ".src_word_emb.weight"]) + pos.unsqueeze(0).expand(B, -1, -1)
+    for i in range(_n_layers(sd, p)):
+        x = fft_block(sd, f"{p}.layer_stack.{i}", x, src_mask, n_head)
+    return x
+
+
+def prior_decoder_stack(sd: SD, p: str, x: torch.Tensor, mask: torch.Tensor, n_head: int) -> torch.Tensor:
+    """Decoder.forward (eval), Models.py:139-171: + position table, FFT blocks."""
+    B, n, _ = x.shape
+    pe = sd[p + ".position_enc"][0]
+    pos = sinusoid_table(n, pe.shape[-1]) if n > pe.shape[0] - 1 else pe[:n]
+    x = x + pos.unsqueeze(0).expand(B, -1, -1)
+    for i in range(_n_layers(sd, p)):
+        x = fft_block(sd, f"{p}.layer_stack.{i}", x, mask, n_head)
+    return x
+
+
+def prior_decode(sd: SD, x_lr: torch.Tensor, tgt_lens: torch.Tensor, prompts: torch.Tensor,
+                 p: str = "prior_generator", n_head: int = 12):
+    """PriorGenerator.sample after the PVA, prior_generator.py:165-188: bridge -> shared decoder ->
+    six prompt-prefixed decoders chained through their target slices (PreEncoding :20-26 adds the
+    segment and quantizer embeddings) -> head, masked and permuted.  x_lr (B, T, 192), prompts
+    (B, nq, P) -> (prior_embs (B, nq, T, 384), logits (B, V+1, nq, T), tgt_mask (B, T))."""
+    B, T, _ = x_lr.shape
+    P = prompts.shape[-1]
+    tgt_mask = mask_from_lengths(tgt_lens, T)
+    out = prior_decoder_stack(sd, p + ".shared_decoder",
+                              F.linear(x_lr, sd[p + ".bridge.weight"], sd[p + ".bridge.bias"]), tgt_mask, n_head)
+    dec_mask = mask_from_lengths(P + tgt_lens, P + T)
+    pemb = F.embedding(prompts, sd[p + ".code_embedding.weight"])
+    hid = []
+    nq = prompts.shape[1]
+    for q in range(nq):
+        z = torch.cat([pemb[:, q], out], dim=1)
+        z = torch.cat([z[:, :P] + sd[p + ".pre_encode.prompt_emb"], z[:, P:] + sd[p + ".pre_encode.target_emb"]], 1)
+        z = z + sd[p + ".pre_encode.quantizer_emb.weight"][q]
+        out = prior_decoder_stack(sd, f"{p}.prior_decoder.{q}", z, dec_mask, n_head)[:, P:]
+        hid.append(out.unsqueeze(1))
+    embs = torch.cat(hid, dim=1)
+    logits = F.linear(embs, sd[p + ".head.weight"], sd[p + ".head.bias"])
+    logits = logits * ~tgt_mask.unsqueeze(1).expand(-1, nq, -1).unsqueeze(3)
+    return embs, logits.permute(0, 3, 1, 2).contiguous(), tgt_mask
+
+
+def prior_sample(sd: SD, texts: torch.Tensor, src_lens: torch.Tensor, prompts: torch.Tensor, nfe: int,
+                 temperature: float, p: str = "prior_generator"):
+    """PriorGenerator.sample, prior_generator.py:141-196: encoder -> PVA flow (global-RNG noise) ->
+    length regulator -> decode."""
+    B, L = texts.shape
+    src_mask = mask_from_lengths(src_lens, L)
+    enc = prior_encoder(sd, texts, src_mask, p + ".encoder")
+    d, s = pva_flow(sd, enc, src_mask, nfe, temperature, p + ".pva")
+    x_lr, tl = length_regulate(enc.numpy(), log_to_frames(d).numpy(), log_to_frames(s).numpy(), src_lens.numpy())
+    return prior_decode(sd, torch.from_numpy(x_lr), torch.from_numpy(tl), prompts, p)

@@ -21,9 +21,10 @@ def test_every_op_is_registered_with_a_schema():
 
 def test_modules_dispatch_through_the_ops():
     import inspect
-    from flamed.models.synthesizer import prob_generator, pva
+    from flamed.models.synthesizer import prob_generator, pva, prior_generator
     from flamed.models.facodec import facodec
-    src = inspect.getsource(prob_generator) + inspect.getsource(pva) + inspect.getsource(facodec)
+    src = inspect.getsource(prob_generator) + inspect.getsource(pva) + inspect.getsource(facodec) + \
+        inspect.getsource(prior_generator)
     for name in ops.OPS:
         assert f"ops.{name}(" in src, name
 
@@ -63,6 +64,15 @@ def test_fake_shapes():
         assert w.shape == (1, 1, 8000)
         e = torch.ops.flamed_hip.enc_encode(eid, torch.empty(1, 1, 48000))
         assert e.shape == (1, 256, 240)
+        ppg = types.SimpleNamespace(encoder=types.SimpleNamespace(d_model=192), prior_decoder=[None] * 6,
+                                    shared_decoder=types.SimpleNamespace(d_model=384),
+                                    head=types.SimpleNamespace(weight=torch.empty(1025, 384)))
+        po, poid = _dummy_owner(pg=ppg)
+        h = torch.ops.flamed_hip.prior_encode(poid, torch.empty(2, 17, dtype=torch.int64), torch.empty(2, 17, dtype=torch.bool))
+        assert h.shape == (2, 17, 192) and h.dtype == torch.float32
+        pe, pl = torch.ops.flamed_hip.prior_decode(poid, torch.empty(2, 40, 192), torch.empty(2, 40, dtype=torch.bool),
+                                                   torch.empty(2, 6, 20, dtype=torch.int64), 20)
+        assert pe.shape == (2, 6, 40, 384) and pl.shape == (2, 1025, 6, 40)
 
 
 def test_dead_owner_raises():

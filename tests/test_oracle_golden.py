@@ -140,3 +140,19 @@ def test_facodec_encode_and_vq():
     assert torch.equal(codes, t32(g["codes"]))
     assert rel_l2(spk, g["spk"]) < TOL
     assert orc.positional_table(256).shape == (5000, 1, 256)
+
+
+def test_prior_sample():
+    """Prior transformer restatement (encoder -> PVA -> LR -> bridge/shared/6 decoders -> head) vs the
+    reference's PriorGenerator.sample fixture (global-RNG draw order as the reference)."""
+    from _flamed_common import build_flamed
+    m, _ = build_flamed("cpu")
+    sd = {k: v.detach() for k, v in m.state_dict().items()}
+    g = golden("flamed_sample")
+    torch.manual_seed(int(g["rng_seed"]))
+    with torch.inference_mode():
+        pe, pl, tm = orc.prior_sample(sd, t32(g["phonemes"]), t32(g["src_lens"]), t32(g["prompts"]), nfe=4,
+                                      temperature=0.3)
+    assert np.array_equal(tm.numpy(), g["tgt_mask"])
+    assert rel_l2(pe, g["prior_embs"]) < TOL
+    assert rel_l2(pl.sum(dim=1), g["prior_logits_sum"]) < TOL
