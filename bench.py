@@ -217,6 +217,10 @@ def secondary_measurements(dev, nfe):
         wav = (0.1 * torch.randn(1, 1, 48000, generator=g)).to(dev)
         ms = _time_ms(lambda: enc_m(wav), dev)
         out["facodec_prompt_encode"] = {"ms": round(ms, 3), "samples": 48000, "dtype": enc_m.hip_dtype}
+        z = enc_m(wav)
+        ms = _time_ms(lambda: dec(z, eval_vq=False, vq=True), dev)
+        out["facodec_prompt_vq_timbre"] = {"ms": round(ms, 3), "frames": int(z.shape[-1]), "dtype": "f32 (exact MFMA)",
+                                           "note": "6 RVQ layers + 4-layer timbre transformer + mean (HIP)"}
         # condition fold (once per utterance, HIP) at the headline shape
         pg = m.prob_generator
         for Bc in (1, 64):

@@ -19,6 +19,7 @@
 //   LN + mask  R -> X (the last block of a decoder also writes its target rows into prior_embs)
 #include "flamed_hip.h"
 #include "gemm.hpp"
+#include "xfmr.hpp"
 
 #include <cmath>
 #include <mutex>
@@ -82,185 +83,6 @@ __global__ void dec_input_kernel(const float* __restrict__ prev, int prev_bstrid
   if (c == 0) dmask[row] = j < P ? 0 : tmask[(size_t)b * T + (j - P)];
 }
 
-// LayerNorm (eps 1e-5, affine) + masked_fill(mask, 0), one wave per row.  With `embs` the rows j >= P
-// of utterance b are also written to embs[b][q][j - P] (the decoder's target slice, :181-182).
-template <int D>
-__global__ __launch_bounds__(256) void ln_mask_kernel(const float* __restrict__ R, const float* __restrict__ g,
-                                                      const float* __restrict__ bb, const uint8_t* __restrict__ mask,
-                                                      float* __restrict__ X, int M, int n, float* __restrict__ embs,
-                                                      int P, int T, int nq, int q) {
-  constexpr int PER = D / 64;
-  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (m >= M) return;
-  const float* r = R + (size_t)m * D;
-  float v[PER];
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    v[j] = r[lane + 64 * j];
-    s += v[j];
-  }
-  const float mean = wave_sum64(s) / (float)D;
-  float qv = 0.f;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    float d = v[j] - mean;
-    qv += d * d;
-  }
-  const float rstd = 1.0f / sqrtf(wave_sum64(qv) / (float)D + 1e-5f);
-  const bool pad = mask[m] != 0;
-  float* x = X + (size_t)m * D;
-  const int b = m / n, l = m - b * n;
-  float* e = (embs && l >= P) ? embs + (((size_t)b * nq + q) * T + (l - P)) * D : nullptr;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    int c = lane + 64 * j;
-    float y = pad ? 0.f : ((v[j] - mean) * rstd) * g[c] + bb[c];
-    x[c] = y;
-    if (e) e[c] = y;
-  }
-}
-
-// Scaled dot-product attention with a key-padding mask (Modules.py:14-25, SubLayers.py:38-52).
-// QKV rows (B*n, 3D): Q at column h*DK, K at D + h*DK, V at 2D + h*DK.  Out O (B*n, D), head h at h*DK.
-// Block: 256 threads = 4 waves; lane = query of a 64-query tile, wave w takes keys [16w, 16w+16) of
-// every 64-key chunk (all lanes read the same K/V row: LDS broadcast).
-template <int DK>
-__global__ __launch_bounds__(256) void attn_kernel(const float* __restrict__ QKV, const uint8_t* __restrict__ kmask,
-                                                   int n, int D, float temp, float* __restrict__ O) {
-  constexpr int KC = 64;        // keys per LDS chunk
-  constexpr int KW = KC / 4;    // keys per wave per chunk
-  constexpr int DS = DK / 4;    // output dims per thread in the merge
-  __shared__ __attribute__((aligned(16))) float sm[4 * 64 * (DK + 2)];
-  float* Ks = sm;               // [KC][DK]
-  float* Vs = sm + KC * DK;     // [KC][DK]
-  __shared__ uint8_t ms[KC];
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 64;
-  const int qi = q0 + lane;
-  const int ld = 3 * D;
-  const float* base = QKV + (size_t)b * n * ld;
-
-  float qv[DK];
-  {
-    const float* qp = base + (size_t)(qi < n ? qi : n - 1) * ld + h * DK;
-#pragma unroll
-    for (int d = 0; d < DK; d += 4) {
-      float4 t = ld4(qp + d);
-      qv[d] = t.x; qv[d + 1] = t.y; qv[d + 2] = t.z; qv[d + 3] = t.w;
-    }
-  }
-  float mx = -INFINITY, sum = 0.f, acc[DK];
-#pragma unroll
-  for (int d = 0; d < DK; ++d) acc[d] = 0.f;
-
-  for (int k0 = 0; k0 < n; k0 += KC) {
-    __syncthreads();
-    constexpr int V4 = KC * DK / 4;  // float4s per operand chunk
-    for (int i = tid; i < 2 * V4; i += 256) {
-      int op = i / V4, r = i - op * V4;
-      int key = r / (DK / 4), c = (r - key * (DK / 4)) * 4;
-      int kk = k0 + key;
-      float4 t = kk < n ? ld4(base + (size_t)kk * ld + (op + 1) * D + h * DK + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>((op ? Vs : Ks) + key * DK + c) = t;
-    }
-    if (tid < KC) {
-      int kk = k0 + tid;
-      ms[tid] = kk < n ? kmask[(size_t)b * n + kk] : 1;
-    }
-    __syncthreads();
-    float s[KW];
-    float cmax = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < KW; ++j) {
-      const int key = w * KW + j;
-      const float* kr = Ks + key * DK;
-      float dot = 0.f;
-#pragma unroll
-      for (int d = 0; d < DK; d += 4) {
-        float4 kv = *reinterpret_cast<const float4*>(kr + d);
-        dot = fmaf(qv[d], kv.x, dot);
-        dot = fmaf(qv[d + 1], kv.y, dot);
-        dot = fmaf(qv[d + 2], kv.z, dot);
-        dot = fmaf(qv[d + 3], kv.w, dot);
-      }
-      s[j] = ms[key] ? -INFINITY : dot / temp;
-      cmax = fmaxf(cmax, s[j]);
-    }
-    if (cmax == -INFINITY) continue;  // every key of this wave's slice is padding (uniform per wave)
-    const float nm = fmaxf(mx, cmax);
-    const float sc = expf(mx - nm);   // mx = -inf on the first live slice: exp(-inf) = 0
-    sum *= sc;
-#pragma unroll
-    for (int d = 0; d < DK; ++d) acc[d] *= sc;
-#pragma unroll
-    for (int j = 0; j < KW; ++j) {
-      const float p = expf(s[j] - nm);  // masked keys: exp(-inf) = 0
-      sum += p;
-      const float* vr = Vs + (w * KW + j) * DK;
-#pragma unroll
-      for (int d = 0; d < DK; d += 4) {
-        float4 vv = *reinterpret_cast<const float4*>(vr + d);
-        acc[d] = fmaf(p, vv.x, acc[d]);
-        acc[d + 1] = fmaf(p, vv.y, acc[d + 1]);
-        acc[d + 2] = fmaf(p, vv.z, acc[d + 2]);
-        acc[d + 3] = fmaf(p, vv.w, acc[d + 3]);
-      }
-    }
-    mx = nm;
-  }
-  // merge the four waves' partial softmax states: [w][d][lane] (conflict-free), then (mx, sum) rows
-  __syncthreads();
-  float* pa = sm;                      // 4 * DK * 64
-  float* pm = sm + 4 * DK * 64;        // 4 * 64
-  float* ps = pm + 4 * 64;             // 4 * 64
-#pragma unroll
-  for (int d = 0; d < DK; ++d) pa[(w * DK + d) * 64 + lane] = acc[d];
-  pm[w * 64 + lane] = mx;
-  ps[w * 64 + lane] = sum;
-  __syncthreads();
-  if (qi >= n) return;
-  float M = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) M = fmaxf(M, pm[u * 64 + lane]);
-  float f[4], L = 0.f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    f[u] = expf(pm[u * 64 + lane] - M);  // all keys padded: M = -inf -> NaN, as the reference's softmax
-    L += ps[u * 64 + lane] * f[u];
-  }
-  float* o = O + ((size_t)b * n + qi) * D + h * DK + w * DS;
-#pragma unroll
-  for (int d = 0; d < DS; ++d) {
-    float a = 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) a += pa[(u * DK + w * DS + d) * 64 + lane] * f[u];
-    o[d] = a / L;
-  }
-}
-
-// ------------------------------------------------------------------ epilogues
-
-// (acc + bias) + residual  (fc(out) + residual, SubLayers.py:54-55; w_2(...) + residual, :91-93)
-struct EpiBiasRes {
-  const float* __restrict__ bias;
-  const float* __restrict__ res;
-  float* __restrict__ out;
-  int ldo;
-  static constexpr bool kRowStats = false;
-  static constexpr int stat_rows(int) { return 0; }
-  __device__ void prologue(int, int, int, float*) const {}
-  __device__ float value(int m, int n, float acc, const float*, int) const {
-    return (acc + bias[n]) + res[(size_t)m * ldo + n];
-  }
-  __device__ void store(int m, int n, float v) const { out[(size_t)m * ldo + n] = v; }
-  __device__ void store4(int m, int n, const float* v) const { store_val4<float>(out + (size_t)m * ldo + n, v); }
-  __device__ void store_stats(int, int, float, float) const {}
-};
-
 // bridge(x) + position_enc[l] of the shared decoder (prior_generator.py:167 + Models.py:156-158)
 struct EpiBiasPos {
   const float* __restrict__ bias;
@@ -314,17 +136,6 @@ struct FftStack {
   std::vector<FftLayer> layers;
 };
 
-struct PriorGraph {
-  hipGraphExec_t exec = nullptr;
-  hipStream_t cap = nullptr;
-  std::vector<const void*> key;
-  void release() {
-    if (exec) (void)hipGraphExecDestroy(exec);
-    if (cap) (void)hipStreamDestroy(cap);
-    *this = PriorGraph();
-  }
-};
-
 struct Prior {
   int n_sym = 0, vocab = 0, nq = 0;
   int device = -1;
@@ -335,7 +146,7 @@ struct Prior {
   const float *src_emb = nullptr, *bridge_w = nullptr, *bridge_b = nullptr, *code_emb = nullptr;
   const float *prompt_emb = nullptr, *target_emb = nullptr, *q_emb = nullptr, *head_w = nullptr, *head_b = nullptr;
   int head_n = 0;  // padded head rows (multiple of 64)
-  PriorGraph genc, gdec;
+  CapGraph genc, gdec;
 };
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -369,35 +180,6 @@ static size_t prior_ws_layout(const Prior* p, int B, int L, int T, int P, void* 
   }
   if (w) *w = PriorWs{(float*)q[0], (float*)q[1], (float*)q[2], (float*)q[3], (float*)q[4], (float*)q[5], (uint8_t*)q[6]};
   return off;
-}
-
-template <int D>
-static int launch_ln(const float* R, const float* g, const float* b, const uint8_t* mask, float* X, int M, int n,
-                     float* embs, int P, int T, int nq, int q, hipStream_t st) {
-  hipLaunchKernelGGL(ln_mask_kernel<D>, dim3((M + 3) / 4), dim3(256), 0, st, R, g, b, mask, X, M, n, embs, P, T, nq, q);
-  FL_LAUNCH_CHECK();
-  return kOk;
-}
-static int ln_mask(int D, const float* R, const float* g, const float* b, const uint8_t* mask, float* X, int M, int n,
-                   float* embs, int P, int T, int nq, int q, hipStream_t st) {
-  switch (D) {
-    case 192: return launch_ln<192>(R, g, b, mask, X, M, n, embs, P, T, nq, q, st);
-    case 256: return launch_ln<256>(R, g, b, mask, X, M, n, embs, P, T, nq, q, st);
-    case 384: return launch_ln<384>(R, g, b, mask, X, M, n, embs, P, T, nq, q, st);
-    default: FL_REQUIRE(false, "prior: unsupported model width %d", D);
-  }
-}
-static int attention(int DK, const float* QKV, const uint8_t* mask, int B, int n, int D, int H, float* O, hipStream_t st) {
-  // temperature = np.power(d_k, 0.5) (SubLayers.py:21), applied as a division (Modules.py:17)
-  const float temp = (float)std::sqrt((double)DK);
-  dim3 grid((n + 63) / 64, H, B);
-  switch (DK) {
-    case 32: hipLaunchKernelGGL(attn_kernel<32>, grid, dim3(256), 0, st, QKV, mask, n, D, temp, O); break;
-    case 48: hipLaunchKernelGGL(attn_kernel<48>, grid, dim3(256), 0, st, QKV, mask, n, D, temp, O); break;
-    default: FL_REQUIRE(false, "prior: unsupported head width %d", DK);
-  }
-  FL_LAUNCH_CHECK();
-  return kOk;
 }
 
 // One FFTBlock stack (Models.py:94-98 / :160-169) in place on X (M = B*n rows).  `embs` (decoders): the
@@ -456,27 +238,6 @@ static int run_decode(Prior* p, const float* x, const uint8_t* tmask, const int6
   // code head over (B, nq, T) rows, masked and permuted (:186-188)
   return launch_gemm<float>(LoadF32<float>{embs, D}, p->head_w, D, EpiHead{p->head_b, tmask, logits, p->vocab + 1, nq, T},
                             B * nq * T, p->head_n, D, st);
-}
-
-template <class F>
-static int with_graph(PriorGraph& g, const std::vector<const void*>& key, bool use_graph, hipStream_t st, F&& body) {
-  if (!use_graph) return body(st);
-  if (!g.exec || g.key != key) {
-    if (g.exec) { FL_HIP(hipGraphExecDestroy(g.exec)); g.exec = nullptr; }
-    if (!g.cap) FL_HIP(hipStreamCreateWithFlags(&g.cap, hipStreamNonBlocking));
-    FL_HIP(hipStreamBeginCapture(g.cap, hipStreamCaptureModeRelaxed));
-    int r = body(g.cap);
-    hipGraph_t gr = nullptr;
-    hipError_t e = hipStreamEndCapture(g.cap, &gr);
-    if (r) { if (gr) (void)hipGraphDestroy(gr); return r; }
-    FL_HIP(e);
-    hipError_t ie = hipGraphInstantiate(&g.exec, gr, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(gr);
-    FL_HIP(ie);
-    g.key = key;
-  }
-  FL_HIP(hipGraphLaunch(g.exec, st));
-  return kOk;
 }
 
 }  // namespace fl

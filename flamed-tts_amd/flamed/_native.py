@@ -64,6 +64,12 @@ SIGNATURES = {
     "flamed_enc_out_len": (c_int, [P, c_int]),
     "flamed_enc_workspace_size": (c_size_t, [P, c_int, c_int]),
     "flamed_enc_encode": (c_int, [P, P, c_int, c_int, P, P, c_size_t, c_int, P]),
+    "flamed_vq_create": (c_int, [ctypes.POINTER(c_int), c_int, ctypes.POINTER(P)]),
+    "flamed_vq_destroy": (c_int, [P]),
+    "flamed_vq_num_weights": (c_int, [P]),
+    "flamed_vq_load": (c_int, [P, ctypes.POINTER(P), c_int, P]),
+    "flamed_vq_workspace_size": (c_size_t, [P, c_int, c_int]),
+    "flamed_vq_encode": (c_int, [P, P, c_int, c_int, P, P, P, P, P, c_size_t, c_int, P]),
     "flamed_prior_create": (c_int, [ctypes.POINTER(c_int), c_int, ctypes.POINTER(P)]),
     "flamed_prior_destroy": (c_int, [P]),
     "flamed_prior_num_weights": (c_int, [P]),

@@ -144,6 +144,7 @@ class FACodecEncoder(nn.Module):
         self.hip_dtype = "f32"
         self.hip_graph = True
         self._hip = None
+        self._vq_hip = None
         for m in self.modules():
             if isinstance(m, nn.Conv1d):
                 nn.init.trunc_normal_(m.weight, std=0.02)
@@ -153,6 +154,8 @@ class FACodecEncoder(nn.Module):
         """Force the next HIP call to re-pack the weights (load_state_dict does this by itself)."""
         if self._hip is not None:
             self._hip._sig = None
+        if self._vq_hip is not None:
+            self._vq_hip._sig = None
 
     def _load_from_state_dict(self, *args, **kwargs):
         self.hip_invalidate()  # load_state_dict copies in place: same pointers, maybe no version bump
@@ -160,6 +163,13 @@ class FACodecEncoder(nn.Module):
 
     def _use_hip(self, x):
         return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+
+    def _vq_hip_ok(self, x, n_quantizers):
+        """The HIP prompt path covers the eval quantizers with every layer and the non-conditional timbre
+        encoder; anything else (training, n_quantizers < all, use_cln) stays on the torch modules."""
+        te = self.timbre_encoder
+        full = n_quantizers is None or all(n_quantizers >= q.num_quantizers for q in self.quantizer)
+        return self._use_hip(x) and full and not self.quantizer.training and not te.use_cln
 
     def forward(self, x):
         """waveform (B, 1, n) -> (B, out_channels, T) (reference :215-217)."""
@@ -241,6 +251,7 @@ class FACodecDecoder(nn.Module):
         self.hip_dtype = "bf16"
         self.hip_graph = True
         self._hip = None
+        self._vq_hip = None
         for m in self.modules():
             if isinstance(m, nn.Conv1d):
                 nn.init.trunc_normal_(m.weight, std=0.02)
@@ -256,6 +267,8 @@ class FACodecDecoder(nn.Module):
         """Force the next HIP call to re-pack the weights (load_state_dict does this by itself)."""
         if self._hip is not None:
             self._hip._sig = None
+        if self._vq_hip is not None:
+            self._vq_hip._sig = None
 
     def _load_from_state_dict(self, *args, **kwargs):
         self.hip_invalidate()  # load_state_dict copies in place: same pointers, maybe no version bump
@@ -263,6 +276,13 @@ class FACodecDecoder(nn.Module):
 
     def _use_hip(self, x):
         return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+
+    def _vq_hip_ok(self, x, n_quantizers):
+        """The HIP prompt path covers the eval quantizers with every layer and the non-conditional timbre
+        encoder; anything else (training, n_quantizers < all, use_cln) stays on the torch modules."""
+        te = self.timbre_encoder
+        full = n_quantizers is None or all(n_quantizers >= q.num_quantizers for q in self.quantizer)
+        return self._use_hip(x) and full and not self.quantizer.training and not te.use_cln
 
     def quantize(self, x, n_quantizers=None):
         """prosody and content RVQs on x, residual RVQ on x - (prosody + content) (reference :470-507)."""
@@ -287,6 +307,12 @@ class FACodecDecoder(nn.Module):
                                       "which this build does not implement")
         if eval_vq:
             self.quantizer.eval()
+        if self._vq_hip_ok(x, n_quantizers):
+            if self._vq_hip is None:
+                self._vq_hip = VqHIP(self)
+            outs, qs, qb, spk = ops.vq_encode(self._vq_hip.oid, x)
+            commit_loss = torch.zeros(qs.shape[0], device=x.device)
+            return outs, qs, commit_loss, list(qb.unbind(0)), spk
         outs, qs, commit_loss, qbuf = self.quantize(x, n_quantizers=n_quantizers)
         spk = self.timbre_encoder(x.transpose(1, 2), None, None).transpose(1, 2).mean(dim=2)
         return outs, qs, commit_loss, qbuf, spk
@@ -484,3 +510,92 @@ class EncoderHIP:
         nat.check(L.flamed_enc_encode(self.handle, nat.ptr(bufs["x"]), B, n, nat.ptr(bufs["out"]), nat.ptr(ws), ws.numel(),
                                       int(bool(self.enc.hip_graph)), nat.stream_ptr(dev)), "flamed_enc_encode")
         return bufs["out"].clone()
+
+
+def vq_weight_list(dec: FACodecDecoder) -> List[torch.Tensor]:
+    """Weights in the order flamed_vq_load expects (include/flamed_hip.h)."""
+    w = []
+    for rvq in dec.quantizer:
+        for ly in rvq.layers:
+            w += [ly.in_proj.weight_g, ly.in_proj.weight_v, ly.in_proj.bias, ly.out_proj.weight_g,
+                  ly.out_proj.weight_v, ly.out_proj.bias, ly._codebook.weight]
+    te = dec.timbre_encoder
+    w.append(te.position_emb.pe)
+    for ly in te.layers:
+        a = ly.self_attn
+        w += [ly.ln_1.weight, ly.ln_1.bias, a.in_proj_weight, a.in_proj_bias, a.out_proj.weight, a.out_proj.bias,
+              ly.ln_2.weight, ly.ln_2.bias, ly.ffn.ffn_1.weight, ly.ffn.ffn_1.bias, ly.ffn.ffn_2.weight,
+              ly.ffn.ffn_2.bias]
+    return w + [te.last_ln.weight, te.last_ln.bias]
+
+
+class VqHIP:
+    """Owns one flamed_vq_t handle: the prompt-side quantizers + timbre encoder of a FACodecDecoder
+    (FACodecDecoder.forward(vq=True), reference facodec.py:470-533)."""
+
+    def __init__(self, dec: FACodecDecoder):
+        self.dec = dec
+        self.handle = None
+        self._sig = None
+        self.ws = nat.Workspace()
+        self._bufs = {}
+        self.oid = ops.register(self)  # torch.ops.flamed_hip.vq_encode
+
+    def __del__(self):
+        try:
+            if self.handle is not None:
+                nat.lib().flamed_vq_destroy(self.handle)
+        except Exception:
+            pass
+
+    def dims(self) -> List[int]:
+        d = self.dec
+        te = d.timbre_encoder
+        nl = [len(q.layers) for q in d.quantizer]
+        ks = [q.layers[0]._codebook.weight.shape[0] for q in d.quantizer]
+        fvq = d.quantizer[0].layers[0]
+        return [fvq.in_proj.weight_v.shape[1], fvq.codebook_dim, len(nl), *nl, *ks, te.encoder_hidden, te.encoder_head, te.conv_filter_size,
+                te.conv_kernel_size, len(te.layers), te.position_emb.pe.shape[0]]
+
+    def _ensure(self, dev):
+        params = vq_weight_list(self.dec)
+        sig = tuple((p.data_ptr(), nat.tensor_version(p)) for p in params) + (str(dev),)
+        if sig == self._sig and self.handle is not None:
+            return
+        L = nat.lib()
+        if self.handle is None:
+            h = ctypes.c_void_p()
+            d = self.dims()
+            nat.check(L.flamed_vq_create((ctypes.c_int * len(d))(*d), len(d), ctypes.byref(h)), "flamed_vq_create")
+            self.handle = h
+        keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
+        arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
+        nat.check(L.flamed_vq_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_vq_load")
+        torch.cuda.current_stream(dev).synchronize()  # the arena copies read `keep`
+        self._sig = sig
+        self._bufs = {}
+
+    def encode(self, x: torch.Tensor):
+        """x (B, C, T) encoder output -> (outs (B, C, T), codes (n_q, B, T) int64, per-group quantized sums
+        (G, B, C, T), speaker embedding (B, C))."""
+        dev = x.device
+        self._ensure(dev)
+        B, C, T = x.shape
+        G = len(self.dec.quantizer)
+        nq = sum(len(q.layers) for q in self.dec.quantizer)
+        key = (B, C, T)
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            bufs = {"x": torch.empty((B, C, T), dtype=torch.float32, device=dev),
+                    "outs": torch.empty((B, C, T), dtype=torch.float32, device=dev),
+                    "codes": torch.empty((nq, B, T), dtype=torch.int64, device=dev),
+                    "qbuf": torch.empty((G, B, C, T), dtype=torch.float32, device=dev),
+                    "spk": torch.empty((B, C), dtype=torch.float32, device=dev)}
+            self._bufs = {key: bufs}
+        bufs["x"].copy_(x)
+        L = nat.lib()
+        ws = self.ws.get(L.flamed_vq_workspace_size(self.handle, B, T), dev)
+        nat.check(L.flamed_vq_encode(self.handle, nat.ptr(bufs["x"]), B, T, nat.ptr(bufs["outs"]), nat.ptr(bufs["codes"]),
+                                     nat.ptr(bufs["qbuf"]), nat.ptr(bufs["spk"]), nat.ptr(ws), ws.numel(),
+                                     int(bool(self.dec.hip_graph)), nat.stream_ptr(dev)), "flamed_vq_encode")
+        return tuple(bufs[k].clone() for k in ("outs", "codes", "qbuf", "spk"))

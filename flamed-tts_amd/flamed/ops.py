@@ -4,7 +4,7 @@ Every hot-path entry point the modules dispatch to on ROCm is registered as a Py
 `flamed_hip` namespace, so the calls are visible to the dispatcher: `torch.compile` (dynamo traces them
 as single opaque nodes instead of graph-breaking on ctypes), FakeTensor / meta shape propagation, and
 `torch.library.opcheck`.  The ops are thin: the work is done by the per-module owner objects
-(`DenoiserHIP`, `CondFoldHIP`, `PvaHIP`, `FacDecoderHIP`, `EncoderHIP`, `PriorHIP`), which own the native handles and
+(`DenoiserHIP`, `CondFoldHIP`, `PvaHIP`, `FacDecoderHIP`, `EncoderHIP`, `VqHIP`, `PriorHIP`), which own the native handles and
 their device-resident weight arenas.  An owner is passed to an op by an integer id (custom-op schemas
 take tensors and scalars only); the registry holds weak references, so a dropped module frees its handle.
 
@@ -16,6 +16,7 @@ take tensors and scalars only); the registry holds weak references, so a dropped
   flamed_hip::length_regulate(x, pd, sd, lens, max_len, log_domain)  LengthRegulator.LR  pva.py:125-166
   flamed_hip::fac_decode(id, x, spk)               FACodecDecoder.inference        facodec.py:630-638
   flamed_hip::enc_encode(id, x)                    FACodecEncoder.forward          facodec.py:158-243
+  flamed_hip::vq_encode(id, x)                     FACodecDecoder.forward(vq=True) facodec.py:470-533
   flamed_hip::prior_encode(id, texts, mask)        Encoder.forward (prior)         prior_generator.py:152-153
   flamed_hip::prior_decode(id, x, mask, prompts, P) bridge + decoders + head       prior_generator.py:165-188
 
@@ -139,6 +140,20 @@ def _(oid, x):
     return x.new_empty((B, o.enc.out_channels, o.out_len(n)), dtype=torch.float32)
 
 
+@torch.library.custom_op("flamed_hip::vq_encode", mutates_args=())
+def vq_encode(oid: int, x: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    return owner(oid).encode(x)
+
+
+@vq_encode.register_fake
+def _(oid, x):
+    B, C, T = x.shape
+    q = owner(oid).dec.quantizer
+    nq = sum(len(r.layers) for r in q)
+    return (x.new_empty((B, C, T)), x.new_empty((nq, B, T), dtype=torch.int64), x.new_empty((len(q), B, C, T)),
+            x.new_empty((B, C)))
+
+
 # ---------------------------------------------------------------- prior transformer stack
 
 @torch.library.custom_op("flamed_hip::prior_encode", mutates_args=())
@@ -166,4 +181,4 @@ def _(oid, x, tgt_mask, prompts, prompts_len):
 
 
 OPS = ("den_velocity", "den_solve", "cond_fold", "pva_flow", "length_regulate", "fac_decode", "enc_encode",
-       "prior_encode", "prior_decode")
+       "vq_encode", "prior_encode", "prior_decode")

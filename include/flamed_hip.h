@@ -292,6 +292,31 @@ FLAMED_API int flamed_prior_decode(flamed_prior_t h, const float* x, const uint8
                                    int B, int T, int P, const float* pos, float* embs, float* logits, void* ws,
                                    size_t ws_bytes, int use_graph, hipStream_t stream);
 
+/* ============== prompt-side quantizers + timbre encoder (once per prompt) ==============
+ * Replaces FACodecDecoder.forward(vq=True) (facodec.py:470-533) after the encoder
+ * conv stack: the prosody / content / residual ResidualVQs of FactorizedVectorQuantize layers
+ * (quantize/rvq.py:27-73, quantize/fvq.py:35-116) and the timbre TransformerEncoder (pre-LN,
+ * facodec/transformer.py:154-234) averaged over time.  Exact fp32; codes = argmax like the reference.
+ * dims (3 + 2G + 6 ints): C (vq_dim, 256), codebook_dim (8), G (groups), layers[G], codebook sizes[G],
+ *   timbre {hidden (= C), heads, conv_filter, kernel, layers, position-table rows}.
+ * Weight order for flamed_vq_load (fp32 device tensors, prefix of the FACodecDecoder):
+ *   for each group g, layer l: quantizer.g.layers.l.{in_proj.weight_g, in_proj.weight_v, in_proj.bias,
+ *     out_proj.weight_g, out_proj.weight_v, out_proj.bias, _codebook.weight};
+ *   timbre_encoder.position_emb.pe; per layer: ln_1.{weight,bias}, self_attn.{in_proj_weight,
+ *     in_proj_bias}, self_attn.out_proj.{weight,bias}, ln_2.{weight,bias}, ffn.ffn_1.{weight,bias},
+ *     ffn.ffn_2.{weight,bias}; timbre_encoder.last_ln.{weight,bias}.
+ * Weight norm is folded and the codebooks normalised at load, into the handle's arena. */
+typedef struct flamed_vq_s* flamed_vq_t;
+FLAMED_API int flamed_vq_create(const int* dims, int n_dims, flamed_vq_t* out);
+FLAMED_API int flamed_vq_destroy(flamed_vq_t h);
+FLAMED_API int flamed_vq_num_weights(flamed_vq_t h);
+FLAMED_API int flamed_vq_load(flamed_vq_t h, const float* const* weights, int n_weights, hipStream_t stream);
+FLAMED_API size_t flamed_vq_workspace_size(flamed_vq_t h, int B, int T);
+/* x (B, C, T) encoder output -> outs (B, C, T) summed quantized, codes (n_layers, B, T) int64,
+ * qbuf (G, B, C, T) per-group quantized sums, spk (B, C) speaker embedding. */
+FLAMED_API int flamed_vq_encode(flamed_vq_t h, const float* x, int B, int T, float* outs, int64_t* codes, float* qbuf,
+                                float* spk, void* ws, size_t ws_bytes, int use_graph, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

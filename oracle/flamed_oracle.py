@@ -387,7 +387,7 @@ def _wn_linear(sd: SD, p: str, x: torch.Tensor) -> torch.Tensor:
     return F.linear(x, wn_weight(sd, p), sd[p + ".bias"])
 
 
-def fvq_quantize(sd: SD, p: str, z: torch.Tensor):
+def fvq_quantize(sd: SD, p: str, z: torch.Tensor, gaps: Optional[list] = None):
     """FactorizedVectorQuantize.forward (eval), fvq.py:35-87 + decode_latents :102-116.
     z (B,D,T) -> (z_q (B,D,T), indices (B,T) int64).  Nearest code under L2-normalised euclidean
     distance (first index on ties, as torch.max), straight-through `z_e + (z_q - z_e)` kept."""
@@ -398,16 +398,19 @@ def fvq_quantize(sd: SD, p: str, z: torch.Tensor):
     cb = F.normalize(cb_raw)
     dist = e.pow(2).sum(1, keepdim=True) - 2 * e @ cb.t() + cb.pow(2).sum(1, keepdim=True).t()
     idx = (-dist).max(1)[1].reshape(B, T)
+    if gaps is not None:  # top-2 distance gap per frame (test diagnostics: near-ties)
+        top2 = torch.topk(-dist, 2, dim=1).values
+        gaps.append((top2[:, 0] - top2[:, 1]).reshape(B, T))
     z_q = cb_raw[idx]                                                               # (B,T,d)
     z_q = z_e + (z_q - z_e)
     return _wn_linear(sd, p + ".out_proj", z_q).transpose(1, 2), idx
 
 
-def rvq_quantize(sd: SD, p: str, x: torch.Tensor, n_layers: int):
+def rvq_quantize(sd: SD, p: str, x: torch.Tensor, n_layers: int, gaps: Optional[list] = None):
     """ResidualVQ.forward (eval), rvq.py:27-76.  Returns (sum, indices (n,B,T), quantized (n,B,D,T))."""
     out, res, idx, qs = 0.0, x, [], []
     for i in range(n_layers):
-        q, ind = fvq_quantize(sd, f"{p}.layers.{i}", res)
+        q, ind = fvq_quantize(sd, f"{p}.layers.{i}", res, gaps)
         res = res - q
         out = out + q
         idx.append(ind)
@@ -447,15 +450,15 @@ def timbre_encoder(sd: SD, x: torch.Tensor, p: str = "timbre_encoder", n_layers:
     return F.layer_norm(x, (d,), sd[p + ".last_ln.weight"], sd[p + ".last_ln.bias"], 1e-5)
 
 
-def decoder_vq(sd: SD, x: torch.Tensor, n_q=(1, 2, 3)):
+def decoder_vq(sd: SD, x: torch.Tensor, n_q=(1, 2, 3), gaps: Optional[list] = None):
     """FACodecDecoder.forward(vq=True) (eval), facodec.py:470-530.  x (B,C,T) encoder output ->
     (codes (sum n_q, B, T) int64 in [prosody, content, residual] order, spk (B,C)).  The residual RVQ
     sees x - (sum of prosody layers + sum of content layers) (:495-497)."""
-    _, ip, qp = rvq_quantize(sd, "quantizer.0", x, n_q[0])
-    _, ic, qc = rvq_quantize(sd, "quantizer.1", x, n_q[1])
+    _, ip, qp = rvq_quantize(sd, "quantizer.0", x, n_q[0], gaps)
+    _, ic, qc = rvq_quantize(sd, "quantizer.1", x, n_q[1], gaps)
     codes = [ip, ic]
     if n_q[2] > 0:
-        _, ir, _ = rvq_quantize(sd, "quantizer.2", x - (qp.sum(0) + qc.sum(0)), n_q[2])
+        _, ir, _ = rvq_quantize(sd, "quantizer.2", x - (qp.sum(0) + qc.sum(0)), n_q[2], gaps)
         codes.append(ir)
     spk = timbre_encoder(sd, x.transpose(1, 2)).transpose(1, 2).mean(dim=2)
     return torch.cat(codes, dim=0), spk

@@ -71,3 +71,36 @@ def test_encode_bf16_and_graph(enc):
         ref_bf16 = orc.facodec_encode(seeded("facodec_encoder"), t32(g["wav"])).float()
     e_ref = rel_l2(ref_bf16, g["enc_out"])
     assert rel_l2(z_graph.cpu(), g["enc_out"]) < 1.122 * max(e_ref, 1e-3)
+
+
+@pytest.mark.parametrize("B,T", [(2, 240), (1, 37)])
+def test_vq_timbre_vs_oracle(B, T):
+    """Prompt-side RVQ codes + timbre speaker embedding on HIP (flamed_vq_encode) vs the oracle
+    (decoder_vq: facodec.py:470-533) on random encoder outputs.  Codes bit-exact except where the
+    oracle's top-2 distance gap is below 1e-5 (counted; fp32 summation-order ties), spk rel-L2 <= 1e-4;
+    quantized sums vs the module's own torch path on CPU."""
+    from _flamed_common import build_flamed
+    _, dec = build_flamed(DEV, "f32")
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    x = torch.randn(B, 256, T, generator=torch.Generator().manual_seed(11))
+    with torch.inference_mode():
+        outs, codes, _, qb, spk = dec(x.to(DEV), eval_vq=False, vq=True)
+        gaps = []
+        rc, rspk = orc.decoder_vq(sd, x, gaps=gaps)
+        dec_cpu = dec.to("cpu")
+        couts, ccodes, _, cqb, cspk = dec_cpu(x, eval_vq=False, vq=True)
+        dec.to(DEV)
+    assert dec._vq_hip is not None and dec._vq_hip.handle is not None  # the HIP path ran
+    codes = codes.cpu()
+    assert codes.shape == rc.shape
+    near = torch.stack(gaps) < 1e-5  # (n_q, B, T) near-ties of the oracle's own distances
+    neq = codes != rc
+    # a mismatch in one layer changes every later residual of that group: only frames whose first
+    # mismatch sits on a near-tie are excused
+    first = neq.float().cumsum(0) == 1
+    assert bool((near | ~(neq & first)).all()), "code mismatch away from a near-tie"
+    assert rel_l2(spk.cpu(), rspk) < 1e-4
+    if not bool(neq.any()):
+        assert rel_l2(outs.cpu(), couts) < 1e-4
+        for a, b in zip(qb, cqb):
+            assert rel_l2(a.cpu(), b) < 1e-4

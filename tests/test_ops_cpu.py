@@ -64,6 +64,11 @@ def test_fake_shapes():
         assert w.shape == (1, 1, 8000)
         e = torch.ops.flamed_hip.enc_encode(eid, torch.empty(1, 1, 48000))
         assert e.shape == (1, 256, 240)
+        vq = types.SimpleNamespace(quantizer=[types.SimpleNamespace(layers=[0] * n) for n in (1, 2, 3)])
+        vo, void = _dummy_owner(dec=vq)
+        outs, codes, qb, spk = torch.ops.flamed_hip.vq_encode(void, torch.empty(2, 256, 30))
+        assert outs.shape == (2, 256, 30) and codes.shape == (6, 2, 30) and codes.dtype == torch.int64
+        assert qb.shape == (3, 2, 256, 30) and spk.shape == (2, 256)
         ppg = types.SimpleNamespace(encoder=types.SimpleNamespace(d_model=192), prior_decoder=[None] * 6,
                                     shared_decoder=types.SimpleNamespace(d_model=384),
                                     head=types.SimpleNamespace(weight=torch.empty(1025, 384)))
