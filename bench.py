@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--g8p-rows", type=int, default=None, help="flamed_tune g8p_rows (256x256 8-phase GEMM tiles from this many rows; 0 off)")
     ap.add_argument("--dwgn", type=int, default=None, help="flamed_tune dwgn (large-M whole-utterance depthwise conv + GroupNorm kernel)")
     ap.add_argument("--dwgn-small", type=int, default=None, help="flamed_tune dwgn_small (small-M one-workgroup depthwise conv + GroupNorm)")
+    ap.add_argument("--fuse-euler", type=int, default=None, help="flamed_tune fuse_euler (combine + Euler update in the next proj_in)")
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
@@ -80,7 +81,8 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fold: bool | None = None):
+def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fold: bool | None = None,
+                 fused: bool = False):
     """Algorithmic (bytes, flops) per launch of each kernel class, and launches per Euler step.
     Bytes = every operand read once + every output written once.  With the
     LayerNorm fold (bf16 default) conv_3 also writes x*alpha in bf16 and mlp.0 / conv_out read it
@@ -93,6 +95,8 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fol
     TS = (T + 63) // 64
     stats = M * NT * 8
     if cls == 0:
+        if fused:  # + the previous step's tap combine + Euler update in the loader: Y read, x_s written
+            return M * C * 4 + M * 3 * C * 4 + M * C * 4 + H * C * es + M * H * 4 + stats, 2 * M * H * C + 4 * M * C, 1
         return M * C * 4 + H * C * es + M * H * 4 + stats, 2 * M * H * C, 1
     if cls == 1:
         return M * H * 4 + stats + M * H * 4 + B * TS * H * 12, 2 * 31 * M * H, NB + 1
@@ -353,16 +357,17 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
                                                   nat.stream_ptr(dev)), "flamed_den_time_kernels_graph")
         torch.cuda.synchronize()
     es = 2 if args.dtype == "bf16" else 4
+    fused = ms[N_CLASSES - 1] <= 0.0  # no combine launches: fused into proj_in (small M only)
     ks = []
     for cls in range(N_CLASSES):
-        if cls == 2 and ms[cls] <= 0.0:
+        if (cls == 2 or cls == N_CLASSES - 1) and ms[cls] <= 0.0:
             continue
-        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es, fused=fused)
         t = max(ms[cls], 1e-6) * 1e-3
         ks.append({"name": KERNEL_NAMES[cls], "us": round(ms[cls] * 1e3, 2), "per_step": per_step,
                    "GBps": round(nbytes / t / 1e9, 1), "TFLOPs": round(flops / t / 1e12, 2)})
     dom = max(ks, key=lambda k: k["us"] * k["per_step"])
-    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es)
+    nbytes, flops, _ = kernel_costs(KERNEL_NAMES.index(dom["name"]), B, T, H, C, NB, es, fused=fused)
     ridge = MFMA_PEAK_TFS[args.dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
     if flops / nbytes > ridge:
         roof = {"bound": "mfma", "achieved": dom["TFLOPs"], "peak": MFMA_PEAK_TFS[args.dtype], "unit": "TFLOP/s"}
@@ -396,7 +401,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")
@@ -457,10 +462,15 @@ def main():
                                                   args.kernel_iters, ms, nat.stream_ptr(dev)), "flamed_den_time_kernels_graph")
         torch.cuda.synchronize()
     es = 2 if args.dtype == "bf16" else 4
+    # small-M solve graphs fuse the conv_out combine + Euler update into the next proj_in (flamed_tune
+    # fuse_euler; 25 launches per step): the timing graph then has no combine launches (class cost 0)
+    fused = ms[N_CLASSES - 1] <= 0.0
     kernels = []
     for cls in range(N_CLASSES):
-        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es)
+        nbytes, flops, per_step = kernel_costs(cls, B, T, H, C, NB, es, fused=fused)
         if cls == 2 and ms[cls] <= 0.0:  # GroupNorm finalize fused into class 1 (the last-arriving block)
+            continue
+        if cls == N_CLASSES - 1 and fused:  # combine + Euler update fused into the next step's proj_in
             continue
         t = max(ms[cls], 1e-6) * 1e-3
         kernels.append({"name": KERNEL_NAMES[cls], "us": round(ms[cls] * 1e3, 2), "per_step": per_step,

@@ -83,6 +83,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"g8p_rows", &Tune::g8p_rows, 0, 1 << 30, nullptr},
       {"dwgn", &Tune::dwgn, 0, 1, nullptr},
       {"dwgn_small", &Tune::dwgn_small, 0, 1, nullptr},
+      {"fuse_euler", &Tune::fuse_euler, 0, 1, nullptr},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(k.name, key) != 0) continue;

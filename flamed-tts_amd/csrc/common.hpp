@@ -123,6 +123,7 @@ struct Tune {
   int g8p_rows = 16384;    // large-M GEMMs from this many rows on 256 x 256 8-phase tiles (0 = off)
   int dwgn = 1;            // large-M path: whole-utterance depthwise conv + GroupNorm kernel (T <= 512)
   int dwgn_small = 1;      // small-M bf16 path: one-workgroup-per-8-channels depthwise conv + GroupNorm (T <= 576)
+  int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)
 Tune tune_snapshot(int* epoch);                       // process defaults + their epoch

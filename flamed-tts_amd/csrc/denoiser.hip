@@ -1164,8 +1164,10 @@ struct LoadGN {
 
 // FinalLayer conv_out (k=3, pad=1) from the tap-stacked GEMM Y[m] = [W_0; W_1; W_2] x_mod[m]:
 // v[t] = b + Y0[t-1] + Y1[t] + Y2[t+1] within each utterance; then xt += dt*v (or v_out = v).
+// `src` (null: xt itself) is the state the update starts from (the fused solve's last step).
 __global__ void conv3_combine_kernel(const float* __restrict__ Y, const float* __restrict__ bias, float* xt,
-                                     float* __restrict__ vout, int M, int T, int C, float dt, int* step_ctr) {
+                                     float* __restrict__ vout, int M, int T, int C, float dt, int* step_ctr,
+                                     const float* src = nullptr) {
   size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (step_ctr && idx == 0) *step_ctr += 1;  // last kernel of the step; nothing in it reads the counter
   if (idx >= (size_t)M * C) return;
@@ -1178,8 +1180,80 @@ __global__ void conv3_combine_kernel(const float* __restrict__ Y, const float* _
   if (vout) {
     vout[idx] = v;
   } else {
-    xt[idx] = __fadd_rn(xt[idx], __fmul_rn(dt, v));
+    xt[idx] = __fadd_rn((src ? src : xt)[idx], __fmul_rn(dt, v));
   }
+}
+
+// Fused solve (small M, graph path): the conv_out tap combine + Euler update of step s-1 is computed
+// inside step s's proj_in A loader, exactly as conv3_combine_kernel does it (same fp32 operation order,
+// so the solve stays bitwise equal to the eager one):  x_s = x_{s-1} + dt * (b + Y1[t] + Y0[t-1] +
+// Y2[t+1]).  The state ping-pongs between two buffers (src = x_{s-1}, dst = x_s, written once by the
+// column-tile-0 workgroups while every column tile reads src); the loader's prologue advances the step
+// counter (nothing in proj_in reads it).  Step 0 starts from euler_init_kernel's image: src = x_0,
+// Y1 = -b, Y0 = Y2 = 0, so v = b + (-b) = 0 exactly and x_0 passes through.
+template <typename DT>
+struct LoadEulerIn {
+  const float* __restrict__ src;
+  float* dst;
+  const float* __restrict__ Y;
+  const float* __restrict__ bias;
+  int* ctr;
+  float dt;
+  int T, C;
+  static constexpr int EPC = DTraits<DT>::EPC;
+  static constexpr int kSrcBytes = 4;
+  struct Raw { float x[EPC], b[EPC], y1[EPC], y0[EPC], y2[EPC]; int t; };
+  static constexpr int stat_rows(int) { return 0; }
+  __device__ void prologue(int, int, int, float*) const {
+    if (ctr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) *ctr += 1;
+  }
+  __device__ Raw issue(int m, int k) const {
+    Raw r;
+    r.t = m % T;
+    const size_t ld = 3 * (size_t)C;
+#pragma unroll
+    for (int j = 0; j < EPC; j += 4) {
+      float4 a = ld4(src + (size_t)m * C + k + j), b = ld4(bias + k + j), y1 = ld4(Y + (size_t)m * ld + C + k + j);
+      float4 y0 = r.t > 0 ? ld4(Y + (size_t)(m - 1) * ld + k + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 y2 = r.t < T - 1 ? ld4(Y + (size_t)(m + 1) * ld + 2 * C + k + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.x[j] = a.x; r.x[j + 1] = a.y; r.x[j + 2] = a.z; r.x[j + 3] = a.w;
+      r.b[j] = b.x; r.b[j + 1] = b.y; r.b[j + 2] = b.z; r.b[j + 3] = b.w;
+      r.y1[j] = y1.x; r.y1[j + 1] = y1.y; r.y1[j + 2] = y1.z; r.y1[j + 3] = y1.w;
+      r.y0[j] = y0.x; r.y0[j + 1] = y0.y; r.y0[j + 2] = y0.z; r.y0[j + 3] = y0.w;
+      r.y2[j] = y2.x; r.y2[j + 1] = y2.y; r.y2[j + 2] = y2.z; r.y2[j + 3] = y2.w;
+    }
+    return r;
+  }
+  template <typename D>
+  __device__ u32x4 finish(const Raw& r, int m, int k, const float*, int) const {
+    float o[EPC];
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) {
+      float v = r.b[j] + r.y1[j];
+      if (r.t > 0) v += r.y0[j];
+      if (r.t < T - 1) v += r.y2[j];
+      o[j] = __fadd_rn(r.x[j], __fmul_rn(dt, v));
+    }
+    if (blockIdx.x == 0) {
+#pragma unroll
+      for (int j = 0; j < EPC; j += 4)
+        *reinterpret_cast<float4*>(dst + (size_t)m * C + k + j) = make_float4(o[j], o[j + 1], o[j + 2], o[j + 3]);
+    }
+    return pack_chunk<D>(o);
+  }
+};
+
+// Fused solve start: src image x_0 and a conv_out output whose combine is exactly 0 (see LoadEulerIn).
+__global__ void euler_init_kernel(const float* __restrict__ xt, const float* __restrict__ bias, float* __restrict__ xs,
+                                  float* __restrict__ Y, int M, int C) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)M * C) return;
+  int m = idx / C, n = idx - (size_t)m * C;
+  xs[idx] = xt[idx];
+  float* y = Y + (size_t)m * 3 * C;
+  y[n] = 0.f;
+  y[C + n] = -bias[n];
+  y[2 * C + n] = 0.f;
 }
 
 // ------------------------------ AdaLN helpers ------------------------------
@@ -1540,6 +1614,7 @@ struct DenWs {
   size_t SLn;
   bf16* A16;   // large-M bf16 path: normalised A operand rows, M x H (null otherwise)
   bf16* XA;    // LayerNorm fold: X * alpha_next rows (bf16 handles), M x H
+  float* XP;   // fused solve: second Euler-state buffer, M x C
 };
 
 // split-K slab capacity: 32 x 64 tiles of the widest GEMM (max(H, 3C) columns) x 4 slices, small M only
@@ -1568,11 +1643,11 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
   const size_t sl = den_slab_floats(d, B, T);
   const size_t a16 = (d->dt == FLAMED_BF16 && M >= (size_t)tn().big_min_rows) ? 2 * M * d->H : 0;  // large-M path range
   const size_t xa = d->fold ? 2 * M * d->H : 0;
-  size_t sizes[11] = {xs * M * d->H, 8 * M * NTmax, 8 * M * NTmax, xs * M * d->H, es * M * d->H, 12 * B * TS * d->H,
-                      8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16, xa};
+  size_t sizes[12] = {xs * M * d->H, 8 * M * NTmax, 8 * M * NTmax, xs * M * d->H, es * M * d->H, 12 * B * TS * d->H,
+                      8 * (size_t)B * d->H, 12 * M * d->C, 4 * sl, a16, xa, 4 * M * d->C};
   size_t off = 0;
-  void* ptrs[11];
-  for (int i = 0; i < 11; ++i) {
+  void* ptrs[12];
+  for (int i = 0; i < 12; ++i) {
     ptrs[i] = base ? (char*)base + off : nullptr;
     off += align256(sizes[i]);
   }
@@ -1582,6 +1657,7 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
     w->SL = (float*)ptrs[8]; w->SLn = sl;
     w->A16 = a16 ? (bf16*)ptrs[9] : nullptr;
     w->XA = xa ? (bf16*)ptrs[10] : nullptr;
+    w->XP = (float*)ptrs[11];
   }
   return off;
 }
@@ -1859,7 +1935,7 @@ namespace fl {
 // mods + (*ctr) * B * MS and the last kernel increments it (graph replay of captured steps).
 template <typename DT, typename XT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
-                         const DenWs& w, int* ctr, hipStream_t st) {
+                         const DenWs& w, int* ctr, hipStream_t st, const float* xsrc) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const Tune& tu = tn();
   const StepOff so{tu.noctr ? nullptr : ctr, (long long)B * MS};
@@ -1905,7 +1981,17 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
 #define K_(cls, x) do { if (tu.stamp_class >= 0) stamp_select(cls, st); TRY(x); if (tu.dup_class == (cls)) TRY(x); } while (0)
-  K_(0, (den_gemm<DT>(cfg, false, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStatsT<false, XT>{d->bin, X, H, w.S0, NT}, M, H, C, st)));
+  // fused solve step (xsrc != null; small M only, den_fused_ok): the previous step's combine + Euler
+  // update is proj_in's A loader, and there is no combine launch at the end of the step
+  FL_REQUIRE(!xsrc || (!big && !vout), "den_step: fused Euler step needs the small-M path");
+  if (xsrc) {
+    const LoadEulerIn<DT> le{xsrc, xt, w.Y, d->bout, ctr, dt, T, C};
+    const EpiBiasStatsT<false, XT> ep{d->bin, X, H, w.S0, NT};
+    if (cfg == kCfgTiny) K_(0, (launch_gemm_cfg<32, 32, 3, DT>(le, (const DT*)d->win, C, ep, M, H, C, st)));
+    else K_(0, (launch_gemm_auto<DT>(cfg, le, (const DT*)d->win, C, ep, M, H, C, st)));
+  } else {
+    K_(0, (den_gemm<DT>(cfg, false, LoadF32<DT>{xt, C}, (const DT*)d->win, C, EpiBiasStatsT<false, XT>{d->bin, X, H, w.S0, NT}, M, H, C, st)));
+  }
   for (int i = 0; i < d->NB; ++i) {
     const DenBlockW& Bw = d->blk[i];
     const float* md = mods + (size_t)i * 6 * H;
@@ -1996,12 +2082,12 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
     K_(7, (den_gemm<DT>(cfg, true, LoadLNMod<DT, false>{w.X, H, w.S1, NT, BN, 1e-6f, mo, nullptr, nullptr, H, X16p}, (const DT*)d->wout, H,
                                         EpiBiasAct<float, 0>{nullptr, w.Y, 3 * C}, M, 3 * C, H, st)));
   }
-  {
+  if (!xsrc) {
     size_t n = (size_t)M * C;
-    hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, ctr);
+    hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, ctr, nullptr);
     FL_LAUNCH_CHECK();
     if (tu.dup_class == 8) {  // duplicate without a second counter increment
-      hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, nullptr);
+      hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, vout, M, T, C, dt, nullptr, nullptr);
       FL_LAUNCH_CHECK();
     }
   }
@@ -2011,14 +2097,24 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
 }
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
-                    hipStream_t st, int* ctr = nullptr) {
+                    hipStream_t st, int* ctr = nullptr, const float* xsrc = nullptr) {
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   if (d->dt == FLAMED_BF16) {
-    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
-    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc);
+    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc);
   }
-  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st);
+  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc);
+}
+
+// The fused Euler step (LoadEulerIn) runs where proj_in takes the small-M register loop with one
+// workgroup column per tile column (no XCD strip remap) and no split-K of its fp32-A GEMM; the large-M
+// path keeps the combine kernel.
+static bool den_fused_ok(const Den* d, int B, int T) {
+  const Tune& tu = tn();
+  const int M = B * T;
+  const bool big = d->dt == FLAMED_BF16 && tu.big && M >= tu.big_min_rows;
+  return tu.fuse_euler && !big && tu.xcd_strips == 0 && !d->f8;
 }
 
 // Steps per captured graph: the largest divisor of nfe that is <= tn().graph_steps (default 16; the
@@ -2086,6 +2182,11 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   }
   const int G = graph_chunk(nfe);
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
+  // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
+  // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even
+  const bool fused = den_fused_ok(d, B, T) && G % 2 == 0;
+  DenWs w;
+  den_ws_layout(d, B, T, ws, &w);
   // the graph bakes in dt = 1/nfe, so nfe is part of the key
   const bool hit = d->gexec && d->g_B == B && d->g_T == T && d->g_nfe == nfe && d->g_xt == xt && d->g_mods == mods && d->g_ws == ws &&
                    d->g_epoch == d->tune_ver;
@@ -2094,7 +2195,10 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
     int rc = kOk;
-    for (int s = 0; s < G && rc == kOk; ++s) rc = den_step(d, xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr);
+    for (int s = 0; s < G && rc == kOk; ++s) {
+      if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr, s % 2 ? xt : w.XP);
+      else rc = den_step(d, xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr);
+    }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
@@ -2104,8 +2208,20 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     FL_HIP(ie);
     d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_epoch = d->tune_ver; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
   }
-  FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
+  const size_t n = (size_t)B * T * d->C;
+  if (fused) {  // counter -1: each step's proj_in advances it before the step's first modulation read
+    hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, w.XP, w.Y, B * T, d->C);
+    FL_LAUNCH_CHECK();
+    FL_HIP(hipMemsetAsync(d->ctr, 0xff, sizeof(int), st));
+  } else {
+    FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
+  }
   for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
+  if (fused) {  // the last step's combine + Euler update: x_nfe = XP + dt * v (nfe even: XP holds x_{nfe-1})
+    hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, nullptr, B * T, T,
+                       d->C, dt, nullptr, w.XP);
+    FL_LAUNCH_CHECK();
+  }
   return kOk;
 }
 
@@ -2140,11 +2256,23 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
   FL_HIP(hipEventCreate(&e0));
   FL_HIP(hipEventCreate(&e1));
   const int saved_dup = d->tune.dup_class;  // the handle's active snapshot (this call's TuneScope)
+  // the step structure the solve graph uses: fused Euler steps (no combine launches) where it fuses
+  const bool fused = den_fused_ok(d, B, T);
+  DenWs w;
+  den_ws_layout(d, B, T, ws, &w);
+  if (fused) {
+    const size_t n = (size_t)B * T * d->C;
+    hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, w.XP, w.Y, B * T, d->C);
+    FL_LAUNCH_CHECK();
+  }
   auto timed = [&](int dup, float* ms) -> int {
     d->tune.dup_class = dup;
     FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
     int rc = kOk;
-    for (int i = 0; i < kSteps && rc == kOk; ++i) rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream);
+    for (int i = 0; i < kSteps && rc == kOk; ++i) {
+      if (fused) rc = den_step(d, i % 2 ? w.XP : xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream, nullptr, i % 2 ? xt : w.XP);
+      else rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream);
+    }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
     d->tune.dup_class = saved_dup;
@@ -2168,7 +2296,7 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
   float base = 0.f;
   int rc = timed(-1, &base);
   const int NB = d->NB;
-  const int per_step[FLAMED_DEN_KERNEL_CLASSES] = {1, NB + 1, 0, NB + 1, NB + 1, NB, NB, 1, 1};
+  const int per_step[FLAMED_DEN_KERNEL_CLASSES] = {1, NB + 1, 0, NB + 1, NB + 1, NB, NB, 1, fused ? 0 : 1};
   for (int c = 0; c < FLAMED_DEN_KERNEL_CLASSES && rc == kOk; ++c) {
     float t = base;
     if (per_step[c] > 0 && (c != 2 || d->gcnt == nullptr)) rc = timed(c, &t);

@@ -143,6 +143,13 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "dw_cg32"       — below this many rows (default 1536) the depthwise conv uses narrow channel
  *                     groups of "dw_cg" channels (16 or 32; default 32);
  *   "xcd_strips"    — XCD strip width of small/mid-M register-staged tile placement (0 = off);
+ *   "x16"           — 1: bf16 residual stream / depthwise output on the large-M path (0 default);
+ *   "g8p_rows"      — large-M GEMMs from this many rows on 256 x 256 8-phase tiles (16384; 0 off);
+ *   "dwgn"          — 1 (default): large-M whole-utterance depthwise conv + GroupNorm kernel;
+ *   "dwgn_small"    — 1 (default): small-M one-workgroup-per-8-channels depthwise conv + GroupNorm;
+ *   "fuse_euler"    — 1 (default): small-M solve graphs compute the conv_out tap combine + Euler
+ *                     update inside the next step's proj_in A loader (25 launches per step, state
+ *                     ping-ponged through the workspace); 0: separate combine kernel (26);
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     FLAMED_DEN_KERNEL_CLASSES) twice per Euler step; -1 (default) = off.

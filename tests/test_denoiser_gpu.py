@@ -296,3 +296,31 @@ def test_cond_fold_vs_oracle(B, T, pg_f32):
     e = rel_l2(cf, orc.cond_fold(sd, cond, mask))
     print(f"cond fold B={B} T={T} f32 rel-L2 {e:.3e}")
     assert e < 1e-5
+
+
+@pytest.mark.parametrize("B,T,nfe", [(1, 400, 128), (3, 37, 8), (2, 1, 4), (1, 50, 7)])
+def test_fused_euler_solve_bitwise(B, T, nfe, pg_bf16):
+    """Small-M solve graphs compute the conv_out tap combine + Euler update (prob_generator.py:238-245,
+    445) inside the next step's proj_in loader (flamed_tune fuse_euler, 25 launches per step).  Same fp32
+    operation order as the combine kernel, so the solve is bitwise equal to the unfused graph and to the
+    eager solve; nfe = 7 has an odd graph chunk and takes the unfused path."""
+    from flamed import _native as nat
+    pg, _ = pg_bf16
+    hip = pg.denoiser.hip()
+    g = torch.Generator().manual_seed(31)
+    x0 = torch.randn(B, T, 256, generator=g).to(DEV)
+    spk = torch.randn(B, 256, generator=g).to(DEV)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    L = nat.lib()
+    outs = []
+    try:
+        with torch.inference_mode():
+            for fuse, graph in ((1, True), (0, True), (1, False)):
+                nat.check(L.flamed_tune(b"fuse_euler", fuse), "tune")
+                pg.denoiser.hip_graph = graph
+                outs.append(hip.solve(x0, ts, spk, nfe).cpu())
+    finally:
+        nat.check(L.flamed_tune(b"fuse_euler", 1), "tune")
+        pg.denoiser.hip_graph = True
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

@@ -17,7 +17,7 @@ import shutil
 from collections import defaultdict
 
 CLASSES = [
-    ("proj_in_gemm", [r"LoadF32.*EpiBiasStatsT", r"LoadF32I.*EpiBiasStatsT"]),
+    ("proj_in_gemm", [r"LoadF32.*EpiBiasStatsT", r"LoadF32I.*EpiBiasStatsT", r"LoadEulerIn"]),
     ("lnmod_dwconv_gnpartials", [r"dwconv_stats_kernel", r"dwgn_small_kernel", r"dwgn_kernel"]),
     ("gn_finalize", [r"gn_finalize_kernel"]),
     ("gnapply_conv2_gemm_gelu", [r"LoadGN", r"EpiBiasActIDF16bLi1E", r"EpiBiasAct<bf16, 1>"]),
