@@ -190,14 +190,14 @@ static int fft_forward(const FftStack& s, float* X, const uint8_t* mask, int B, 
   int rc;
   for (size_t li = 0; li < s.layers.size(); ++li) {
     const FftLayer& Ly = s.layers[li];
-    if ((rc = launch_gemm<float>(LoadF32<float>{X, D}, Ly.wqkv, D, EpiBiasAct<float, 0>{Ly.bqkv, w.QKV, 3 * D}, M, 3 * D, D, st))) return rc;
+    if ((rc = xf_gemm(LoadF32<float>{X, D}, Ly.wqkv, D, EpiBiasAct<float, 0>{Ly.bqkv, w.QKV, 3 * D}, M, 3 * D, D, st))) return rc;
     if ((rc = attention(D / s.H, w.QKV, mask, B, n, D, s.H, w.O, st))) return rc;
-    if ((rc = launch_gemm<float>(LoadF32<float>{w.O, D}, Ly.wfc, D, EpiBiasRes{Ly.bfc, X, w.R, D}, M, D, D, st))) return rc;
+    if ((rc = xf_gemm(LoadF32<float>{w.O, D}, Ly.wfc, D, EpiBiasRes{Ly.bfc, X, w.R, D}, M, D, D, st))) return rc;
     if ((rc = ln_mask(D, w.R, Ly.g1, Ly.b1, mask, X, M, n, nullptr, 0, 0, 0, 0, st))) return rc;
-    if ((rc = launch_gemm<float>(LoadConvRows<float, false>{X, D, n, s.k0, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, Ly.w1,
+    if ((rc = xf_gemm(LoadConvRows<float, false>{X, D, n, s.k0, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, Ly.w1,
                                  s.k0 * D, EpiBiasAct<float, 3>{Ly.c1b, w.Hf, F}, M, F, s.k0 * D, st)))
       return rc;
-    if ((rc = launch_gemm<float>(LoadConvRows<float, false>{w.Hf, F, n, s.k1, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, Ly.w2,
+    if ((rc = xf_gemm(LoadConvRows<float, false>{w.Hf, F, n, s.k1, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, Ly.w2,
                                  s.k1 * F, EpiBiasRes{Ly.c2b, X, w.R, D}, M, D, s.k1 * F, st)))
       return rc;
     const bool last = li + 1 == s.layers.size();
@@ -220,7 +220,7 @@ static int run_decode(Prior* p, const float* x, const uint8_t* tmask, const int6
   const int De = p->enc.D, D = p->shared.D, nq = p->nq;
   int rc;
   // bridge + shared decoder (prior_generator.py:165-168)
-  if ((rc = launch_gemm<float>(LoadF32<float>{x, De}, p->bridge_w, De, EpiBiasPos{p->bridge_b, pos ? pos : p->shared.pos, T, w.Xs, D},
+  if ((rc = xf_gemm(LoadF32<float>{x, De}, p->bridge_w, De, EpiBiasPos{p->bridge_b, pos ? pos : p->shared.pos, T, w.Xs, D},
                                B * T, D, De, st)))
     return rc;
   if ((rc = fft_forward(p->shared, w.Xs, tmask, B, T, w, st))) return rc;
@@ -236,7 +236,7 @@ static int run_decode(Prior* p, const float* x, const uint8_t* tmask, const int6
     if ((rc = fft_forward(p->dec[q], w.X, w.dmask, B, n, w, st, embs, P, T, nq, q))) return rc;
   }
   // code head over (B, nq, T) rows, masked and permuted (:186-188)
-  return launch_gemm<float>(LoadF32<float>{embs, D}, p->head_w, D, EpiHead{p->head_b, tmask, logits, p->vocab + 1, nq, T},
+  return xf_gemm(LoadF32<float>{embs, D}, p->head_w, D, EpiHead{p->head_b, tmask, logits, p->vocab + 1, nq, T},
                             B * nq * T, p->head_n, D, st);
 }
 

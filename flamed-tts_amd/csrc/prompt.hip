@@ -223,15 +223,15 @@ static int run_vq(PromptVq* p, const float* x, int B, int T, float* outs, int64_
   int rc;
   for (const TimbreLayer& L : p->tl) {  // pre-LN layer, transformer.py:122-151
     if ((rc = ln_mask(d, X, L.g1, L.b1, nullptr, w.H, M, T, nullptr, 0, 0, 0, 0, st))) return rc;
-    if ((rc = launch_gemm<float>(LoadF32<float>{w.H, d}, L.wqkv, d, EpiBiasAct<float, 0>{L.bqkv, w.QKV, 3 * d}, M, 3 * d, d, st))) return rc;
+    if ((rc = xf_gemm(LoadF32<float>{w.H, d}, L.wqkv, d, EpiBiasAct<float, 0>{L.bqkv, w.QKV, 3 * d}, M, 3 * d, d, st))) return rc;
     if ((rc = attention(d / p->heads, w.QKV, nullptr, B, T, d, p->heads, w.O, st))) return rc;
-    if ((rc = launch_gemm<float>(LoadF32<float>{w.O, d}, L.wo, d, EpiBiasRes{L.bo, X, R, d}, M, d, d, st))) return rc;
+    if ((rc = xf_gemm(LoadF32<float>{w.O, d}, L.wo, d, EpiBiasRes{L.bo, X, R, d}, M, d, d, st))) return rc;
     std::swap(X, R);
     if ((rc = ln_mask(d, X, L.g2, L.b2, nullptr, w.H, M, T, nullptr, 0, 0, 0, 0, st))) return rc;
-    if ((rc = launch_gemm<float>(LoadConvRows<float, false>{w.H, d, T, p->k, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, L.w1,
+    if ((rc = xf_gemm(LoadConvRows<float, false>{w.H, d, T, p->k, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, L.w1,
                                  p->k * d, EpiBiasAct<float, 3>{L.c1b, w.Hf, F}, M, F, p->k * d, st)))
       return rc;
-    if ((rc = launch_gemm<float>(LoadF32<float>{w.Hf, F}, L.w2, F, EpiBiasRes{L.c2b, X, R, d}, M, d, F, st))) return rc;
+    if ((rc = xf_gemm(LoadF32<float>{w.Hf, F}, L.w2, F, EpiBiasRes{L.c2b, X, R, d}, M, d, F, st))) return rc;
     std::swap(X, R);
   }
   if ((rc = ln_mask(d, X, p->lg, p->lb, nullptr, w.H, M, T, nullptr, 0, 0, 0, 0, st))) return rc;

@@ -8,8 +8,6 @@
 
 namespace fl {
 
-constexpr size_t attn_lds_bytes(int DK) { return (size_t)4 * 64 * (DK + 2) * 4 + 64; }
-
 // LayerNorm (eps 1e-5, affine) + masked_fill(mask, 0), one wave per row.  With `embs` the rows j >= P
 // of utterance b are also written to embs[b][q][j - P] (the decoder's target slice, :181-182).
 template <int D>
@@ -53,23 +51,32 @@ __global__ __launch_bounds__(256) void ln_mask_kernel(const float* __restrict__ 
 // Scaled dot-product attention with an optional key-padding mask (prior: Modules.py:14-25,
 // SubLayers.py:38-52; timbre encoder: nn.MultiheadAttention without a mask, facodec/transformer.py:116).
 // QKV rows (B*n, 3D): Q at column h*DK, K at D + h*DK, V at 2D + h*DK.  Out O (B*n, D), head h at h*DK.
-// Block: 256 threads = 4 waves; lane = query of a 64-query tile, wave w takes keys [16w, 16w+16) of
-// every 64-key chunk (all lanes read the same K/V row: LDS broadcast).
+// Block: 512 threads = 8 waves; lane = query of a 64-query tile, wave w takes keys [8w, 8w+8) of every
+// 64-key chunk (all lanes read the same K/V row: LDS broadcast).  K/V chunks are double-buffered in LDS
+// and the next chunk's global loads are issued before the current chunk's math (registers -> LDS after
+// it), so one HBM/L2 latency per chunk is hidden.  Each wave keeps an online-softmax state (max, sum,
+// acc[DK]); the eight states of a query are merged through LDS at the end.
+constexpr int kAttnWaves = 8;
+constexpr int kAttnKC = 64;  // keys per chunk
+constexpr size_t attn_lds_bytes(int DK) {
+  const size_t buf = (size_t)2 * 2 * kAttnKC * DK * 4;            // 2 buffers x (K, V)
+  const size_t merge = (size_t)kAttnWaves * 64 * (DK + 2) * 4;    // per-wave (acc, max, sum) of 64 queries
+  return (buf > merge ? buf : merge) + 2 * kAttnKC;               // + 2 mask chunks
+}
 template <int DK>
-__global__ __launch_bounds__(256) void attn_kernel(const float* __restrict__ QKV, const uint8_t* __restrict__ kmask,
+__global__ __launch_bounds__(512) void attn_kernel(const float* __restrict__ QKV, const uint8_t* __restrict__ kmask,
                                                    int n, int D, float temp, float* __restrict__ O) {
-  constexpr int KC = 64;        // keys per LDS chunk
-  constexpr int KW = KC / 4;    // keys per wave per chunk
-  constexpr int DS = DK / 4;    // output dims per thread in the merge
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // attn_lds_bytes(DK)
-  float* Ks = sm;               // [KC][DK]
-  float* Vs = sm + KC * DK;     // [KC][DK]
-  uint8_t* ms = reinterpret_cast<uint8_t*>(sm + 4 * 64 * (DK + 2));
+  constexpr int NW = kAttnWaves, KC = kAttnKC, KW = KC / NW;
+  constexpr int V4 = KC * DK / 4;              // float4s per operand chunk
+  constexpr int PT = (2 * V4 + 511) / 512;     // float4s per thread per chunk (K and V)
+  constexpr int DS = DK / NW;                  // output dims per thread in the merge
+  static_assert(DK % NW == 0 && DK % 4 == 0, "head width");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  uint8_t* msk = reinterpret_cast<uint8_t*>(sm) + attn_lds_bytes(DK) - 2 * KC;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 64;
-  const int qi = q0 + lane;
+  const int qi = blockIdx.x * 64 + lane;
   const int ld = 3 * D;
   const float* base = QKV + (size_t)b * n * ld;
 
@@ -82,25 +89,49 @@ __global__ __launch_bounds__(256) void attn_kernel(const float* __restrict__ QKV
       qv[d] = t.x; qv[d + 1] = t.y; qv[d + 2] = t.z; qv[d + 3] = t.w;
     }
   }
+  float4 pf[PT];
+  uint8_t pm = 1;
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = tid + j * 512;
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < 2 * V4) {
+        const int op = i / V4, r = i - op * V4;
+        const int key = r / (DK / 4), c = (r - key * (DK / 4)) * 4;
+        const int kk = k0 + key;
+        if (kk < n) t = ld4(base + (size_t)kk * ld + (op + 1) * D + h * DK + c);
+      }
+      pf[j] = t;
+    }
+    if (tid < KC) {
+      const int kk = k0 + tid;
+      pm = kk < n ? (kmask ? kmask[(size_t)b * n + kk] : 0) : 1;
+    }
+  };
+  auto stash = [&](int buf) {
+    float* KV = sm + buf * 2 * KC * DK;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = tid + j * 512;
+      if (i < 2 * V4) *reinterpret_cast<float4*>(KV + (size_t)i * 4) = pf[j];  // K rows then V rows
+    }
+    if (tid < KC) msk[buf * KC + tid] = pm;
+  };
+
   float mx = -INFINITY, sum = 0.f, acc[DK];
 #pragma unroll
   for (int d = 0; d < DK; ++d) acc[d] = 0.f;
-
-  for (int k0 = 0; k0 < n; k0 += KC) {
-    __syncthreads();
-    constexpr int V4 = KC * DK / 4;  // float4s per operand chunk
-    for (int i = tid; i < 2 * V4; i += 256) {
-      int op = i / V4, r = i - op * V4;
-      int key = r / (DK / 4), c = (r - key * (DK / 4)) * 4;
-      int kk = k0 + key;
-      float4 t = kk < n ? ld4(base + (size_t)kk * ld + (op + 1) * D + h * DK + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>((op ? Vs : Ks) + key * DK + c) = t;
-    }
-    if (tid < KC) {
-      int kk = k0 + tid;
-      ms[tid] = kk < n ? (kmask ? kmask[(size_t)b * n + kk] : 0) : 1;
-    }
-    __syncthreads();
+  const int nch = (n + KC - 1) / KC;
+  fetch(0);
+  stash(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) fetch((c + 1) * KC);  // in flight during this chunk's math
+    const float* Ks = sm + buf * 2 * KC * DK;
+    const float* Vs = Ks + KC * DK;
+    const uint8_t* ms = msk + buf * KC;
     float s[KW];
     float cmax = -INFINITY;
 #pragma unroll
@@ -119,54 +150,56 @@ __global__ __launch_bounds__(256) void attn_kernel(const float* __restrict__ QKV
       s[j] = ms[key] ? -INFINITY : dot / temp;
       cmax = fmaxf(cmax, s[j]);
     }
-    if (cmax == -INFINITY) continue;  // every key of this wave's slice is padding (uniform per wave)
-    const float nm = fmaxf(mx, cmax);
-    const float sc = expf(mx - nm);   // mx = -inf on the first live slice: exp(-inf) = 0
-    sum *= sc;
+    if (cmax != -INFINITY) {  // uniform per wave: every key of this wave's slice may be padding
+      const float nm = fmaxf(mx, cmax);
+      const float sc = __expf(mx - nm);  // mx = -inf on the first live slice: 0
+      sum *= sc;
 #pragma unroll
-    for (int d = 0; d < DK; ++d) acc[d] *= sc;
+      for (int d = 0; d < DK; ++d) acc[d] *= sc;
 #pragma unroll
-    for (int j = 0; j < KW; ++j) {
-      const float p = expf(s[j] - nm);  // masked keys: exp(-inf) = 0
-      sum += p;
-      const float* vr = Vs + (w * KW + j) * DK;
+      for (int j = 0; j < KW; ++j) {
+        const float p = __expf(s[j] - nm);  // masked keys: 0
+        sum += p;
+        const float* vr = Vs + (w * KW + j) * DK;
 #pragma unroll
-      for (int d = 0; d < DK; d += 4) {
-        float4 vv = *reinterpret_cast<const float4*>(vr + d);
-        acc[d] = fmaf(p, vv.x, acc[d]);
-        acc[d + 1] = fmaf(p, vv.y, acc[d + 1]);
-        acc[d + 2] = fmaf(p, vv.z, acc[d + 2]);
-        acc[d + 3] = fmaf(p, vv.w, acc[d + 3]);
+        for (int d = 0; d < DK; d += 4) {
+          float4 vv = *reinterpret_cast<const float4*>(vr + d);
+          acc[d] = fmaf(p, vv.x, acc[d]);
+          acc[d + 1] = fmaf(p, vv.y, acc[d + 1]);
+          acc[d + 2] = fmaf(p, vv.z, acc[d + 2]);
+          acc[d + 3] = fmaf(p, vv.w, acc[d + 3]);
+        }
       }
+      mx = nm;
     }
-    mx = nm;
+    if (c + 1 < nch) stash(buf ^ 1);  // that buffer's last readers finished before the previous barrier
+    __syncthreads();
   }
-  // merge the four waves' partial softmax states: [w][d][lane] (conflict-free), then (mx, sum) rows
-  __syncthreads();
-  float* pa = sm;                      // 4 * DK * 64
-  float* pm = sm + 4 * DK * 64;        // 4 * 64
-  float* ps = pm + 4 * 64;             // 4 * 64
+  // merge the eight waves' partial softmax states: acc as [w][d][lane] (conflict-free), then (max, sum)
+  float* pa = sm;                          // NW * DK * 64
+  float* pmx = sm + NW * DK * 64;          // NW * 64
+  float* psm = pmx + NW * 64;              // NW * 64
 #pragma unroll
   for (int d = 0; d < DK; ++d) pa[(w * DK + d) * 64 + lane] = acc[d];
-  pm[w * 64 + lane] = mx;
-  ps[w * 64 + lane] = sum;
+  pmx[w * 64 + lane] = mx;
+  psm[w * 64 + lane] = sum;
   __syncthreads();
   if (qi >= n) return;
   float M = -INFINITY;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) M = fmaxf(M, pm[u * 64 + lane]);
-  float f[4], L = 0.f;
+  for (int u = 0; u < NW; ++u) M = fmaxf(M, pmx[u * 64 + lane]);
+  float f[NW], L = 0.f;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    f[u] = expf(pm[u * 64 + lane] - M);  // all keys padded: M = -inf -> NaN, as the reference's softmax
-    L += ps[u * 64 + lane] * f[u];
+  for (int u = 0; u < NW; ++u) {
+    f[u] = __expf(pmx[u * 64 + lane] - M);  // all keys padded: M = -inf -> NaN, as the reference's softmax
+    L += psm[u * 64 + lane] * f[u];
   }
   float* o = O + ((size_t)b * n + qi) * D + h * DK + w * DS;
 #pragma unroll
   for (int d = 0; d < DS; ++d) {
     float a = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a += pa[(u * DK + w * DS + d) * 64 + lane] * f[u];
+    for (int u = 0; u < NW; ++u) a += pa[(u * DK + w * DS + d) * 64 + lane] * f[u];
     o[d] = a / L;
   }
 }
@@ -190,6 +223,15 @@ struct EpiBiasRes {
   __device__ void store_stats(int, int, float, float) const {}
 };
 
+// fp32 GEMM of the transformer stacks: the shape-driven config, but 32 x 32 tiles when 32 x 64 tiles
+// would not give every CU a workgroup (N = 384 outputs at a few hundred rows: long K chains on few CUs).
+template <class AL, class EP>
+static int xf_gemm(const AL& al, const float* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  if (M < 2048 && (size_t)(N / 64) * ((M + 31) / 32) < 256 && N % 32 == 0)
+    return launch_gemm_cfg<32, 32, 3, float>(al, W, ldw, ep, M, N, K, st);
+  return launch_gemm<float>(al, W, ldw, ep, M, N, K, st);
+}
+
 template <int D>
 static int launch_ln(const float* R, const float* g, const float* b, const uint8_t* mask, float* X, int M, int n,
                      float* embs, int P, int T, int nq, int q, hipStream_t st) {
@@ -211,7 +253,7 @@ static int launch_attn(const float* QKV, const uint8_t* mask, int B, int n, int 
   const size_t lds = attn_lds_bytes(DK);
   auto kern = attn_kernel<DK>;
   if (lds > 64 * 1024) FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
-  hipLaunchKernelGGL(kern, dim3((n + 63) / 64, H, B), dim3(256), lds, st, QKV, mask, n, D, temp, O);
+  hipLaunchKernelGGL(kern, dim3((n + 63) / 64, H, B), dim3(512), lds, st, QKV, mask, n, D, temp, O);
   FL_LAUNCH_CHECK();
   return kOk;
 }
