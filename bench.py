@@ -375,11 +375,27 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
         roof = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof.update({"frac": round(roof["achieved"] / roof["peak"], 4), "kernel": dom["name"], "launch_us": dom["us"],
                  "tflops": dom["TFLOPs"], "gbps": dom["GBps"]})
+    # the same workload on an MX-fp8 handle (conv_2/conv_3/mlp.0/mlp.2 block-scaled e4m3 at 25,600 rows)
+    fp8 = None
+    if args.dtype == "bf16":
+        from flamed.models.synthesizer.prob_generator import DenoiserHIP
+        hip8 = DenoiserHIP(pg.denoiser, "fp8")
+        with torch.inference_mode():
+            ref = hip.solve(x0, ts, spk, nfe)
+            hip8.solve(x0, ts, spk, nfe)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sol8 = hip8.solve(x0, ts, spk, nfe)
+            torch.cuda.synchronize()
+            sec8 = time.perf_counter() - t0
+        fp8 = {"dtype": "mx-fp8 e4m3 (pointwise H x H GEMMs) + bf16", "value": round(B * T / sec8, 2),
+               "ms_per_solve": round(sec8 * 1e3, 3), "rel_l2_vs_bf16": float((sol8 - ref).norm() / ref.norm())}
+        del hip8
     return {"workload": f"BASELINE configs[2]: {B} utterances x {T} frames, nsteps-denoiser={nfe}, hipGraph solve",
             "value": round(B * T / sec, 2), "unit": "latent frames/s", "ms_per_solve": round(sec * 1e3, 3),
             "rtf_denoiser": round(sec / (B * T * 200 / 16000.0), 6), "step_us_graph": round(ms[N_CLASSES] * 1e3, 2),
             "roofline": roof,
-            "kernels": ks}
+            "kernels": ks, "fp8": fp8}
 
 
 def main():

@@ -38,6 +38,10 @@
 // K-tile, picked by the MFMA's op_sel byte).
 #pragma once
 #include "gemm.hpp"
+
+#ifndef FL_8P_EPI_U
+#define FL_8P_EPI_U 4  // epilogue row-iterations whose residual loads are in flight together (16 spills)
+#endif
 #include "gemm_dma.hpp"
 
 namespace fl {
@@ -467,7 +471,7 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
     const float* e_vec = h ? e_vec1 : e_vec0;
     __syncthreads();
     constexpr int IT = 256 * 32 / k8pThreads, RPI = k8pThreads / 32;  // 16 rows per iteration
-    constexpr int U = 4;  // iterations whose residual loads are in flight together (16-B vector loads)
+    constexpr int U = FL_8P_EPI_U;  // iterations whose residual loads are in flight together (16-B vector loads)
 #pragma unroll 1
     for (int it0 = 0; it0 < IT; it0 += U) {
       float xr[U][4];
