@@ -255,8 +255,11 @@ def secondary_measurements(dev, nfe):
         _, codes, _, _, timbre = dec(z, eval_vq=False, vq=True)
         prompts = codes.permute(1, 0, 2).contiguous()
 
-        def e2e(L):
-            phon = torch.randint(1, 300, (1, L), generator=torch.Generator().manual_seed(L)).to(dev)
+        base_phon = torch.randint(1, 300, (1, 1024), generator=torch.Generator().manual_seed(1234))
+
+        def e2e(L, phon=None):
+            phon = (phon if phon is not None else
+                    torch.randint(1, 300, (1, L), generator=torch.Generator().manual_seed(L))).to(dev)
             res = {}
 
             def run():
@@ -276,19 +279,23 @@ def secondary_measurements(dev, nfe):
         r60 = e2e(L)
         r60["note"] = "random-init weights: the utterance length T comes from the seeded duration flow"
         out["end_to_end"] = r60
-        # the headline 5 s utterance: phoneme count scaled so the seeded duration flow yields ~400 frames
-        # (the seeded flow's frames per phoneme vary with the phoneme draw: a short secant search, closest kept)
-        best, Lc = r60, max(8, int(round(L * 400 / max(r60["frames"], 1))))
-        for _ in range(5):
-            r = e2e(Lc)
+        # the headline 5 s utterance: a prefix of one fixed phoneme sequence, its length bisected until the
+        # seeded duration flow yields ~400 frames (frames grow with the prefix; closest kept)
+        best, lo, hi = r60, 8, 1024
+        for _ in range(9):
+            Lc = (lo + hi) // 2
+            r = e2e(Lc, base_phon[:, :Lc])
             if abs(r["frames"] - 400) < abs(best["frames"] - 400):
                 best = r
-            if abs(r["frames"] - 400) <= 8:
+            if abs(r["frames"] - 400) <= 8 or hi - lo <= 1:
                 break
-            Lc = max(8, int(round(Lc * 400 / max(r["frames"], 1))) + (1 if r["frames"] < 400 else -1))
+            if r["frames"] < 400:
+                lo = Lc
+            else:
+                hi = Lc
         r5 = dict(best)
-        r5["note"] = ("BASELINE metric at the configs[1] length: phoneme count chosen so the seeded duration "
-                      "flow gives ~400 frames (5 s); B = 1, nsteps-denoiser = 128")
+        r5["note"] = ("BASELINE metric at the configs[1] length: the phoneme prefix length bisected so the seeded "
+                      "duration flow gives ~400 frames (5 s); B = 1, nsteps-denoiser = 128")
         out["end_to_end_5s"] = r5
     return out
 

@@ -152,9 +152,15 @@ struct DurNet {
   float *w0, *we, *c1w, *c2w;  // packed
   const float *pb, *t1w, *t1b, *t2w, *t2b, *c1b, *g1, *b1, *c2b, *g2, *b2, *lw, *lb;  // copies in the arena
   PvaGraph graph;   // the (duration, silence) pair's cached flow graph, kept on the duration net's handle
+  // split-K of the net's small-M GEMMs (their K chains, 18 / 36 fp32 K-steps, are the step's latency):
+  // per-handle slab + self-resetting tile counters, so the two nets' concurrent graph branches never share
+  SplitCtx split;
+  char* split_mem = nullptr;
+  static constexpr int kSplitTarget = 256, kSplitCounters = 1024;
 };
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+static bool tune_snapshot_pva_split() { return tn().pva_split != 0; }
 
 struct PvaWs {
   float *Fd, *TH, *TEMBd, *TEMBs, *Pd, *Ps, *R1, *S1, *R2, *R1s, *S1s, *R2s;  // R*/S* per net (chains run concurrently)
@@ -190,9 +196,11 @@ struct NetBufs {
   float *R1, *S1, *R2;
 };
 static int net_step(DurNet* n, const float* P, const float* temb, float* xt, const uint8_t* mask, int B, int L, float dt,
-                    const NetBufs& w, hipStream_t st, const int* ctr = nullptr, int* ctr_inc = nullptr) {
+                    const NetBufs& w, hipStream_t st, const int* ctr = nullptr, int* ctr_inc = nullptr,
+                    bool split = true) {
   const int M = B * L, D = n->D, F = n->F;
   const int NT = F / 64;
+  SplitScope split_scope(split && n->split_mem && tune_snapshot_pva_split() ? &n->split : nullptr);
   int rc;
   if ((rc = launch_gemm_auto<float>(pick_cfg(M) == kCfgSmall ? kCfgSmall : kCfgMid, LoadDurIn{P, n->w0, xt, temb, D, L, ctr}, n->c1w, 3 * D,
                                           EpiBiasStatsT<true>{n->c1b, w.R1, F, w.S1, NT}, M, F, 3 * D, st)))
@@ -304,6 +312,7 @@ FLAMED_API int flamed_dur_destroy(flamed_dur_t h) {
     DeviceGuard dg(n->device);
     n->graph.release();
     if (n->dev) (void)hipFree(n->dev);
+    if (n->split_mem) (void)hipFree(n->split_mem);
   }
   delete n;
   return kOk;
@@ -321,6 +330,7 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* w, int nw, hi
     DeviceGuard og(n->device);
     n->graph.release();
     if (n->dev) { (void)hipFree(n->dev); n->dev = nullptr; }
+    if (n->split_mem) { (void)hipFree(n->split_mem); n->split_mem = nullptr; }
   }
   n->device = wdev;
   FL_ON_DEVICE(wdev);
@@ -334,6 +344,18 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* w, int nw, hi
   if (n->dev) { FL_HIP(hipFree(n->dev)); n->dev = nullptr; }
   n->graph.release();
   FL_HIP(hipMalloc(&n->dev, total));
+  if (!n->split_mem) {  // slab: up to kSplitTarget workgroups of 32 x 64 fp32 tiles; zeroed tile counters
+    const size_t slab_floats = (size_t)DurNet::kSplitTarget * 32 * 64;
+    FL_HIP(hipMalloc(&n->split_mem, 4 * slab_floats + 4 * DurNet::kSplitCounters));
+    FL_HIP(hipMemsetAsync(n->split_mem + 4 * slab_floats, 0, 4 * DurNet::kSplitCounters, st));
+    n->split.slab = reinterpret_cast<float*>(n->split_mem);
+    n->split.slab_floats = slab_floats;
+    n->split.cnt = reinterpret_cast<int*>(n->split_mem + 4 * slab_floats);
+    n->split.cnt_n = DurNet::kSplitCounters;
+    n->split.target = DurNet::kSplitTarget;
+    n->split.max_split = 4;
+    n->split.f32 = true;
+  }
   n->w0 = (float*)(n->dev + o_w0); n->we = (float*)(n->dev + o_we);
   n->c1w = (float*)(n->dev + o_c1); n->c2w = (float*)(n->dev + o_c2);
   hipLaunchKernelGGL(split_proj_kernel, dim3((D * (D + 1) + 255) / 256), dim3(256), 0, st, w[0], n->w0, n->we, D);
@@ -423,9 +445,11 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
     hipError_t fe = hipEventRecord(gp.fork, gp.cap);
     if (fe == hipSuccess) fe = hipStreamWaitEvent(gp.cap2, gp.fork, 0);
     if (fe != hipSuccess) r = kHip;
-    for (int i = 0; i < G && r == kOk; ++i) r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, bd, gp.cap, gp.ctr, gp.ctr);
+    // one handle for both nets: its split-K counters would be shared by the concurrent branches
+    const bool split = nd != ns;
+    for (int i = 0; i < G && r == kOk; ++i) r = net_step(nd, w.Pd, w.TEMBd, dur_t, mask, B, L, dt, bd, gp.cap, gp.ctr, gp.ctr, split);
     for (int i = 0; i < G && r == kOk; ++i)
-      r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, bs, gp.cap2, gp.ctr + 1, gp.ctr + 1);
+      r = net_step(ns, w.Ps, w.TEMBs, sil_t, mask, B, L, dt, bs, gp.cap2, gp.ctr + 1, gp.ctr + 1, split);
     if (r == kOk) {
       fe = hipEventRecord(gp.join, gp.cap2);
       if (fe == hipSuccess) fe = hipStreamWaitEvent(gp.cap, gp.join, 0);

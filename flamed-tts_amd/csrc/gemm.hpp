@@ -672,6 +672,7 @@ struct SplitCtx {
   int cnt_n = 0;
   int target = 1;  // aim for about this many workgroups (tiles x splits); 1 = no split
   int max_split = 4;
+  bool f32 = false;  // also split exact-fp32 GEMMs (PVA nets: a fixed slice order is still deterministic)
 };
 extern thread_local SplitCtx* g_split;
 // Pipeline depth of the small-M (32 x 64) config: tn().small_stages 3 = LDS ring of 3 / 2 K-steps in
@@ -694,7 +695,7 @@ inline SplitK choose_split(int M, int N, int K) {
     if (xs > 0 && gx % xs == 0 && M < 8192) sk.strips = xs;
   }
   SplitCtx* c = g_split;
-  if (!c || DTraits<DT>::kCode != 1) return sk;  // fp32 parity mode keeps one exact FMA chain
+  if (!c || (DTraits<DT>::kCode != 1 && !c->f32)) return sk;  // the denoiser's fp32 parity mode keeps one FMA chain
   const int tiles = (N / BN) * ((M + BM - 1) / BM);
   int n = 1;
   while (n * 2 <= c->max_split && tiles * n * 2 <= c->target && (K / BKE) % (n * 2) == 0 && K / (n * 2) >= 2 * BKE) n *= 2;

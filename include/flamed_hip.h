@@ -150,6 +150,9 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "fuse_euler"    — 1 (default): small-M solve graphs compute the conv_out tap combine + Euler
  *                     update inside the next step's proj_in A loader (25 launches per step, state
  *                     ping-ponged through the workspace); 0: separate combine kernel (26);
+ *   "pva_split"     — 1: the PVA nets' small-M exact-fp32 GEMMs split K over workgroups
+ *                     (per-handle slabs, fixed slice order: deterministic); 0 (default: measured
+ *                     no faster): one K chain;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     FLAMED_DEN_KERNEL_CLASSES) twice per Euler step; -1 (default) = off.

@@ -122,3 +122,30 @@ def test_length_regulator_log_domain():
     out, tl = hip_length_regulate(t32(x).to(DEV), t32(d).to(DEV), t32(s).to(DEV), t32(sl).to(DEV), None,
                                   log_domain=True)
     assert np.array_equal(tl.cpu().numpy(), rtl) and np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("B,L", [(1, 60), (2, 247)])
+def test_pva_split_k_deterministic(pva, B, L):
+    """The nets' small-M fp32 GEMMs split K over workgroups (flamed_tune pva_split, per-handle slabs and
+    counters, slices summed in a fixed order): repeated graph solves are bitwise equal, and the flow
+    differs from the one-chain form by fp32 reassociation only."""
+    from flamed import _native as nat
+    m, _ = pva
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(B, L, 192, generator=gen).to(DEV)
+    mask = torch.zeros(B, L, dtype=torch.bool, device=DEV)
+    d0 = torch.randn(B, L, generator=gen).to(DEV) * 0.3
+    s0 = torch.randn(B, L, generator=gen).to(DEV) * 0.3
+    ts = torch.linspace(0, 1, 65, device=DEV)
+    L_ = nat.lib()
+    outs = []
+    try:
+        with torch.inference_mode():
+            for sp in (1, 1, 0):
+                nat.check(L_.flamed_tune(b"pva_split", sp), "tune")
+                outs.append(m.hip().flow(x, mask, d0, s0, ts, 64))
+    finally:
+        nat.check(L_.flamed_tune(b"pva_split", 0), "tune")
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for a, b in zip(outs[0], outs[2]):
+        assert rel_l2(a.cpu(), b.cpu()) < 1e-5
