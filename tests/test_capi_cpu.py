@@ -60,6 +60,27 @@ def test_host_side_validation_errors(lib):
     assert lib.flamed_fac_destroy(f) == 0
     with pytest.raises(RuntimeError, match="status 1001"):
         _native.check(lib.flamed_den_create(256, 1024, 4, 31, 256, 9, ctypes.byref(h)), "create")
+    # prior transformer handle (prior.yaml dims): 22 FFT layers x 16 + 2 + 3 + 1 + 3 + 6 + 2 weights
+    pd = [361, 192, 4, 768, 9, 1, 6, 4096, 384, 12, 1536, 3, 1, 2, 8192, 1024, 6, 1, 2, 2, 3, 3, 3]
+    pr = ctypes.c_void_p()
+    assert lib.flamed_prior_create((ctypes.c_int * len(pd))(*pd), len(pd), ctypes.byref(pr)) == 0
+    assert lib.flamed_prior_num_weights(pr) == 2 + 16 * 6 + 3 + 1 + 16 * 2 + 3 + sum(1 + 16 * n for n in pd[17:]) + 2
+    assert lib.flamed_prior_encode(pr, None, None, 1, 10, None, None, None, 0, 0, None) == 1001  # not loaded
+    assert b"not loaded" in lib.flamed_last_error()
+    assert lib.flamed_prior_destroy(pr) == 0
+    bad = list(pd)
+    bad[2] = 5  # 192 / 5 heads
+    assert lib.flamed_prior_create((ctypes.c_int * len(bad))(*bad), len(bad), ctypes.byref(pr)) == 1001
+    assert lib.flamed_prior_create((ctypes.c_int * 17)(*pd[:17]), 17, ctypes.byref(pr)) == 1001
+    # prompt quantizers + timbre encoder (codec.yaml dims)
+    vd = [256, 8, 3, 1, 2, 3, 1024, 1024, 1024, 256, 4, 1024, 5, 4, 5000]
+    vq = ctypes.c_void_p()
+    assert lib.flamed_vq_create((ctypes.c_int * len(vd))(*vd), len(vd), ctypes.byref(vq)) == 0
+    assert lib.flamed_vq_num_weights(vq) == 7 * 6 + 1 + 12 * 4 + 2
+    assert lib.flamed_vq_destroy(vq) == 0
+    bad = list(vd)
+    bad[1] = 16  # codebook_dim
+    assert lib.flamed_vq_create((ctypes.c_int * len(bad))(*bad), len(bad), ctypes.byref(vq)) == 1001
 
 
 DIAG_HDR = os.path.join(os.path.dirname(PKG), "include", "flamed_diag.h")
