@@ -2159,11 +2159,24 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
   return den_step(d, xt, mods, mod_div, B, T, dt, nullptr, ws, st);
 }
 
+FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe) {
+  Den* d = reinterpret_cast<Den*>(h);
+  if (!d || nfe <= 0) return -1;
+  FL_DEN_CALL(d);
+  return graph_chunk(nfe);
+}
+
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t st) {
+  return flamed_den_solve_part(h, xt, mods, nfe, B, T, ws, ws_bytes, use_graph, 0, nfe, st);
+}
+
+FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
+                                     size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t st) {
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && d->dev, "flamed_den_solve: handle not loaded");
   FL_REQUIRE(xt && mods && ws && B > 0 && T > 0 && nfe > 0, "flamed_den_solve: bad args");
+  FL_REQUIRE(0 <= s0 && s0 < s1 && s1 <= nfe, "flamed_den_solve_part: bad step range [%d, %d) of %d", s0, s1, nfe);
   FL_DEN_CALL(d);
   FL_REQUIRE_ON(xt, d->device, "flamed_den_solve");
   if (ws_bytes < den_ws_bytes(d, B, T)) {
@@ -2174,13 +2187,15 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   const float dt = (float)(1.0 / (double)nfe);
   const size_t step_stride = (size_t)B * d->MS;
   if (!use_graph) {
-    for (int s = 0; s < nfe; ++s) {
+    for (int s = s0; s < s1; ++s) {
       int rc = den_step(d, xt, mods + s * step_stride, T, B, T, dt, nullptr, ws, st);
       if (rc) return rc;
     }
     return kOk;
   }
   const int G = graph_chunk(nfe);
+  FL_REQUIRE(s0 % G == 0 && (s1 % G == 0 || s1 == nfe), "flamed_den_solve_part: range [%d, %d) not on %d-step graph chunks",
+             s0, s1, G);
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
   // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even
@@ -2209,15 +2224,17 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
     d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_epoch = d->tune_ver; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
   }
   const size_t n = (size_t)B * T * d->C;
-  if (fused) {  // counter -1: each step's proj_in advances it before the step's first modulation read
-    hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, w.XP, w.Y, B * T, d->C);
-    FL_LAUNCH_CHECK();
-    FL_HIP(hipMemsetAsync(d->ctr, 0xff, sizeof(int), st));
-  } else {
-    FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
+  if (s0 == 0) {
+    if (fused) {  // counter -1: each step's proj_in advances it before the step's first modulation read
+      hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, w.XP, w.Y, B * T, d->C);
+      FL_LAUNCH_CHECK();
+      FL_HIP(hipMemsetAsync(d->ctr, 0xff, sizeof(int), st));
+    } else {
+      FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
+    }
   }
-  for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
-  if (fused) {  // the last step's combine + Euler update: x_nfe = XP + dt * v (nfe even: XP holds x_{nfe-1})
+  for (int r = s0 / G; r < s1 / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
+  if (fused && s1 == nfe) {  // the last step's combine + Euler update: x_nfe = XP + dt * v (nfe even: XP holds x_{nfe-1})
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, nullptr, B * T, T,
                        d->C, dt, nullptr, w.XP);
     FL_LAUNCH_CHECK();

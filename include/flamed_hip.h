@@ -98,6 +98,14 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
  * replays it. */
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t stream);
+/* Steps per captured solve graph for nfe steps (the granularity of flamed_den_solve_part); -1 on error. */
+FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe);
+/* Steps [s0, s1) of the same solve (s0, s1 on flamed_den_solve_chunk boundaries, or s1 = nfe), so a
+ * caller can start the solve while later AdaLN rows are still being computed on another stream:
+ * s0 = 0 initialises the step counter, s1 = nfe finishes the solve.  Calls for one solve must be
+ * stream-ordered and use the same arguments apart from s0 / s1. */
+FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
+                                     size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t stream);
 
 /* Kernel classes of an Euler step (flamed_den_time_kernels_graph): 0 proj_in GEMM, 1 LN/mod +
  * depthwise conv (+ GroupNorm partials, + finalize by the last-arriving T-chunk), 2 standalone GroupNorm

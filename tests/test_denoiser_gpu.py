@@ -324,3 +324,32 @@ def test_fused_euler_solve_bitwise(B, T, nfe, pg_bf16):
         pg.denoiser.hip_graph = True
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+def test_solve_in_parts_equals_whole(pg_bf16):
+    """flamed_den_solve_part: the graph-chunked solve run as [0, G) then [G, nfe) (as a caller overlapping
+    later AdaLN rows would) is bitwise the whole flamed_den_solve."""
+    from flamed import _native as nat
+    pg, _ = pg_bf16
+    hip = pg.denoiser.hip()
+    L = nat.lib()
+    g = torch.Generator().manual_seed(41)
+    B, T, nfe = 1, 400, 32
+    x0 = torch.randn(B, T, 256, generator=g).to(DEV)
+    spk = torch.randn(B, 256, generator=g).to(DEV)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        whole = hip.solve(x0, ts, spk, nfe).cpu()
+        G = L.flamed_den_solve_chunk(hip.handle, nfe)
+        assert 0 < G < nfe and nfe % G == 0
+        r = torch.arange(nfe * B, device=DEV)
+        mods = hip.adaln(ts[:nfe], spk, (r // B).to(torch.int32), (r % B).to(torch.int32))
+        x = x0.clone()
+        ws = nat.Workspace().get(L.flamed_den_workspace_size(hip.handle, B, T), DEV)
+        for s0, s1 in ((0, G), (G, nfe)):
+            nat.check(L.flamed_den_solve_part(hip.handle, nat.ptr(x), nat.ptr(mods), nfe, B, T, nat.ptr(ws), ws.numel(),
+                                              1, s0, s1, nat.stream_ptr(DEV)), "flamed_den_solve_part")
+        assert L.flamed_den_solve_part(hip.handle, nat.ptr(x), nat.ptr(mods), nfe, B, T, nat.ptr(ws), ws.numel(),
+                                       1, 1, nfe, nat.stream_ptr(DEV)) == 1001  # off a chunk boundary
+        torch.cuda.synchronize()
+    assert torch.equal(x.cpu(), whole)
