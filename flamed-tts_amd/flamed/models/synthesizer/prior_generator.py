@@ -191,9 +191,12 @@ class PriorHIP:
         self._bufs = {}
 
     def _buf(self, key, make):
+        """Persistent I/O buffers of the latest shape per call kind (their pointers key the captured
+        graph); a new shape replaces the previous buffers instead of accumulating one set per length."""
         b = self._bufs.get(key)
         if b is None:
             b = make()
+            self._bufs = {k: v for k, v in self._bufs.items() if k[0] != key[0]}
             self._bufs[key] = b
         return b
 
