@@ -39,7 +39,7 @@ def _ids(B, L, seed):
     return torch.randint(1, 361, (B, L), generator=g)
 
 
-@pytest.mark.parametrize("lens", [[97, 60, 33], [1], [130]])
+@pytest.mark.parametrize("lens", [[97, 60, 33], [1], [130], [250, 247, 200, 180, 150, 99, 64, 12]])
 def test_encode_vs_oracle(model, lens):
     pg, sd = model
     B, L = len(lens), max(lens)
@@ -66,7 +66,8 @@ def test_encode_beyond_position_table(model):
     assert rel_l2(out, ref) < 2e-5
 
 
-@pytest.mark.parametrize("B,T,P,tl", [(1, 400, 240, [400]), (2, 96, 20, [96, 61]), (3, 37, 0, [37, 5, 30])])
+@pytest.mark.parametrize("B,T,P,tl", [(1, 400, 240, [400]), (2, 96, 20, [96, 61]), (3, 37, 0, [37, 5, 30]),
+                                      (8, 420, 160, [420, 400, 377, 350, 301, 256, 199, 64])])
 def test_decode_vs_oracle(model, B, T, P, tl):
     """bridge -> shared decoder -> six prompt-prefixed decoders -> head at the bench shape (T=400 target
     frames behind a 3 s prompt) and ragged / prompt-less batches."""
