@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU rehearsal of the launcher/timing harness over gloo (no GPU; tests/test_bench_cpu.py)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary rows (PVA flow + LR, FaCodec decode / prompt encode, end-to-end RTF)")
     return ap.parse_args()
@@ -90,6 +92,11 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fol
     M = B * T
     if fold is None:  # the denoiser's default policy: folded below the large-M path and from 6144 rows on it
         fold = es == 2 and FOLD is not False and (M < 1536 or M >= 6144)
+    # bf16 handles run the depthwise conv + exact two-pass GroupNorm in ONE kernel per (utterance, channel
+    # group) (dwgn_small below 1536 rows with T <= 576, dwgn on the large-M path with T <= 512): it reads
+    # the fp32 residual + LN partials and writes the normalised bf16 conv_2 operand; conv_2 then reads
+    # that bf16 operand (no fp32 depthwise output round trip, no GroupNorm partials)
+    dwgn = es == 2 and ((M < 1536 and T <= 576) or (M >= 1536 and T <= 512))
     ea = 2 if fold else 4  # bytes per A element of the LayerNorm-consuming GEMMs
     NT = H // 64
     TS = (T + 63) // 64
@@ -99,10 +106,14 @@ def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fol
             return M * C * 4 + M * 3 * C * 4 + M * C * 4 + H * C * es + M * H * 4 + stats, 2 * M * H * C + 4 * M * C, 1
         return M * C * 4 + H * C * es + M * H * 4 + stats, 2 * M * H * C, 1
     if cls == 1:
+        if dwgn:
+            return M * H * 4 + stats + M * H * 2, 2 * 31 * M * H, NB + 1
         return M * H * 4 + stats + M * H * 4 + B * TS * H * 12, 2 * 31 * M * H, NB + 1
     if cls == 2:
         return B * TS * H * 12 + B * H * 8, 10 * B * TS * H, NB + 1
     if cls == 3:
+        if dwgn:
+            return M * H * 2 + H * H * es + M * H * es, 2 * M * H * H, NB + 1
         return M * H * 4 + B * H * 8 + H * H * es + M * H * es, 2 * M * H * H, NB + 1
     if cls == 4:
         return M * H * es + H * H * es + 2 * M * H * 4 + 2 * stats + (M * H * 2 if fold else 0), 2 * M * H * H, NB + 1
@@ -296,8 +307,34 @@ def secondary_measurements(dev, nfe):
         r5 = dict(best)
         r5["note"] = ("BASELINE metric at the configs[1] length: the phoneme prefix length bisected so the seeded "
                       "duration flow gives ~400 frames (5 s); B = 1, nsteps-denoiser = 128")
+        r5["duration_flips"] = duration_flips(pr, base_phon[:, :r5["phonemes"]].to(dev), nfe_d, dev)
         out["end_to_end_5s"] = r5
     return out
+
+
+def duration_flips(pr, phon, nfe_d, dev, temperature=0.3):
+    """Integer duration flip rate of an end-to-end run (SURVEY.md §7 hard part 2): the same encoder
+    output and the same CPU-RNG noise (seed 0, as the timed e2e run draws it) through the HIP PVA flow
+    (exact-fp32 MFMA) and through the package's own fp32 torch-CPU PVA modules (the reference op order,
+    pva.py:97-112); frames = clamp(round(exp(d) - 1), 0) compared per phoneme."""
+    from flamed.models.synthesizer.pva import PVA
+    L = phon.shape[1]
+    smask = torch.zeros(1, L, dtype=torch.bool, device=dev)
+    with torch.inference_mode():
+        enc = pr.hip().encode(phon, smask)
+        torch.manual_seed(0)
+        d_g, s_g = pr.pva.flow(enc, smask, nfe_d, temperature)
+        cpu = PVA(pr.config["variance_adaptor"]).eval()
+        cpu.load_state_dict({k: v.detach().cpu() for k, v in pr.pva.state_dict().items()})
+        torch.manual_seed(0)
+        d_c, s_c = cpu.flow(enc.cpu(), smask.cpu(), nfe_d, temperature)
+
+    def frames(d):
+        return torch.clamp(torch.round(torch.exp(d.float().cpu()) - 1), min=0)
+    flips = int((frames(d_g) != frames(d_c)).sum()) + int((frames(s_g) != frames(s_c)).sum())
+    return {"phonemes": L, "durations_compared": 2 * L, "flips": flips, "flip_rate": flips / (2.0 * L),
+            "max_abs_log_dur_diff": float(max((d_g.cpu() - d_c).abs().max(), (s_g.cpu() - s_c).abs().max())),
+            "vs": "package fp32 torch-CPU PVA modules, same encoder output and noise"}
 
 
 def long_form(pg, dev, args, C, T=2400, nfe=256):
@@ -405,13 +442,86 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
             "kernels": ks, "fp8": fp8}
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) outside a torchrun job: start N ranks of this same script under
+    torch.distributed.run as a CHILD process (nothing here has touched the GPU: no exec from a process
+    that initialised HIP) and return its exit code.  One rank per GPU, RCCL over xGMI only for the
+    barrier and the max-over-ranks timing all-reduce (utterances shard with no data-path collective,
+    reference synthesize.py:268-291 batches)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def plumbing(args, rank, world):
+    """--plumbing: the launcher / timing / reporting harness on CPU over gloo (CI rehearsal of the
+    multi-rank path; no GPU): each rank runs ProbGenerator.sample on its own tiny synthetic shard with
+    the module's torch ops (the reference's --device cpu path, BASELINE configs[0]) and rank 0 prints
+    the same JSON line shape as the GPU bench."""
+    import torch.distributed as dist
+    from flamed.models.synthesizer.prob_generator import ProbGenerator
+    from flamed.utils.seeded_init import randomize_module
+    torch.set_num_threads(1)
+    if world > 1:
+        dist.init_process_group("gloo")
+    cfg = yaml.safe_load(open(os.path.join(REPO, "flamed-tts_amd", "configs", "prob.yaml")))
+    pg = ProbGenerator(cfg).eval()
+    randomize_module(pg, 20251205)
+    B, T, nfe = args.batch, args.frames, args.nfe
+    g = torch.Generator().manual_seed(args.seed + rank)
+    cond = torch.randn(B, cfg["n_quantizers"], T, cfg["cond_dim"], generator=g)
+    spk = torch.randn(B, cfg["target_dim"], generator=g)
+    mask = torch.ones(B, T, 1, dtype=torch.bool)
+    with torch.inference_mode():
+        for _ in range(max(1, args.warmup)):
+            pg.sample(cond, spk, mask, nfe=nfe, temperature=0.3)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = pg.sample(cond, spk, mask, nfe=nfe, temperature=0.3)
+        sec = (time.perf_counter() - t0) / args.steps
+        if world > 1:
+            dist.barrier()
+            tt = torch.tensor([sec], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            sec = float(tt.item())
+            per = torch.zeros(world, dtype=torch.float64)
+            per[rank] = B * T / sec
+            dist.all_reduce(per)
+    line = {"metric": "latent frames/s (plumbing: CPU torch path over gloo)", "value": round(world * B * T / sec, 3),
+            "unit": "latent frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(sec * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic", "plumbing": True, "finite": bool(torch.isfinite(out).all()),
+            "config": {"workload": f"CPU plumbing: {B} x {T} frames per rank, nfe={nfe}", "batch_per_gpu": B,
+                       "frames": T, "nfe": nfe, "global_batch": world * B,
+                       "parallelism": f"utterance-sharded x{world} (no collectives)"}}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     global FOLD
     args = parse()
     FOLD = args.lnfold != 0  # flamed_tune lnfold (kernel_costs applies the size policy)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.plumbing:
+        return plumbing(args, rank, world)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811

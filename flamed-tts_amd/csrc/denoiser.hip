@@ -1555,6 +1555,7 @@ struct Den {
   int tune_seen = -1;       // process tune epoch of that snapshot
   bool tune_own = false;    // set by flamed_den_tune: this handle keeps its own knobs
   int tune_ver = 0;         // bumped on every change of `tune` (graph cache key)
+  int part_epoch = -1;      // tune_ver pinned by the s0 == 0 part of a flamed_den_solve_part sequence
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
@@ -2196,6 +2197,10 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   const int G = graph_chunk(nfe);
   FL_REQUIRE(s0 % G == 0 && (s1 % G == 0 || s1 == nfe), "flamed_den_solve_part: range [%d, %d) not on %d-step graph chunks",
              s0, s1, G);
+  // the parts of one solve must run one step structure: a knob change between parts is rejected
+  if (s0 == 0) d->part_epoch = d->tune_ver;
+  FL_REQUIRE(d->part_epoch == d->tune_ver, "flamed_den_solve_part: knobs changed since step 0 of this solve (part [%d, %d))",
+             s0, s1);
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
   // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even
@@ -2269,10 +2274,21 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
   }
   constexpr int kSteps = 4;
   if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
-  hipEvent_t e0, e1;
-  FL_HIP(hipEventCreate(&e0));
-  FL_HIP(hipEventCreate(&e1));
-  const int saved_dup = d->tune.dup_class;  // the handle's active snapshot (this call's TuneScope)
+  // every exit (early error returns included) restores the handle's knob snapshot and frees the events
+  struct Restore {
+    Den* d;
+    int dup;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ~Restore() {
+      d->tune.dup_class = dup;
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+    }
+  } guard{d, d->tune.dup_class};
+  FL_HIP(hipEventCreate(&guard.e0));
+  FL_HIP(hipEventCreate(&guard.e1));
+  hipEvent_t e0 = guard.e0, e1 = guard.e1;
+  const int saved_dup = guard.dup;  // the handle's active snapshot (this call's TuneScope)
   // the step structure the solve graph uses: fused Euler steps (no combine launches) where it fuses
   const bool fused = den_fused_ok(d, B, T);
   DenWs w;
@@ -2320,8 +2336,6 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
     ms_out[c] = per_step[c] > 0 ? (t - base) / (float)per_step[c] : 0.f;
   }
   ms_out[FLAMED_DEN_KERNEL_CLASSES] = base;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return rc;
 }
 

@@ -401,7 +401,8 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   else std::lock(lk_d, lk_s);
   FL_ON_DEVICE(nd->device);
   FL_REQUIRE_ON(enc, nd->device, "flamed_pva_flow");
-  const Tune tsnap = tune_snapshot(nullptr);  // process defaults, read once for this call's GEMM launches
+  int tune_ep = 0;
+  const Tune tsnap = tune_snapshot(&tune_ep);  // process defaults, read once for this call's GEMM launches
   TuneScope ts_(&tsnap);
   if (ws_bytes < pva_ws_layout(nd, B, L, nfe, nullptr, nullptr)) {
     set_error("flamed_pva_flow: workspace too small");
@@ -433,7 +434,8 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   PvaGraph& gp = nd->graph;
   if (!gp.ctr) FL_HIP(hipMalloc(&gp.ctr, 256));
   std::vector<const void*> key = {nd, ns, enc, mask, dur_t, sil_t, ts, ws, (const void*)(intptr_t)nfe,
-                                  (const void*)(intptr_t)B, (const void*)(intptr_t)L, nd->dev, ns->dev};
+                                  (const void*)(intptr_t)B, (const void*)(intptr_t)L, nd->dev, ns->dev,
+                                  (const void*)(intptr_t)tune_ep};  // knobs (pva_split) are baked into the graph
   if (!gp.exec || gp.key != key) {
     if (gp.exec) { FL_HIP(hipGraphExecDestroy(gp.exec)); gp.exec = nullptr; }
     if (!gp.cap) FL_HIP(hipStreamCreateWithFlags(&gp.cap, hipStreamNonBlocking));

@@ -283,8 +283,11 @@ struct CapGraph {
 };
 
 template <class F>
-static int with_graph(CapGraph& g, const std::vector<const void*>& key, bool use_graph, hipStream_t st, F&& body) {
+static int with_graph(CapGraph& g, const std::vector<const void*>& key_in, bool use_graph, hipStream_t st, F&& body) {
   if (!use_graph) return body(st);
+  // the captured launches bake in the knobs the body read: the process tune epoch is part of the key
+  std::vector<const void*> key = key_in;
+  key.push_back((const void*)(intptr_t)tune_epoch());
   if (!g.exec || g.key != key) {
     if (g.exec) { FL_HIP(hipGraphExecDestroy(g.exec)); g.exec = nullptr; }
     if (!g.cap) FL_HIP(hipStreamCreateWithFlags(&g.cap, hipStreamNonBlocking));

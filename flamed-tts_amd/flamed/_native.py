@@ -144,6 +144,34 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what} failed (status {rc}): {msg.decode() if msg else ''}")
 
 
+_supported = {}
+
+
+def supported(kind: str, *dims) -> bool:
+    """Whether the library specialises a module's dims: runs flamed_<kind>_create (host-only: it
+    validates the dims and allocates no device memory) and destroys the handle again.  Ints are passed
+    as C ints, tuples as C int arrays.  The answer is cached per (kind, dims).  A module whose dims are
+    not specialised keeps its own torch ops on ROCm (as before the HIP path existed); a MISSING library
+    still raises (lib())."""
+    key = (kind,) + tuple(tuple(d) if isinstance(d, (list, tuple)) else int(d) for d in dims)
+    hit = _supported.get(key)
+    if hit is not None:
+        return hit
+    L = lib()
+    args = [(ctypes.c_int * len(d))(*d) if isinstance(d, tuple) else ctypes.c_int(d) for d in key[1:]]
+    h = ctypes.c_void_p()
+    ok = getattr(L, f"flamed_{kind}_create")(*args, ctypes.byref(h)) == 0
+    if ok and h.value:
+        getattr(L, f"flamed_{kind}_destroy")(h)
+    if not ok:
+        import warnings
+        msg = L.flamed_last_error()
+        warnings.warn(f"flamed HIP library does not specialise these {kind} dims ({msg.decode() if msg else ''}); "
+                      "the module runs on its torch ops")
+    _supported[key] = ok
+    return ok
+
+
 def ptr(t: torch.Tensor | None):
     if t is None:
         return None

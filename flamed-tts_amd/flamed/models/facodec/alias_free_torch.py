@@ -1,3 +1,5 @@
+# Adapted from https://github.com/junjun3518/alias-free-torch under the Apache License 2.0
+# (via the reference's flamed/models/facodec/alias_free_torch/, which carries the same notice).
 """Alias-free activation (drop-in for reference flamed/models/facodec/alias_free_torch/{act,filter,
 resample}.py): replicate-pad + 2x kaiser-sinc upsample -> activation -> 2x lowpass downsample.
 The filters are state-dict buffers (`upsample.filter`, `downsample.lowpass.filter`)."""

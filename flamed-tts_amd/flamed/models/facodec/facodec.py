@@ -162,14 +162,14 @@ class FACodecEncoder(nn.Module):
         super()._load_from_state_dict(*args, **kwargs)
 
     def _use_hip(self, x):
-        return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+        if not x.is_cuda or (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            return False
+        return self.hip_dims_ok()
 
-    def _vq_hip_ok(self, x, n_quantizers):
-        """The HIP prompt path covers the eval quantizers with every layer and the non-conditional timbre
-        encoder; anything else (training, n_quantizers < all, use_cln) stays on the torch modules."""
-        te = self.timbre_encoder
-        full = n_quantizers is None or all(n_quantizers >= q.num_quantizers for q in self.quantizer)
-        return self._use_hip(x) and full and not self.quantizer.training and not te.use_cln
+    def hip_dims_ok(self) -> bool:
+        """flamed_enc_create specialises these dims; otherwise the encoder keeps its torch ops."""
+        return nat.supported("enc", self.ngf, len(self.up_ratios), tuple(self.up_ratios), self.out_channels,
+                             nat.dtype_code(self.hip_dtype))
 
     def forward(self, x):
         """waveform (B, 1, n) -> (B, out_channels, T) (reference :215-217)."""
@@ -275,14 +275,27 @@ class FACodecDecoder(nn.Module):
         super()._load_from_state_dict(*args, **kwargs)
 
     def _use_hip(self, x):
-        return x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))
+        if not x.is_cuda or (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())):
+            return False
+        return self.hip_dims_ok()
+
+    def hip_dims_ok(self) -> bool:
+        """flamed_fac_create specialises these dims; otherwise the decoder keeps its torch ops."""
+        return nat.supported("fac", self.in_channels, self.upsample_initial_channel, len(self.up_ratios),
+                             tuple(self.up_ratios), nat.dtype_code(self.hip_dtype))
 
     def _vq_hip_ok(self, x, n_quantizers):
         """The HIP prompt path covers the eval quantizers with every layer and the non-conditional timbre
-        encoder; anything else (training, n_quantizers < all, use_cln) stays on the torch modules."""
+        encoder; anything else (training, n_quantizers < all, use_cln, dims flamed_vq_create does not
+        specialise) stays on the torch modules."""
         te = self.timbre_encoder
         full = n_quantizers is None or all(n_quantizers >= q.num_quantizers for q in self.quantizer)
-        return self._use_hip(x) and full and not self.quantizer.training and not te.use_cln
+        if not (x.is_cuda and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()))):
+            return False
+        if not full or self.quantizer.training or te.use_cln:
+            return False
+        d = VqHIP.dims_of(self)
+        return nat.supported("vq", tuple(d), len(d))
 
     def quantize(self, x, n_quantizers=None):
         """prosody and content RVQs on x, residual RVQ on x - (prosody + content) (reference :470-507)."""
@@ -549,7 +562,10 @@ class VqHIP:
             pass
 
     def dims(self) -> List[int]:
-        d = self.dec
+        return VqHIP.dims_of(self.dec)
+
+    @staticmethod
+    def dims_of(d) -> List[int]:
         te = d.timbre_encoder
         nl = [len(q.layers) for q in d.quantizer]
         ks = [q.layers[0]._codebook.weight.shape[0] for q in d.quantizer]

@@ -64,7 +64,12 @@ class PriorGenerator(nn.Module):
             return False
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             return False  # autograd training: the HIP path is inference-only
-        return True
+        return self.hip_dims_ok()
+
+    def hip_dims_ok(self) -> bool:
+        """flamed_prior_create specialises these dims (head widths 32 / 48, ...); else torch ops."""
+        d = PriorHIP.dims_of(self)
+        return nat.supported("prior", tuple(d), len(d))
 
     def hip(self) -> "PriorHIP":
         if self._hip is None:
@@ -162,7 +167,10 @@ class PriorHIP:
             pass
 
     def dims(self) -> List[int]:
-        pg = self.pg
+        return PriorHIP.dims_of(self.pg)
+
+    @staticmethod
+    def dims_of(pg: PriorGenerator) -> List[int]:
         tc = pg.config["transformer"]
         e, s = pg.encoder, pg.shared_decoder
         n_sym = e.src_word_emb.weight.shape[0] - 1

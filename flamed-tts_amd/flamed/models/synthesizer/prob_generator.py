@@ -194,6 +194,8 @@ class SimpleMLPAdaLN(nn.Module):
         self.num_res_blocks = num_res_blocks
         self.spk_dim = spk_dim
         self.kernel_size = convnext_kernel
+        self._convnext_plain = (convnext_stride == 1 and convnext_padding == convnext_kernel // 2 and convnext_expand == 1
+                                and convnext_groups in (None, model_channels))
         self.time_embed = TimestepEmbedder(model_channels)
         self.cond_embed = nn.Linear(spk_dim, model_channels)
         self.proj_in = nn.Linear(in_channels, model_channels)
@@ -229,7 +231,13 @@ class SimpleMLPAdaLN(nn.Module):
             return False
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             return False  # autograd training: the HIP path is inference-only
-        return True
+        return self.hip_dims_ok()
+
+    def hip_dims_ok(self) -> bool:
+        """The library specialises these dims (flamed_den_create accepts them; stride-1 'same' depthwise
+        ConvNeXt); otherwise the module keeps its torch ops on ROCm."""
+        return self._convnext_plain and nat.supported("den", self.in_channels, self.model_channels, self.num_res_blocks,
+                                                      self.kernel_size, self.spk_dim, nat.dtype_code(self.hip_dtype))
 
     def hip(self) -> "DenoiserHIP":
         if self._hip is None or self._hip.dtype_name != self.hip_dtype:
@@ -282,7 +290,13 @@ class ProbGenerator(nn.Module):
         if not cond.is_cuda:
             return False
         mods = (self.quantizer_encoding, self.cond_downsampling)
-        return not (torch.is_grad_enabled() and (cond.requires_grad or any(p.requires_grad for m in mods for p in m.parameters())))
+        if torch.is_grad_enabled() and (cond.requires_grad or any(p.requires_grad for m in mods for p in m.parameters())):
+            return False
+        return self.cond_hip_dims_ok()
+
+    def cond_hip_dims_ok(self) -> bool:
+        q, d = self.quantizer_encoding.quantizer_emb.weight.shape
+        return nat.supported("cond", q, d, self.target_dim, self.n_stages, nat.dtype_code(self.cond_hip_dtype))
 
     def fold_condition(self, cond, mask):
         """QuantizerEncoding + ConditionDownSampler (reference :435-436); on ROCm at inference one HIP
@@ -398,8 +412,13 @@ class DenoiserHIP:
         sidx = sidx.to(device=dev, dtype=torch.int32).contiguous()
         R = tidx.numel()
         ms = L.flamed_den_mods_stride(self.handle)  # modulation floats (+ LayerNorm-fold tables, bf16)
-        if out is not None and out.shape == (R, ms) and out.device == dev and out.dtype == torch.float32:
-            mods = out  # the solve's persistent table (its pointer is baked into the captured graph)
+        if out is not None:
+            # the solve's persistent table (its pointer is baked into the captured graph): a mismatch is a
+            # caller bug, never silently replaced by a fresh table the solve would not read
+            if out.shape != (R, ms) or out.device != dev or out.dtype != torch.float32 or not out.is_contiguous():
+                raise ValueError(f"adaln: out must be a contiguous float32 ({R}, {ms}) tensor on {dev}; got "
+                                 f"{tuple(out.shape)} {out.dtype} on {out.device}")
+            mods = out
         else:
             mods = torch.empty((R, ms), dtype=torch.float32, device=dev)
         nbytes = L.flamed_den_adaln_workspace_size(self.handle, t_vals.numel(), spk.shape[0])

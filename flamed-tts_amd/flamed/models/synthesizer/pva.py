@@ -110,7 +110,9 @@ class ProbabilisticModule(nn.Module):
 def _hip_ok(t: torch.Tensor, module: nn.Module) -> bool:
     if not t.is_cuda:
         return False
-    return not (torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()))
+    if torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()):
+        return False
+    return module.hip_dims_ok()
 
 
 def _lr_hip_ok(x: torch.Tensor) -> bool:
@@ -220,6 +222,11 @@ class PVA(nn.Module):
         phone_duration = torch.clamp(torch.round(torch.exp(dur_t) - 1), min=0)
         sil_duration = torch.clamp(torch.round(torch.exp(sil_t) - 1), min=0)
         return self.length_regulator(x, phone_duration, sil_duration, src_len, max_tgt_len)
+
+    def hip_dims_ok(self) -> bool:
+        """flamed_dur_create specialises both generators' dims; otherwise the torch ops run."""
+        return all(nat.supported("dur", g.input_size, g.filter_size, g.kernel)
+                   for g in (self.duration_generator, self.sil_generator))
 
     def hip(self) -> "PvaHIP":
         if self._hip is None:

@@ -132,3 +132,21 @@ def test_fp8_configs4_long_form():
     pg.denoiser.hip_graph = True
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_fp8_configs4_solve_vs_oracle():
+    """configs[4] as benchmarked: the 256-step B = 16, T = 2400 MX-fp8 graph solve (38,400 rows, fp8 GEMMs
+    active), utterance 0 against a single-utterance fp32 oracle solve (equal lengths: no padding coupling,
+    so a one-utterance reference is exact; reference prob_generator.py:439-447).  rel-L2 <= 5e-2."""
+    pg, sd = _prob_gen("fp8")
+    B, T, nfe = 16, 2400, 256
+    x, _, c = _inputs(17, B, T)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        sol = pg.denoiser.hip().solve(x.to(DEV), ts, c.to(DEV), nfe).cpu()
+    assert torch.isfinite(sol).all()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref = orc.euler_solve(sd, x[:1], c[:1], nfe)
+    e = rel_l2(sol[:1], ref)
+    print(f"fp8 configs[4] 256-step solve, utterance 0 vs fp32 oracle: rel-L2 {e:.3e}")
+    assert e < FP8_SOLVE, e

@@ -144,3 +144,42 @@ def test_tensor_version_handles_inference_tensors():
     with torch.inference_mode():
         u = torch.zeros(3)
     assert nat.tensor_version(u) == -1
+
+
+def test_hip_dims_gates_fall_back_to_torch():
+    """Dims the HIP library does not specialise keep the module on its torch ops (the gates ask the host-only
+    flamed_*_create validators; no GPU is touched), while the shipped configs are specialised."""
+    import copy
+    from flamed.models.synthesizer.prob_generator import ProbGenerator
+    from flamed.models.synthesizer.prior_generator import PriorGenerator
+    from flamed.models.synthesizer.pva import PVA
+    from flamed.models.facodec import FACodecDecoder, FACodecEncoder
+    prob = yaml.safe_load(open(os.path.join(PKG, "configs", "prob.yaml")))
+    prior = yaml.safe_load(open(os.path.join(PKG, "configs", "prior.yaml")))
+    pg = ProbGenerator(prob)
+    assert pg.denoiser.hip_dims_ok() and pg.cond_hip_dims_ok()
+    bad = copy.deepcopy(prob)
+    bad["hidden_dim"] = 96                      # H % 256 != 0
+    bad["downsampling_stages"] = 2              # cond fold specialises one stage
+    pgb = ProbGenerator(bad)
+    assert not pgb.denoiser.hip_dims_ok() and not pgb.cond_hip_dims_ok()
+    bad = copy.deepcopy(prob)
+    bad["convnext"]["kernel_size"], bad["convnext"]["padding"] = 7, 3   # only k = 31 is specialised
+    assert not ProbGenerator(bad).denoiser.hip_dims_ok()
+    assert PVA(prior["variance_adaptor"]).hip_dims_ok()
+    va = copy.deepcopy(prior["variance_adaptor"])
+    va["sil_generator"]["filter_size"] = 256
+    assert not PVA(va).hip_dims_ok()
+    assert PriorGenerator(prior).hip_dims_ok()
+    pb = copy.deepcopy(prior)
+    pb["transformer"]["decoder_head"] = 6       # head width 64 on the decoders: not specialised
+    assert not PriorGenerator(pb).hip_dims_ok()
+    from flamed import _native as nat
+    from flamed.models.facodec.facodec import VqHIP
+    from flamed.utils.random_ckpt import codec_models, load_yaml
+    enc, dec = codec_models(load_yaml("codec.yaml"))
+    assert dec.hip_dims_ok() and enc.hip_dims_ok()
+    d = VqHIP.dims_of(dec)
+    assert nat.supported("vq", tuple(d), len(d))
+    assert not FACodecDecoder(upsample_initial_channel=1536).hip_dims_ok()  # 1536 >> 4 = 96 channels: not specialised
+    assert not dec._use_hip(torch.zeros(1, 256, 4))  # CPU tensors never take the HIP path

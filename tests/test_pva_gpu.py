@@ -147,5 +147,36 @@ def test_pva_split_k_deterministic(pva, B, L):
     finally:
         nat.check(L_.flamed_tune(b"pva_split", 0), "tune")
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # the split really ran (the knob is part of the graph key): reassociated, so not bitwise equal
+    assert not (torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1]))
     for a, b in zip(outs[0], outs[2]):
         assert rel_l2(a.cpu(), b.cpu()) < 1e-5
+
+
+def test_pva_flow_default_nsteps_ragged(pva):
+    """The reference CLI's default --nsteps-durgen 64 (synthesize.py:338; loop pva.py:97-112) at an
+    end-to-end phoneme count (L = 285, the bench's 5 s utterance) on a ragged batch of 4: log-durations
+    rel-L2 <= 1e-5 against the oracle, and ZERO integer frame flips at every position that is not within
+    1e-4 of a .5 rounding boundary (positions near a boundary are counted and reported)."""
+    m, sd = pva
+    gen = torch.Generator().manual_seed(31)
+    B, L, nfe = 4, 285, 64
+    enc = torch.randn(B, L, 192, generator=gen)
+    lens = torch.tensor([285, 240, 131, 17])
+    mask = torch.arange(L)[None, :] >= lens[:, None]
+    torch.manual_seed(41)
+    dn, sn = torch.randn((B, L)), torch.randn((B, L))
+    with torch.inference_mode():
+        torch.manual_seed(41)
+        d, s = m.flow(enc.to(DEV), mask.to(DEV), nfe, 0.3)
+    rd, rs = orc.pva_flow(sd, enc, mask, nfe, 0.3, noise=(dn, sn))
+    assert rel_l2(d.cpu(), rd) < 1e-5 and rel_l2(s.cpu(), rs) < 1e-5
+    near, flips = 0, 0
+    for got, ref in ((d.cpu(), rd), (s.cpu(), rs)):
+        e = torch.exp(ref) - 1
+        safe = (e - e.floor() - 0.5).abs() > 1e-4
+        near += int((~safe).sum())
+        gf, rf = orc.log_to_frames(got), orc.log_to_frames(ref)
+        flips += int((gf[safe] != rf[safe]).sum())
+    print(f"PVA nfe=64 L=285 B=4: non-boundary flips {flips}, positions near a .5 boundary {near}")
+    assert flips == 0
