@@ -14,6 +14,7 @@
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
 #include "gemm_8p.hpp"
+#include "persist.hpp"
 
 #include <mutex>
 #include <string>
@@ -1566,6 +1567,12 @@ struct Den {
   static constexpr int kSplitCounters = 16384;
   int* gcnt = nullptr;  // fused GroupNorm-finalize counters, one per (utterance, 64-channel group)
   static constexpr int kGnCounters = 65536;
+  // persistent B = 1 solve (persist.hpp): scratch (counters first), pinned error word, device verdict
+  char* pmem = nullptr;
+  int* perr_host = nullptr;
+  int pdev_ok = -1;          // 1: 256 CUs and one 256-thread workgroup per CU fits; 0: not on this device
+  bool pbroken = false;      // a persistent solve timed out on this handle: launch path from then on
+  int pruns = 0;             // persistent launches completed
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1701,6 +1708,8 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
     if (d->ctr) (void)hipFree(d->ctr);
     if (d->scnt) (void)hipFree(d->scnt);
     if (d->gcnt) (void)hipFree(d->gcnt);
+    if (d->pmem) (void)hipFree(d->pmem);
+    if (d->perr_host) (void)hipHostFree(d->perr_host);
     if (d->dev) (void)hipFree(d->dev);
   }
   delete d;
@@ -1747,7 +1756,9 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     if (d->ctr) { (void)hipFree(d->ctr); d->ctr = nullptr; }
     if (d->scnt) { (void)hipFree(d->scnt); d->scnt = nullptr; }
     if (d->gcnt) { (void)hipFree(d->gcnt); d->gcnt = nullptr; }
+    if (d->pmem) { (void)hipFree(d->pmem); d->pmem = nullptr; }
     if (d->dev) { (void)hipFree(d->dev); d->dev = nullptr; }
+    d->pdev_ok = -1;
   }
   d->device = wdev;
   FL_ON_DEVICE(wdev);
@@ -2121,6 +2132,100 @@ static bool den_fused_ok(const Den* d, int B, int T) {
 // Steps per captured graph: the largest divisor of nfe that is <= tn().graph_steps (default 16; the
 // graph is replayed nfe/G times per solve, so a new (B, T) costs one G-step capture instead of an
 // nfe-step one).
+// ------------------------------ persistent B = 1 solve (persist.hpp) ------------------------------
+
+// Scratch of the persistent solve, sized for T <= pk::kMaxT: the counters first (the per-launch memset
+// block starts the allocation and is a multiple of 16 B), then the hand-off buffers and a copy of x.
+static size_t persist_layout(char* base, pk::Params* P, float** backup) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off = align256(off + bytes); return p; };
+  const size_t T = pk::kMaxT, H = pk::kH, C = pk::kC;
+  char* ctr = take(4 * (size_t)pk::kCtrInts);
+  char* xp0 = take(T * pk::kSlots * 8);
+  char* xp1 = take(T * pk::kSlots * 8);
+  char* ximg = take(T * H * 4);
+  char* a2 = take(T * H * 2);
+  char* u = take(T * H * 2);
+  char* xa = take(T * H * 2);
+  char* xs = take(T * C * 2);
+  char* gnp = take((size_t)pk::kGroups * H * 16);
+  char* yb = take((size_t)pk::kWGs * 16 * 4);
+  char* bk = take(T * C * 4);
+  if (P) {
+    P->ctr = reinterpret_cast<int*>(ctr);
+    P->xpart[0] = reinterpret_cast<float2*>(xp0);
+    P->xpart[1] = reinterpret_cast<float2*>(xp1);
+    P->ximg = reinterpret_cast<float*>(ximg);
+    P->a2 = reinterpret_cast<bf16*>(a2);
+    P->u = reinterpret_cast<bf16*>(u);
+    P->xa = reinterpret_cast<bf16*>(xa);
+    P->xs = reinterpret_cast<bf16*>(xs);
+    P->gnp = reinterpret_cast<float4*>(gnp);
+    P->yb = reinterpret_cast<float*>(yb);
+  }
+  if (backup) *backup = reinterpret_cast<float*>(bk);
+  return off;
+}
+
+// The persistent solve covers one utterance of 16..512 frames on a bf16 handle with the LayerNorm fold and
+// the shipped dims, on a device where all 256 workgroups are resident at once (one per CU: the grid-wide
+// hand-offs need every producer running), and never inside a stream capture (its error check syncs).
+static bool persist_eligible(Den* d, int B, int T, hipStream_t st) {
+  const Tune& tu = tn();
+  if (!tu.persist || d->pbroken || d->dt != FLAMED_BF16 || d->f8 || !d->fold || !tu.lnfold) return false;
+  if (B != 1 || T < 16 || T > pk::kMaxT || d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps)
+    return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  if (d->pdev_ok < 0) d->pdev_ok = pk::persist_device_ok(d->device) ? 1 : 0;
+  return d->pdev_ok == 1;
+}
+
+// Steps [s0, s1) of a B = 1 solve in one launch.  *done = false: not run (timed out and rolled back, the
+// handle then stays on the launch path) -- the caller runs the launch path.
+static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, int s0, int s1, hipStream_t st, bool* done) {
+  *done = false;
+  if (!d->pmem) FL_HIP(hipMalloc(&d->pmem, persist_layout(nullptr, nullptr, nullptr)));
+  if (!d->perr_host) FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&d->perr_host), sizeof(int), hipHostMallocDefault));
+  pk::Params P{};
+  float* backup = nullptr;
+  persist_layout(d->pmem, &P, &backup);
+  P.T = T; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
+  P.dt = (float)(1.0 / (double)nfe);
+  P.mods = mods; P.MS = d->MS; P.MS0 = d->MS0;
+  P.win = reinterpret_cast<const bf16*>(d->win); P.bin = d->bin;
+  for (int i = 0; i <= d->NB; ++i) {
+    const DenBlockW& b = i < d->NB ? d->blk[i] : d->fin;
+    pk::BlockW& o = P.blk[i];
+    o.w2 = reinterpret_cast<const bf16*>(b.w2); o.w3 = reinterpret_cast<const bf16*>(b.w3);
+    o.m0 = i < d->NB ? reinterpret_cast<const bf16*>(b.m0) : nullptr;
+    o.m2 = i < d->NB ? reinterpret_cast<const bf16*>(b.m2) : nullptr;
+    o.b2 = b.b2; o.b3 = b.b3; o.dww = b.dww; o.dwb = b.dwb; o.gnw = b.gnw; o.gnb = b.gnb;
+    if (i < d->NB) {
+      o.mb0 = b.mb0; o.mb2 = b.mb2; o.lnw = b.lnw; o.lnb = b.lnb; o.lnmw = b.lnmw; o.lnmb = b.lnmb;
+    }
+  }
+  P.wout = reinterpret_cast<const bf16*>(d->wout); P.bout = d->bout;
+  P.xt = xt;
+  P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
+  const size_t xbytes = (size_t)T * pk::kC * 4;
+  FL_HIP(hipMemcpyAsync(backup, xt, xbytes, hipMemcpyDeviceToDevice, st));
+  FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pk::kCtrInts, st));
+  const int lrc = pk::persist_launch(P, st);
+  if (lrc) return lrc;
+  FL_HIP(hipMemcpyAsync(d->perr_host, P.ctr + pk::CT_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
+  FL_HIP(hipStreamSynchronize(st));
+  if (*d->perr_host != 0) {  // a wait timed out: every workgroup left; x is rolled back
+    FL_HIP(hipMemcpyAsync(xt, backup, xbytes, hipMemcpyDeviceToDevice, st));
+    d->pbroken = true;
+    fprintf(stderr, "flamed: persistent solve timed out (T=%d); this handle uses the launch path from now on\n", T);
+    return kOk;
+  }
+  *done = true;
+  ++d->pruns;
+  return kOk;
+}
+
 static int graph_chunk(int nfe) {
   const int gs = tn().graph_steps;
   for (int g = gs < nfe ? gs : nfe; g > 1; --g)
@@ -2167,6 +2272,15 @@ FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe) {
   return graph_chunk(nfe);
 }
 
+FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && runs && broken, "flamed_den_persist_info: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  *runs = d->pruns;
+  *broken = d->pbroken ? 1 : 0;
+  return kOk;
+}
+
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t st) {
   return flamed_den_solve_part(h, xt, mods, nfe, B, T, ws, ws_bytes, use_graph, 0, nfe, st);
@@ -2201,6 +2315,11 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   if (s0 == 0) d->part_epoch = d->tune_ver;
   FL_REQUIRE(d->part_epoch == d->tune_ver, "flamed_den_solve_part: knobs changed since step 0 of this solve (part [%d, %d))",
              s0, s1);
+  if (persist_eligible(d, B, T, st)) {  // one persistent launch for the whole range (B = 1)
+    bool done = false;
+    const int prc = persist_solve(d, xt, mods, nfe, T, s0, s1, st, &done);
+    if (prc != kOk || done) return prc;
+  }
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
   // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even

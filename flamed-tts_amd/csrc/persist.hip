@@ -1,0 +1,684 @@
+// Persistent B = 1 Euler solve kernel (design notes: persist.hpp).
+#include "flamed_hip.h"
+#include "persist.hpp"
+#include "gemm_dma.hpp"
+
+namespace fl {
+namespace pk {
+
+// Diagnostic build only (FL_STAMPS, libflamed_hip_stamps.so): thread 0 of every workgroup records
+// s_memrealtime (100 MHz, chip-wide) at each wait / compute / signal point of one chosen step into
+// g_pst[workgroup][k] (flamed_persist_stamps; tools/persist_timeline.py).
+#ifdef FL_STAMPS
+__device__ unsigned long long* g_pst = nullptr;
+__device__ int g_pst_step = -1;
+constexpr int kStampSlots = 160;
+#define PST(step)                                                                                       \
+  do {                                                                                                  \
+    if ((step) == g_pst_step && g_pst && threadIdx.x == 0 && pst_k < kStampSlots)                       \
+      g_pst[blockIdx.x * kStampSlots + pst_k] = __builtin_amdgcn_s_memrealtime();                      \
+    ++pst_k;                                                                                            \
+  } while (0)
+#else
+#define PST(step) ((void)0)
+#endif
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+// write-through (sc1) 16-B store / sc1 16-B load (aux 16 = sc1)
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+__device__ __forceinline__ float4 as_f4(u32x4 v) { return __builtin_bit_cast(float4, v); }
+// An opaque copy of a lane index: address arithmetic derived from it is computed where it is used, inside
+// the step loop, instead of being hoisted into hundreds of loop-invariant registers (LDS fragment
+// offsets, DMA source addresses of every phase).
+__device__ __forceinline__ int opq(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Row range of group g: whole 16-row tiles [g MT / 8, (g + 1) MT / 8).
+__device__ __forceinline__ void group_rows(int g, int T, int& r0, int& nr) {
+  const int MT = (T + 15) >> 4;
+  const int tb = g * MT / kGroups, te = (g + 1) * MT / kGroups;
+  r0 = 16 * tb;
+  nr = max(min(16 * te, T) - r0, 0);
+}
+
+// ---- hand-off primitives ----
+// Every storing wave drains its (sc1) stores, the workgroup meets, one lane adds to the counter.
+__device__ __forceinline__ void signal(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 polls n counters (base + k * stride, k < n) with sc1 loads until all reach `target` (s_sleep
+// between polls); bounded by P.tmo, and an error word set by any workgroup ends every wait.  The
+// other waves meet it at a barrier.  Returns false when the solve is being abandoned.
+__device__ __forceinline__ bool wait_ge(int* err, long long tmo, int* base, int stride, int n, int target, int* flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (unsigned it = 0;; ++it) {
+      bool mine = true;
+      if (lane < n) mine = __hip_atomic_load(base + lane * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      if (__all(mine)) break;
+      if ((it & 31) == 31) {  // the error word and the clock only every 32 polls: one round trip per poll
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
+          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = false;
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *flag = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = *flag != 0;
+  __syncthreads();  // the flag word is rewritten by the next wait
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: hand-off loads stay below the poll
+  return ok;
+}
+
+// ---- weight panels: 32 rows (output columns) x K bf16, 16-B chunks XOR-swizzled by row & 15 (the 16
+// lanes of a ds_read_b128 group hit 16 distinct 16-B slots); the swizzle is applied to each lane's DMA
+// SOURCE chunk (an involution), since LDS-DMA writes a wave's 64 lanes linearly.
+template <int K>
+__device__ __forceinline__ int woff(int n, int j) { return n * (2 * K) + ((j ^ (n & 15)) << 4); }
+
+template <int K, class RowF>
+__device__ __forceinline__ void dma_panel(char* dst, RowF rowp, int wave, int lane_in) {
+  constexpr int kRowB = 2 * K, kNI = 32 * kRowB / 1024, kPer = kNI / 4;
+  const int lane = opq(lane_in);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = wave * kPer + k;
+    const int pos = i * 1024 + lane * 16;
+    const int n = pos / kRowB, jl = (pos % kRowB) >> 4;
+    glds16(reinterpret_cast<const char*>(rowp(n)) + ((jl ^ (n & 15)) << 4), dst + i * 1024);
+  }
+}
+
+// ---- one GEMM phase: wave w < ntile computes rows [16 w, 16 w + 16) of the group's tile x the slot's 32
+// columns: A (bf16 rows, K) straight to registers with sc1 loads (rows >= nr read as 0: buffer range),
+// B fragments from the LDS weight panel.
+template <int K>
+__device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[2], int wave, int lane_in) {
+  constexpr int KST = K / 32;
+  const int lane = opq(lane_in);
+  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ntile = (nr + 15) >> 4;
+  const int c = lane & 15, q = lane >> 4;
+  u32x4 a[KST];
+  if (wave < ntile) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
+    const unsigned base = (unsigned)(((16 * wave + c) * K + q * 8) * 2);
+#pragma unroll
+    for (int ks = 0; ks < KST; ++ks) a[ks] = ld16(rs, base + ks * 64);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KST) : "memory");  // this wave's (older) weight DMA landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();  // every wave's DMA: the whole panel is in LDS
+  if (wave < ntile) {
+#pragma unroll
+    for (int ks = 0; ks < KST; ++ks) {
+      const u32x4 b0 = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * ks + q));
+      const u32x4 b1 = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * ks + q));
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, b0), acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, b1), acc[1], 0, 0, 0);
+    }
+  }
+}
+
+// LayerNorm partials (mean, M2 over the slot's 32 columns) of the wave's 16 rows, from the MFMA layout
+// (lane c, q holds rows 4q + i, columns c and 16 + c): write-through 8-B stores.
+__device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int wave, int lane_in) {
+  const int lane = opq(lane_in);
+  const int c = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float sm = wave_sum16(x[0][i] + x[1][i]);
+    const float mean = sm * (1.0f / kCols);
+    const float d0 = x[0][i] - mean, d1 = x[1][i] - mean;
+    const float m2 = wave_sum16(d0 * d0 + d1 * d1);
+    const int row = 16 * wave + 4 * q + i;
+    if (c == 0 && row < nr) {
+      const float2 v = make_float2(mean, m2);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(xpart + (size_t)(r0 + row) * kSlots + s),
+                         __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// (mean, rstd) of rows [ra, rb) from the 32 slots' partials (sc1 loads), into st[2 (r - rbase)]; two
+// lanes per row (16 partials each), combined as row_stats_from_partials does (tile width 32, eps 1e-6).
+__device__ __forceinline__ void row_stats(const float2* xpart, int T, int ra, int rb, int rbase, float* st) {
+  const int n2 = 2 * (rb - ra);
+  const __amdgpu_buffer_rsrc_t rs = rsrc(xpart, (unsigned)T * kSlots * 8);
+  for (int idx = opq(threadIdx.x); idx < ((n2 + 63) & ~63); idx += kThreads) {
+    const bool act = idx < n2;
+    const int row = ra + (act ? idx >> 1 : 0), half = idx & 1;
+    float mv[16], qv[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float4 v = as_f4(ld16(rs, (unsigned)((row * kSlots + half * 16 + 2 * k) * 8)));
+      mv[2 * k] = v.x; qv[2 * k] = v.y; mv[2 * k + 1] = v.z; qv[2 * k + 1] = v.w;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm += mv[k];
+    sm += __shfl_xor(sm, 1);
+    const float mean = sm * (1.0f / kSlots);
+    float m2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float d = mv[k] - mean;
+      m2 += qv[k] + (float)kCols * d * d;
+    }
+    m2 += __shfl_xor(m2, 1);
+    if (act && half == 0) {
+      st[2 * (row - rbase)] = mean;
+      st[2 * (row - rbase) + 1] = 1.0f / sqrtf(m2 * (1.0f / kH) + 1e-6f);
+    }
+  }
+}
+
+// Stage the wave's (16 rows x 32 columns) values in LDS (row-major [64][32] of OT) ...
+template <typename OT>
+__device__ __forceinline__ void stage_tile(char* stg, const float (&v)[2][4], int wave, int lane_in) {
+  const int lane = opq(lane_in);
+  const int c = lane & 15, q = lane >> 4;
+  OT* t = reinterpret_cast<OT*>(stg);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 16 * wave + 4 * q + i;
+    t[row * kCols + c] = (OT)v[0][i];
+    t[row * kCols + 16 + c] = (OT)v[1][i];
+  }
+}
+// ... then write it through with 16-B sc1 stores (rows [ra, rb) of the tile) into dst (row stride ld).
+template <typename OT>
+__device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int r0, int ra, int rb, int col0, int T) {
+  constexpr int CPR = kCols * (int)sizeof(OT) / 16;  // 16-B chunks per staged row
+  const __amdgpu_buffer_rsrc_t rs = rsrc(dst, (unsigned)T * ld * (unsigned)sizeof(OT));
+  for (int idx = opq(threadIdx.x); idx < kMaxRows * CPR; idx += kThreads) {
+    const int row = idx / CPR, ch = idx % CPR;
+    if (row < ra || row >= rb) continue;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(stg + (row * kCols * sizeof(OT)) + ch * 16);
+    st16(rs, (unsigned)(((size_t)(r0 + row) * ld + col0) * sizeof(OT) + ch * 16), v);
+  }
+}
+
+__device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) {
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[nt][i] = acc[nt][i];
+}
+
+__global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.x % kGroups, s = blockIdx.x / kGroups;
+  const int T = P.T, H = kH;
+  int r0, nr;
+  group_rows(g, T, r0, nr);
+  const int c = lane & 15, q = lane >> 4;
+  const int col0 = kCols * s;
+  char* stg = smem + L_HS;  // epilogue staging (aliases the dwconv window)
+  float* hs = reinterpret_cast<float*>(smem + L_HS);
+  float* st = reinterpret_cast<float*>(smem + L_ST);  // window frame r0 - 15 + p -> (mean, rstd) at st[2 p]
+  float* red = reinterpret_cast<float*>(smem + L_RED);
+  float4* gnv = reinterpret_cast<float4*>(smem + L_GNV);
+  int* flag = reinterpret_cast<int*>(smem + L_FLAG);
+  int* grp = P.ctr + CT_GRP;
+  int* mygrp = grp + 16 * g;
+  int* gnc = P.ctr + CT_GN + 16 * s;
+  int* errw = P.ctr + CT_ERR;
+  const long long tmo = P.tmo;
+  int L = 0;    // group signals so far (the same sequence in every workgroup)
+  int ndg = 0;  // GroupNorm hand-offs so far
+  int wb = 0;   // LDS buffer holding (or receiving) the weights of the next GEMM phase
+  const int wbase = 16 * wave;  // first tile row of this wave
+#ifdef FL_STAMPS
+  int pst_k = 0;
+#endif
+  // after a GEMM phase: the next GEMM's panel goes into the buffer the finished one did not use
+  auto next_w = [&](const bf16* W) {
+    wb ^= 1;
+    dma_panel<kH>((smem + wb * kWPanel), [&](int n) { return W + (size_t)(col0 + n) * kH; }, wave, lane);
+  };
+  auto next_win = [&]() {
+    wb ^= 1;
+    dma_panel<kC>((smem + wb * kWPanel), [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane);
+  };
+
+  // Euler state: thread -> tile row xr_row, channels 8 s + 2 (tid & 3) + {0, 1}
+  const int xr_row = tid >> 2, xch = kCh * s + 2 * (tid & 3);
+  float xs0 = 0.f, xs1 = 0.f;
+  if (xr_row < nr) {
+    xs0 = P.xt[(size_t)(r0 + xr_row) * kC + xch];
+    xs1 = P.xt[(size_t)(r0 + xr_row) * kC + xch + 1];
+  }
+  // weights of the first GEMM (proj_in) while the state is published
+  dma_panel<kC>(smem, [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane);
+  // bf16 rows of x (proj_in's operand): 16 B per tile row, staged in LDS
+  auto publish_xs = [&]() {
+    bf16* t = reinterpret_cast<bf16*>(stg);
+    t[xr_row * kCh + 2 * (tid & 3)] = (bf16)xs0;
+    t[xr_row * kCh + 2 * (tid & 3) + 1] = (bf16)xs1;
+    __syncthreads();
+    if (tid < nr) {
+      const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)T * kC * 2);
+      st16(rs, (unsigned)(((size_t)(r0 + tid) * kC + kCh * s) * 2), *reinterpret_cast<const u32x4*>(stg + tid * 16));
+    }
+    signal(mygrp);
+    ++L;
+  };
+  publish_xs();
+
+  float X[2][4];  // residual stream tile (this wave's 16 rows x 32 columns), MFMA layout
+  f32x4 acc[2];
+
+  for (int step = P.s0; step < P.s1; ++step) {
+    const float* md = P.mods + (size_t)step * P.MS;
+    // ------------------------------ proj_in (:361) ------------------------------
+    PST(step);
+    if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+    PST(step);
+    gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+    PST(step);
+    acc_to(X, acc);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const float b = P.bin[col0 + 16 * nt + c];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) X[nt][i] += b;
+    }
+    if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
+    stage_tile<float>(stg, X, wave, lane);
+    __syncthreads();
+    flush_tile<float>(stg, P.ximg, H, r0, 0, nr, col0, T);
+    signal(mygrp);
+    PST(step);
+    ++L;
+    next_w(P.blk[0].w2);
+
+    for (int blk = 0; blk <= P.NB; ++blk) {
+      const bool fin = blk == P.NB;
+      const BlockW& bw = P.blk[blk];
+      const float* mb = md + (size_t)blk * 6 * H;  // [sh, sc, gate] of the ConvNeXt LN (+ [sh, sc, gate] of the next)
+      // per-column LN affine + AdaLN modulation: va = w (1 + sc), vb = b (1 + sc) + sh (no affine: w = 1, b = 0)
+      auto vab = [&](int col, float& va, float& vb) {
+        const float sc1 = 1.0f + mb[H + col];
+        va = fin ? sc1 : bw.lnw[col] * sc1;
+        vb = fin ? mb[col] : bw.lnb[col] * sc1 + mb[col];
+      };
+
+      // -------- LN + modulate + depthwise k31 + GroupNorm(H, H) over T (prob_generator.py:81-89, 153-156)
+      PST(step);
+      if (!wait_ge(errw, tmo, grp, 16, kGroups, 32 * L, flag)) return;  // every group: the halo rows of the neighbours
+      PST(step);
+      const int wa = max(r0 - kHalo, 0), wz = min(r0 + nr + kHalo, T);
+      row_stats(P.xpart[0], T, wa, wz, r0 - kHalo, st);
+      __syncthreads();
+      // window h[p] (frame r0 - 15 + p): own rows from X (registers), halo rows from ximg, 0 outside [0, T)
+      {
+        const __amdgpu_buffer_rsrc_t rx = rsrc(P.ximg, (unsigned)T * H * 4);
+        for (int idx = tid; idx < kWin * 8; idx += kThreads) {
+          const int p = idx >> 3, ch = idx & 7, r = r0 - kHalo + p;
+          if (p >= kHalo && p < kHalo + nr) continue;  // own rows: below
+          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (r >= 0 && r < T) {
+            const float4 xv = as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * ch) * 4)));
+            const float mean = st[2 * p], rstd = st[2 * p + 1];
+            float va, vb;
+            vab(col0 + 4 * ch, va, vb);
+            o.x = ((xv.x - mean) * rstd) * va + vb;
+            vab(col0 + 4 * ch + 1, va, vb);
+            o.y = ((xv.y - mean) * rstd) * va + vb;
+            vab(col0 + 4 * ch + 2, va, vb);
+            o.z = ((xv.z - mean) * rstd) * va + vb;
+            vab(col0 + 4 * ch + 3, va, vb);
+            o.w = ((xv.w - mean) * rstd) * va + vb;
+          }
+          *reinterpret_cast<float4*>(hs + p * kCols + 4 * ch) = o;
+        }
+        if (wbase < nr) {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            float va, vb;
+            vab(col0 + 16 * nt + c, va, vb);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = wbase + 4 * q + i;
+              if (row < nr) {
+                const int p = row + kHalo;
+                hs[p * kCols + 16 * nt + c] = ((X[nt][i] - st[2 * p]) * st[2 * p + 1]) * va + vb;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+      // depthwise conv (zero padding at the utterance edges): thread -> channel cc, tile rows 8 rg .. 8 rg + 7
+      const int cc = tid & 31, rg = tid >> 5;
+      float d[8];
+      {
+        const int col = col0 + cc;
+        float w[kTaps];
+#pragma unroll
+        for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col];
+        const float bias = bw.dwb[col];
+        float win[8 + kTaps - 1];
+#pragma unroll
+        for (int j = 0; j < 8 + kTaps - 1; ++j) win[j] = hs[(8 * rg + j) * kCols + cc];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float a = bias;
+#pragma unroll
+          for (int j = 0; j < kTaps; ++j) a = fmaf(w[j], win[k + j], a);
+          d[k] = a;
+        }
+      }
+      // GroupNorm partials of this group's frames: exact two passes (sum, squared deviations)
+      const int nv = min(max(nr - 8 * rg, 0), 8);
+      {
+        float sm = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k < nv) sm += d[k];
+        red[rg * kCols + cc] = sm;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) tot += red[k * kCols + cc];
+        const float mg = nr > 0 ? tot / (float)nr : 0.f;
+        __syncthreads();
+        float m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k < nv) {
+            const float e = d[k] - mg;
+            m2 = fmaf(e, e, m2);
+          }
+        red[rg * kCols + cc] = m2;
+        __syncthreads();
+        if (tid < kCols) {
+          float m2t = 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) m2t += red[k * kCols + cc];
+          const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
+          st16(rq, (unsigned)((g * H + col0 + cc) * 16), __builtin_bit_cast(u32x4, make_float4((float)nr, mg, m2t, 0.f)));
+        }
+      }
+      signal(gnc);
+      PST(step);
+      ++ndg;
+      PST(step);
+      if (!wait_ge(errw, tmo, gnc, 0, 1, kGroups * ndg, flag)) return;
+      PST(step);
+      if (tid < kCols) {  // the 8 groups' partials of this channel, Chan-combined in group order
+        const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
+        float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < kGroups; ++k) {
+          const float4 v = as_f4(ld16(rq, (unsigned)((k * H + col0 + tid) * 16)));
+          chan_combine(n, mean, m2, v.x, v.y, v.z);
+        }
+        const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * bw.gnw[col0 + tid];
+        gnv[tid] = make_float4(mean, sc, bw.gnb[col0 + tid], 0.f);
+      }
+      __syncthreads();
+      {
+        const float4 gv = gnv[cc];
+        bf16* t = reinterpret_cast<bf16*>(stg);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[(8 * rg + k) * kCols + cc] = (bf16)((d[k] - gv.x) * gv.y + gv.z);
+      }
+      __syncthreads();
+      flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T);
+      signal(mygrp);
+      PST(step);
+      ++L;
+
+      // -------- conv_2 (1x1) + GELU (:90-91)
+      PST(step);
+      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      PST(step);
+      gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+      PST(step);
+      {
+        float v[2][4];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const float b = bw.b2[col0 + 16 * nt + c];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b);
+        }
+        stage_tile<bf16>(stg, v, wave, lane);
+      }
+      __syncthreads();
+      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T);
+      signal(mygrp);
+      PST(step);
+      ++L;
+      next_w(bw.w3);
+
+      // -------- conv_3 (1x1) + ConvNeXt residual + gated residual (:92-93, 109, 156); x * alpha for the fold
+      PST(step);
+      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      PST(step);
+      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+      PST(step);
+      {
+        float v[2][4];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int col = col0 + 16 * nt + c;
+          float va, vb;
+          vab(col, va, vb);
+          const float gate = mb[2 * H + col], b3 = bw.b3[col];
+          // alpha = w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second)
+          const float al = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int p = wbase + 4 * q + i + kHalo;
+            const float xh = (X[nt][i] - st[2 * p]) * st[2 * p + 1];
+            const float h = xh * va + vb;
+            X[nt][i] = X[nt][i] + gate * (h + (acc[nt][i] + b3));
+            v[nt][i] = X[nt][i] * al;
+          }
+        }
+        if (wbase < nr) store_partials(P.xpart[1], X, r0, nr, s, wave, lane);
+        stage_tile<bf16>(stg, v, wave, lane);
+      }
+      __syncthreads();
+      flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T);
+      signal(mygrp);
+      PST(step);
+      ++L;
+      if (fin) break;  // conv_out follows the FinalLayer's conv_3
+      next_w(bw.m0);
+
+      // -------- mlp.0 + SiLU, the LayerNorm folded into the epilogue (:157-158)
+      PST(step);
+      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      PST(step);
+      row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
+      gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane);  // (its barrier orders the statistics)
+      PST(step);
+      {
+        const float* fo = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
+        float v[2][4];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int col = col0 + 16 * nt + c;
+          const float fa = fo[col], fb = fo[H + col];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int p = wbase + 4 * q + i + kHalo;
+            v[nt][i] = silu(st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa) + fb);
+          }
+        }
+        stage_tile<bf16>(stg, v, wave, lane);
+      }
+      __syncthreads();
+      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T);
+      signal(mygrp);
+      PST(step);
+      ++L;
+      next_w(bw.m2);
+
+      // -------- mlp.2 + gated residual (:159-160)
+      PST(step);
+      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      PST(step);
+      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+      PST(step);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = col0 + 16 * nt + c;
+        const float gate = mb[5 * H + col], b = bw.mb2[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X[nt][i] = X[nt][i] + gate * (acc[nt][i] + b);
+      }
+      if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
+      stage_tile<float>(stg, X, wave, lane);
+      __syncthreads();
+      flush_tile<float>(stg, P.ximg, H, r0, 0, nr, col0, T);
+      signal(mygrp);
+      PST(step);
+      ++L;
+      next_w(P.blk[blk + 1].w2);
+    }
+
+    // -------- conv_out k3 (taps stacked; LayerNorm + modulate folded; :238-245, 264).  Panel row n < 24 is
+    // tap n / 8 of latent channel 8 s + n % 8; rows 24..31 repeat rows 0..7 (ignored)
+    wb ^= 1;
+    dma_panel<kH>((smem + wb * kWPanel), [&](int n) {
+      const int m = n < 24 ? n : n - 24;
+      return P.wout + (size_t)((m >> 3) * kC + kCh * s + (m & 7)) * kH;
+    }, wave, lane);
+    PST(step);
+    if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+    PST(step);
+    row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
+    gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+    PST(step);
+    float* yl = reinterpret_cast<float*>(stg);  // Y of the tile: [row][24] fp32 (tap-major x 8 channels)
+    {
+      const float* fo = md + P.MS0 + (size_t)P.NB * 2 * H;  // [wa (3 C), wb (3 C)]
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = 16 * nt + c;
+        if (n < 24) {
+          const int ns = (n >> 3) * kC + kCh * s + (n & 7);  // stacked output column
+          const float fa = fo[ns], fb = fo[3 * kC + ns];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = wbase + 4 * q + i, p = row + kHalo;
+            yl[row * 24 + n] = st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa) + fb;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // publish what the neighbouring groups' Euler updates need: Y0 of the last frame, Y2 of the first
+    if (tid < 4 && nr > 0) {
+      const __amdgpu_buffer_rsrc_t ry = rsrc(P.yb, kWGs * 16 * 4);
+      const int half = tid >> 1, k = tid & 1;
+      const float* src = half == 0 ? yl + (nr - 1) * 24 + 4 * k : yl + 16 + 4 * k;
+      st16(ry, (unsigned)((blockIdx.x * 16 + half * 8 + 4 * k) * 4), __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(src)));
+    }
+    signal(mygrp);
+    PST(step);
+    ++L;
+    if (step + 1 < P.s1) next_win();
+
+    // -------- Euler update x += dt * v, v[t] = b + Y1[t] + Y0[t-1] + Y2[t+1] (:445; conv3_combine order)
+    PST(step);
+    if (!wait_ge(errw, tmo, grp, 16, kGroups, 32 * L, flag)) return;
+    PST(step);
+    if (xr_row < nr) {
+      const int t = r0 + xr_row;
+      int gp = 0, gn_ = 0;  // the groups owning frames r0 - 1 and r0 + nr (nearest non-empty neighbours)
+      for (int k = 0; k < kGroups; ++k) {
+        int a, b;
+        group_rows(k, T, a, b);
+        if (b > 0 && a + b == r0) gp = k;
+        if (b > 0 && a == r0 + nr) gn_ = k;
+      }
+      const __amdgpu_buffer_rsrc_t ry = rsrc(P.yb, kWGs * 16 * 4);
+      float vv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int chl = 2 * (tid & 3) + e, ch = kCh * s + chl;
+        float v = P.bout[ch] + yl[xr_row * 24 + 8 + chl];
+        if (t > 0) {
+          const float y0 = xr_row > 0 ? yl[(xr_row - 1) * 24 + chl]
+                                      : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            ry, (unsigned)(((gp + kGroups * s) * 16 + chl) * 4), 0, 16));
+          v += y0;
+        }
+        if (t < T - 1) {
+          const float y2 = xr_row < nr - 1 ? yl[(xr_row + 1) * 24 + 16 + chl]
+                                           : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 ry, (unsigned)(((gn_ + kGroups * s) * 16 + 8 + chl) * 4), 0, 16));
+          v += y2;
+        }
+        vv[e] = v;
+      }
+      xs0 = __fadd_rn(xs0, __fmul_rn(P.dt, vv[0]));
+      xs1 = __fadd_rn(xs1, __fmul_rn(P.dt, vv[1]));
+    }
+    __syncthreads();  // yl (staging) is rewritten by publish_xs
+    if (step + 1 < P.s1) publish_xs();
+  }
+  if (xr_row < nr) {
+    P.xt[(size_t)(r0 + xr_row) * kC + xch] = xs0;
+    P.xt[(size_t)(r0 + xr_row) * kC + xch + 1] = xs1;
+  }
+}
+
+#ifdef FL_STAMPS
+int persist_stamps(void* buf, int step) {
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(buf);
+  FL_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pst), &p, sizeof(p)));
+  FL_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_step), &step, sizeof(step)));
+  return kOk;
+}
+#endif
+
+bool persist_device_ok(int device) {
+  int cus = 0, nb = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus != kWGs) return false;
+  if (set_max_lds(reinterpret_cast<const void*>(den_persist_kernel)) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, den_persist_kernel, kThreads, kLds) != hipSuccess) return false;
+  return nb >= 1;
+}
+
+int persist_launch(const Params& P, hipStream_t st) {
+  hipLaunchKernelGGL(den_persist_kernel, dim3(kWGs), dim3(kThreads), kLds, st, P);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+}  // namespace pk
+}  // namespace fl
+
+#ifdef FL_STAMPS
+extern "C" FLAMED_API int flamed_persist_stamps(void* buf, int step) { return fl::pk::persist_stamps(buf, step); }
+#endif

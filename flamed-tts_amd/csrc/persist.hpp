@@ -1,0 +1,86 @@
+// Persistent B = 1 Euler solve: every step of ProbGenerator.sample's ODE loop (reference
+// flamed/models/synthesizer/prob_generator.py:434-447; one SimpleMLPAdaLN.forward :349-365 per step)
+// in ONE launch of 256 workgroups (one per CU), the phases of a step chained by in-launch hand-offs
+// instead of 25 kernel boundaries.
+//
+// Work split (speed only; correctness never depends on placement).  Workgroup b is (group g = b % 8,
+// slot s = b / 8): under the round-robin dispatch the 32 slots of a group share one XCD and its L2.
+// Group g owns a contiguous range of <= 64 frames (whole 16-row MFMA tiles); slot s owns hidden
+// columns [32 s, 32 s + 32) and latent channels [8 s, 8 s + 8).  What stays on chip across phases:
+//   * the residual stream X of the workgroup's (frames x 32 columns) tile, in registers;
+//   * the Euler state x of its (frames x 8 channels), in registers across ALL steps (fp32);
+//   * each GEMM phase's weight panel (32 output columns x K, bf16), LDS-DMA'd into one of two LDS
+//     buffers by the previous GEMM phase, so a phase only waits for its activations.
+// Every activation handed to another workgroup (bf16 GEMM operands, LayerNorm row partials, halo rows,
+// GroupNorm partials, conv_out boundary rows) is stored write-through (sc1), drained by every storing
+// wave, then one lane adds to a counter; consumers poll with sc1 loads and read the data with sc1
+// loads only (cdna_hip_programming.md §6 Guideline 16, table row 1: no release / acquire fences).
+//   group counters  grp[g]: the 32 slots of g add 1 after each group phase (GEMM operands, partials)
+//   GroupNorm       gn[s]:  the 8 groups' slot-s workgroups add 1 after publishing their partials
+// Per step: proj_in, 4 x (dwconv+GroupNorm, conv_2, conv_3, mlp.0, mlp.2), FinalLayer (dwconv+
+// GroupNorm, conv_2, conv_3, conv_out), Euler update.  Numerics follow the bf16 launch path (bf16
+// operands, fp32 accumulation / residual / statistics / state, the LayerNorm fold of mlp.0 and
+// conv_out); GroupNorm statistics are exact per group (two passes) and Chan-combined across the 8
+// groups in a fixed order (deterministic).  Every spin is bounded (timeout -> error word -> every
+// workgroup exits); the host then restores x and runs the launch path.
+#pragma once
+#include "common.hpp"
+
+namespace fl {
+namespace pk {
+
+constexpr int kGroups = 8, kSlots = 32, kWGs = kGroups * kSlots, kThreads = 256;
+constexpr int kH = 1024, kC = 256, kCols = kH / kSlots, kCh = kC / kSlots;
+constexpr int kMaxRows = 64, kHalo = 15, kTaps = 31, kWin = kMaxRows + 2 * kHalo;
+constexpr int kMaxNB = 8, kMaxT = kGroups * kMaxRows;
+// LDS carve (bytes): two weight panels, the dwconv window (aliased by the epilogue staging tile), row
+// statistics of the window, GroupNorm reduction scratch, poll flag
+constexpr int kWPanel = kCols * kH * 2;
+constexpr int L_HS = 2 * kWPanel;
+constexpr int L_ST = L_HS + kWin * kCols * 4;
+constexpr int L_RED = L_ST + kWin * 8;
+constexpr int L_GNV = L_RED + 8 * kCols * 4;
+constexpr int L_FLAG = L_GNV + kCols * 16;
+constexpr int kLds = (L_FLAG + 16 + 15) / 16 * 16;
+static_assert(kLds <= 160 * 1024, "persistent solve LDS");
+// counters (ints, one 64-B line each); zeroed before every launch
+constexpr int CT_GRP = 0, CT_GN = 16 * kGroups, CT_ERR = CT_GN + 16 * kSlots, kCtrInts = CT_ERR + 16;
+
+struct BlockW {
+  const bf16 *w2, *w3, *m0, *m2;
+  const float *b2, *b3, *mb0, *mb2, *lnw, *lnb, *lnmw, *lnmb, *dww, *dwb, *gnw, *gnb;
+};
+
+struct Params {
+  int T, NB, s0, s1;
+  float dt;
+  const float* mods;
+  int MS, MS0;
+  const bf16* win;
+  const float* bin;
+  BlockW blk[kMaxNB + 1];  // [NB] = FinalLayer (w2, w3, b2, b3, dww, dwb, gnw, gnb)
+  const bf16* wout;        // conv_out taps stacked (3 C) x H
+  const float* bout;
+  float* xt;               // Euler state (T x C), read at launch start, written at the end
+  float2* xpart[2];        // LayerNorm row partials (mean, M2) over each slot's 32 columns: T x 32; [0]
+                           // from proj_in / mlp.2 (read by the next dwconv phase of EVERY group: halo
+                           // rows), [1] from conv_3 (read by mlp.0 / conv_out of the same group) -- two
+                           // buffers, so a group's conv_3 never overwrites what a slower neighbour's
+                           // dwconv phase is still reading
+  float* ximg;             // X rows (fp32) near the group edges: dwconv halo of the neighbouring groups
+  bf16* a2;                // GroupNorm output = conv_2 operand, T x H
+  bf16* u;                 // conv_2 / mlp.0 output = conv_3 / mlp.2 operand, T x H
+  bf16* xa;                // x * alpha (LayerNorm fold) = mlp.0 / conv_out operand, T x H
+  bf16* xs;                // bf16(x) = proj_in operand, T x C
+  float4* gnp;             // GroupNorm partials (n, mean, M2) per (group, channel): 8 x H
+  float* yb;               // conv_out boundary rows per workgroup: Y0 of its last row, Y2 of its first
+  int* ctr;
+  long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
+};
+
+// Host side (persist.hip): whether this device runs the 256-workgroup grid fully resident, and the launch.
+bool persist_device_ok(int device);
+int persist_launch(const Params& P, hipStream_t st);
+
+}  // namespace pk
+}  // namespace fl

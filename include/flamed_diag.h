@@ -45,6 +45,10 @@ FLAMED_API int flamed_probe_mx_gemm(const float* A, const float* W, int M, int N
 /* libflamed_hip_stamps.so only: device buffer of blocks x 8 u64 into which the denoiser kernels of
  * class `flamed_tune("stamp_class", c)` write s_memtime at their phase boundaries (eager steps). */
 FLAMED_API int flamed_stamp_buffer(void* buf);
+/* Persistent solve timeline (libflamed_hip_stamps.so only): thread 0 of each of the 256 workgroups writes
+ * s_memrealtime at every wait / compute / signal point of Euler step `step` into buf[wg * 160 + k]
+ * (device memory, 256 x 160 uint64); buf = NULL turns it off.  tools/persist_timeline.py. */
+FLAMED_API int flamed_persist_stamps(void* buf, int step);
 
 #ifdef __cplusplus
 }

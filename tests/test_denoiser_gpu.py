@@ -136,6 +136,7 @@ def test_split_k_solve_bf16(target, mx, pg_bf16):
     with torch.inference_mode():
         base = hip.solve(x0.to(DEV), ts.to(DEV), spk.to(DEV), nfe).cpu()
         try:
+            nat.check(L.flamed_tune(b"persist", 0), "tune")  # the graph-of-launches path is under test
             nat.check(L.flamed_tune(b"splitk_target", target), "tune")
             nat.check(L.flamed_tune(b"splitk_max", mx), "tune")
             pg.denoiser.hip_graph = False
@@ -146,6 +147,7 @@ def test_split_k_solve_bf16(target, mx, pg_bf16):
         finally:
             nat.check(L.flamed_tune(b"splitk_target", 1), "tune")
             nat.check(L.flamed_tune(b"splitk_max", 4), "tune")
+            nat.check(L.flamed_tune(b"persist", 1), "tune")
     assert torch.equal(a, b) and torch.equal(b, c)  # deterministic reduction, graph == eager
     assert rel_l2(a, base) < 5e-3  # bf16 re-rounding of U after a different fp32 summation order
     ref = orc.euler_solve(sd, x0, spk, nfe)
@@ -324,6 +326,7 @@ def test_fused_euler_solve_bitwise(B, T, nfe, pg_bf16):
     ts = torch.linspace(0, 1, nfe + 1, device=DEV)
     L = nat.lib()
     outs = []
+    nat.check(L.flamed_tune(b"persist", 0), "tune")  # the graph-of-launches path is under test
     try:
         with torch.inference_mode():
             for fuse, graph in ((1, True), (0, True), (1, False)):
@@ -332,6 +335,7 @@ def test_fused_euler_solve_bitwise(B, T, nfe, pg_bf16):
                 outs.append(hip.solve(x0, ts, spk, nfe).cpu())
     finally:
         nat.check(L.flamed_tune(b"fuse_euler", 1), "tune")
+        nat.check(L.flamed_tune(b"persist", 1), "tune")
         pg.denoiser.hip_graph = True
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

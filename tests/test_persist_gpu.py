@@ -1,0 +1,133 @@
+"""GPU: the persistent B = 1 Euler solve (flamed-tts_amd/csrc/persist.hip) — every step of
+ProbGenerator.sample's ODE loop (reference prob_generator.py:434-447, SimpleMLPAdaLN.forward :349-365) in
+one launch of 256 workgroups with in-launch hand-offs.
+
+Checks: the solve really ran persistently (flamed_den_persist_info), against the fp32 oracle under the
+bf16 solve tolerance of the launch path (rel-L2 <= 6e-3 and max|d| < 0.05 at configs[1]), at edge lengths
+(T = 16: most groups empty; 40 / 131 / 257: partial tiles; 512: every group full), against the launch path
+(same bf16 operands, different fp32 reduction order: rel-L2 <= 4e-3), bitwise determinism, and parts
+[0, G) + [G, nfe) equal to the whole (the fp32 state passes through xt exactly).
+"""
+import contextlib
+import os
+
+import pytest
+import torch
+
+from _common import orc, rel_l2
+from test_denoiser_gpu import _prob_gen
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+C = 256
+BF16_SOLVE = 6e-3
+
+
+@contextlib.contextmanager
+def knob(key, value, default):
+    from flamed import _native as nat
+    L = nat.lib()
+    nat.check(L.flamed_tune(key.encode(), value), "flamed_tune")
+    try:
+        yield
+    finally:
+        nat.check(L.flamed_tune(key.encode(), default), "flamed_tune")
+
+
+@pytest.fixture(scope="module")
+def pgb():
+    return _prob_gen("bf16")
+
+
+def _inputs(seed, B, T, temp=0.3):
+    g = torch.Generator().manual_seed(seed)
+    cond = torch.randn(B, T, C, generator=g)
+    noise = torch.randn(B, T, C, generator=g)
+    spk = torch.randn(B, C, generator=g)
+    return noise * temp + cond, spk
+
+
+def _solve(pg, x0, spk, nfe):
+    hip = pg.denoiser.hip()
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        return hip.solve(x0.to(DEV), ts, spk.to(DEV), nfe).cpu()
+
+
+def _runs(pg):
+    runs, broken = pg.denoiser.hip().persist_info()
+    assert not broken, "a persistent solve timed out and was rolled back"
+    return runs
+
+
+def test_persist_cfg1_vs_oracle_and_launch_path(pgb):
+    pg, sd = pgb
+    x0, spk = _inputs(1, 1, 400)
+    r0 = _runs(pg) if pg.denoiser._hip is not None else 0
+    out = _solve(pg, x0, spk, 128)
+    assert _runs(pg) == r0 + 1, "the B = 1 solve did not take the persistent path"
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    ref = orc.euler_solve(sd, x0, spk, 128)
+    e = rel_l2(out, ref)
+    amax = float((out - ref).abs().max())
+    with knob("persist", 0, 1):
+        launch = _solve(pg, x0, spk, 128)
+    el = rel_l2(out, launch)
+    print(f"persistent configs[1] 128 steps: vs oracle rel-L2 {e:.3e} max|d| {amax:.3e}; vs launch path {el:.3e} "
+          f"(launch path vs oracle {rel_l2(launch, ref):.3e})")
+    assert torch.isfinite(out).all()
+    assert e < BF16_SOLVE and amax < 0.05
+    assert el < 4e-3
+
+
+@pytest.mark.parametrize("T", [16, 40, 131, 257, 512])
+def test_persist_lengths_vs_oracle(pgb, T):
+    pg, sd = pgb
+    x0, spk = _inputs(T, 1, T)
+    r0 = _runs(pg) if pg.denoiser._hip is not None else 0
+    out = _solve(pg, x0, spk, 8)
+    assert _runs(pg) == r0 + 1
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    ref = orc.euler_solve(sd, x0, spk, 8)
+    e = rel_l2(out, ref)
+    print(f"persistent T={T} 8 steps: vs oracle rel-L2 {e:.3e}")
+    assert e < BF16_SOLVE
+
+
+def test_persist_deterministic_and_parts(pgb):
+    from flamed import _native as nat
+    pg, _ = pgb
+    hip = pg.denoiser.hip()
+    L = nat.lib()
+    x0, spk = _inputs(5, 1, 300)
+    nfe = 32
+    a = _solve(pg, x0, spk, nfe)
+    b = _solve(pg, x0, spk, nfe)
+    assert torch.equal(a, b)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        G = L.flamed_den_solve_chunk(hip.handle, nfe)
+        r = torch.arange(nfe, device=DEV)
+        mods = hip.adaln(ts[:nfe], spk.to(DEV), r.to(torch.int32), torch.zeros(nfe, dtype=torch.int32, device=DEV))
+        x = x0.to(DEV).contiguous()
+        ws = nat.Workspace().get(L.flamed_den_workspace_size(hip.handle, 1, 300), DEV)
+        runs0 = _runs(pg)
+        for s0, s1 in ((0, G), (G, nfe)):
+            nat.check(L.flamed_den_solve_part(hip.handle, nat.ptr(x), nat.ptr(mods), nfe, 1, 300, nat.ptr(ws), ws.numel(),
+                                              1, s0, s1, nat.stream_ptr(DEV)), "flamed_den_solve_part")
+        torch.cuda.synchronize()
+    assert _runs(pg) == runs0 + 2
+    assert torch.equal(x.cpu(), a)
+
+
+def test_persist_knob_off_uses_launch_path(pgb):
+    pg, _ = pgb
+    x0, spk = _inputs(7, 1, 64)
+    _solve(pg, x0, spk, 4)
+    r0 = _runs(pg)
+    with knob("persist", 0, 1):
+        _solve(pg, x0, spk, 4)
+    assert _runs(pg) == r0
+    x2, spk2 = _inputs(8, 2, 64)  # B = 2: never persistent
+    _solve(pg, x2, spk2, 4)
+    assert _runs(pg) == r0
