@@ -76,6 +76,7 @@ def parse():
     ap.add_argument("--noctr", type=int, default=None, help="diagnostic: ignore the device step counter")
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
     ap.add_argument("--persist", type=int, default=None, help="flamed_tune persist (B = 1: one persistent launch per solve)")
+    ap.add_argument("--persist-opt", type=int, default=None, help="flamed_tune persist_opt (persistent kernel experiment bits)")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU rehearsal of the launcher/timing harness over gloo (no GPU; tests/test_bench_cpu.py)")
@@ -535,7 +536,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler", "persist"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler", "persist", "persist_opt"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")
@@ -568,11 +569,16 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
+        runs0 = hip.persist_info()[0] if args.dtype == "bf16" else 0
         t0 = time.perf_counter()
+        pms = []  # device time of each persistent launch (HIP events around the kernel, launch stream)
         for _ in range(args.steps):
             out = step()
+            if args.dtype == "bf16":
+                pms.append(hip.persist_info(with_ms=True)[2])
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        persist_runs = (hip.persist_info()[0] - runs0) if args.dtype == "bf16" else 0
         if dist:
             dist.barrier()
         sec = (t1 - t0) / args.steps
@@ -637,13 +643,40 @@ def main():
                     "achieved_GBps": round(sbytes / step_s / 1e9, 1),
                     "frac": round(sbytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
                     "bytes_model": "W (bf16 GEMM weights + fp32 vectors/taps) + 54,272 B per frame"}
+    if persist_runs >= args.steps and pms:
+        # B = 1 solves ran as ONE persistent launch each (persist.hip): that kernel is the dominant (only)
+        # kernel of the timed region.  Algorithmic bytes per launch = nfe x the canonical step bytes;
+        # duration = HIP events around the launch on its stream (median over the timed solves).
+        pk_ms = sorted(pms)[len(pms) // 2]
+        lbytes = sbytes * nfe
+        lflops = nfe * (2 * 20081664 * B * T)  # 40.16 MFLOP per frame-step
+        ach = lbytes / (pk_ms * 1e-3) / 1e9
+        ptraffic = None
+        if os.path.exists(tpath):
+            tj = json.load(open(tpath))
+            if (tj.get("batch"), tj.get("frames"), tj.get("dtype"), tj.get("nfe", nfe)) == (B, T, args.dtype, nfe):
+                ptraffic = tj.get("bytes_per_launch", {}).get("den_persist_kernel")
+        launch_path = dict(roof)
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "den_persist_kernel", "launch_us": round(pk_ms * 1e3, 1),
+                "launches_per_solve": 1, "traffic": ptraffic,
+                "traffic_source": "rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, profiles/latest_traffic.json"
+                if ptraffic is not None else None,
+                "algorithmic_bytes": lbytes, "algorithmic_flops": lflops, "tflops": round(lflops / (pk_ms * 1e-3) / 1e12, 2),
+                "step": {"bytes_canonical": sbytes, "step_us": round(pk_ms * 1e3 / nfe, 2),
+                         "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "bytes_model": "W (bf16 GEMM weights + fp32 vectors/taps) + 54,272 B per frame"},
+                "launch_path": launch_path}
+        sbytes_step_s = pk_ms * 1e-3 / nfe
+    else:
+        sbytes_step_s = step_s
     peaks = None
     if rank == 0 and world == 1 and not args.no_peaks:
         try:
             peaks = measured_peaks(dev)
             roof["peak_measured"] = peaks["hbm_stream_copy_GBps"] if roof["unit"] == "GB/s" else peaks["bf16_gemm_TFs"]
             roof["frac_of_measured"] = round(roof["achieved"] / roof["peak_measured"], 4)
-            roof["step"]["frac_of_measured"] = round(sbytes / step_s / 1e9 / peaks["hbm_stream_copy_GBps"], 4)
+            roof["step"]["frac_of_measured"] = round(sbytes / sbytes_step_s / 1e9 / peaks["hbm_stream_copy_GBps"], 4)
         except Exception as e:  # reported, never fatal
             peaks = {"error": f"{type(e).__name__}: {e}"}
 
@@ -702,7 +735,10 @@ def main():
         "rtf_denoiser": round(sec / audio_s, 6),
         "roofline": roof,
         "kernels": [{k: v for k, v in kk.items() if k not in ("bytes", "flops")} for kk in kernels],
-        "kernel_timing": "in-graph per-launch cost (4-step graph with the class doubled minus as captured, HIP events)",
+        "kernel_timing": "graph-of-launches path (B > 1, and the B = 1 fallback): in-graph per-launch cost "
+                         "(4-step graph with the class doubled minus as captured, HIP events)",
+        "persistent": {"runs": persist_runs, "solves": args.steps,
+                       "launch_ms": [round(x, 3) for x in pms] if persist_runs else None},
         "step_us_graph": round(ms[N_CLASSES] * 1e3, 2),
         "cpu_baseline": cpu,
         "peaks": {"hbm_spec_GBps": HBM_PEAK_GBS, "bf16_dense_spec_TFs": MFMA_PEAK_TFS["bf16"], **(peaks or {})},

@@ -1573,6 +1573,8 @@ struct Den {
   int pdev_ok = -1;          // 1: 256 CUs and one 256-thread workgroup per CU fits; 0: not on this device
   bool pbroken = false;      // a persistent solve timed out on this handle: launch path from then on
   int pruns = 0;             // persistent launches completed
+  float plast_ms = 0.f;      // device time of the last one (HIP events around the kernel)
+  hipEvent_t pev[2] = {nullptr, nullptr};
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1710,6 +1712,8 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
     if (d->gcnt) (void)hipFree(d->gcnt);
     if (d->pmem) (void)hipFree(d->pmem);
     if (d->perr_host) (void)hipHostFree(d->perr_host);
+    for (hipEvent_t e : d->pev)
+      if (e) (void)hipEventDestroy(e);
     if (d->dev) (void)hipFree(d->dev);
   }
   delete d;
@@ -1757,6 +1761,8 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     if (d->scnt) { (void)hipFree(d->scnt); d->scnt = nullptr; }
     if (d->gcnt) { (void)hipFree(d->gcnt); d->gcnt = nullptr; }
     if (d->pmem) { (void)hipFree(d->pmem); d->pmem = nullptr; }
+    for (hipEvent_t& e : d->pev)
+      if (e) { (void)hipEventDestroy(e); e = nullptr; }
     if (d->dev) { (void)hipFree(d->dev); d->dev = nullptr; }
     d->pdev_ok = -1;
   }
@@ -2208,11 +2214,16 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, i
   P.wout = reinterpret_cast<const bf16*>(d->wout); P.bout = d->bout;
   P.xt = xt;
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
+  P.opt = tn().persist_opt;
   const size_t xbytes = (size_t)T * pk::kC * 4;
   FL_HIP(hipMemcpyAsync(backup, xt, xbytes, hipMemcpyDeviceToDevice, st));
   FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pk::kCtrInts, st));
+  if (!d->pev[0]) FL_HIP(hipEventCreate(&d->pev[0]));
+  if (!d->pev[1]) FL_HIP(hipEventCreate(&d->pev[1]));
+  FL_HIP(hipEventRecord(d->pev[0], st));
   const int lrc = pk::persist_launch(P, st);
   if (lrc) return lrc;
+  FL_HIP(hipEventRecord(d->pev[1], st));
   FL_HIP(hipMemcpyAsync(d->perr_host, P.ctr + pk::CT_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
   FL_HIP(hipStreamSynchronize(st));
   if (*d->perr_host != 0) {  // a wait timed out: every workgroup left; x is rolled back
@@ -2223,6 +2234,7 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, i
   }
   *done = true;
   ++d->pruns;
+  FL_HIP(hipEventElapsedTime(&d->plast_ms, d->pev[0], d->pev[1]));
   return kOk;
 }
 
@@ -2272,12 +2284,13 @@ FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe) {
   return graph_chunk(nfe);
 }
 
-FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken) {
+FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, float* last_ms) {
   Den* d = reinterpret_cast<Den*>(h);
-  FL_REQUIRE(d && runs && broken, "flamed_den_persist_info: bad args");
+  FL_REQUIRE(d && runs && broken && last_ms, "flamed_den_persist_info: bad args");
   std::lock_guard<std::recursive_mutex> lk(d->mu);
   *runs = d->pruns;
   *broken = d->pbroken ? 1 : 0;
+  *last_ms = d->plast_ms;
   return kOk;
 }
 

@@ -1,4 +1,7 @@
 // Persistent B = 1 Euler solve kernel (design notes: persist.hpp).
+#include <cstdio>
+#include <cstdlib>
+
 #include "flamed_hip.h"
 #include "persist.hpp"
 #include "gemm_dma.hpp"
@@ -10,17 +13,19 @@ namespace pk {
 // s_memrealtime (100 MHz, chip-wide) at each wait / compute / signal point of one chosen step into
 // g_pst[workgroup][k] (flamed_persist_stamps; tools/persist_timeline.py).
 #ifdef FL_STAMPS
-__device__ unsigned long long* g_pst = nullptr;
-__device__ int g_pst_step = -1;
 constexpr int kStampSlots = 160;
 #define PST(step)                                                                                       \
   do {                                                                                                  \
-    if ((step) == g_pst_step && g_pst && threadIdx.x == 0 && pst_k < kStampSlots)                       \
-      g_pst[blockIdx.x * kStampSlots + pst_k] = __builtin_amdgcn_s_memrealtime();                      \
+    if ((step) == P.pst_step && P.pst && threadIdx.x == 0 && pst_k < kStampSlots)                       \
+      P.pst[blockIdx.x * kStampSlots + pst_k] = __builtin_amdgcn_s_memrealtime();                      \
     ++pst_k;                                                                                            \
   } while (0)
+// the address of the next stamp slot (or null), for a stamp taken inside a helper
+#define PSTP(step) \
+  (((step) == P.pst_step && P.pst && pst_k < kStampSlots) ? P.pst + blockIdx.x * kStampSlots + pst_k++ : (++pst_k, nullptr))
 #else
 #define PST(step) ((void)0)
+#define PSTP(step) nullptr
 #endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
@@ -29,6 +34,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned b
 // write-through (sc1) 16-B store / sc1 16-B load (aux 16 = sc1)
 __device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+// plain 16-B store: the line stays in this XCD's L2 (group-local hand-offs when groups are XCDs)
+__device__ __forceinline__ void st16p(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
@@ -42,12 +51,21 @@ __device__ __forceinline__ int opq(int v) {
   return v;
 }
 
-// Row range of group g: whole 16-row tiles [g MT / 8, (g + 1) MT / 8).
-__device__ __forceinline__ void group_rows(int g, int T, int& r0, int& nr) {
-  const int MT = (T + 15) >> 4;
-  const int tb = g * MT / kGroups, te = (g + 1) * MT / kGroups;
-  r0 = 16 * tb;
-  nr = max(min(16 * te, T) - r0, 0);
+// Row range of group g: ceil(T / 8) consecutive frames (the last groups may be short or empty).  Equal
+// shares, not whole 16-row tiles: every group's GEMM operand then moves the same bytes (T = 400: 50 rows
+// each, instead of one 64-row group pacing seven 48-row ones); rows past nr in a wave's last 16-row
+// fragment read as zero through the buffer range and are never stored.
+__device__ __forceinline__ void group_rows(int g, int T, int& r0, int& nr, int opt) {
+  if (opt & 2) {  // whole 16-row tiles [g MT / 8, (g + 1) MT / 8)
+    const int MT = (T + 15) >> 4;
+    const int tb = g * MT / kGroups, te = (g + 1) * MT / kGroups;
+    r0 = 16 * tb;
+    nr = max(min(16 * te, T) - r0, 0);
+    return;
+  }
+  const int R = (T + kGroups - 1) / kGroups;
+  r0 = g * R;
+  nr = max(min(R, T - r0), 0);
 }
 
 // ---- hand-off primitives ----
@@ -96,12 +114,14 @@ template <int K>
 __device__ __forceinline__ int woff(int n, int j) { return n * (2 * K) + ((j ^ (n & 15)) << 4); }
 
 template <int K, class RowF>
-__device__ __forceinline__ void dma_panel(char* dst, RowF rowp, int wave, int lane_in) {
-  constexpr int kRowB = 2 * K, kNI = 32 * kRowB / 1024, kPer = kNI / 4;
+// Issued by waves 1..3 only: wave 0 goes straight to polling the next hand-off (issuing 64 LDS-DMA
+// wave-instructions takes ~1 us of a wave's time), and its vmcnt never waits for weight traffic.
+__device__ __forceinline__ void dma_panel(char* dst, RowF rowp, int wave, int lane_in, int opt) {
+  constexpr int kRowB = 2 * K, kNI = 32 * kRowB / 1024;
   const int lane = opq(lane_in);
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = wave * kPer + k;
+  const bool w4 = opt & 1;  // all four waves issue
+  if (wave == 0 && !w4) return;
+  for (int i = w4 ? wave : wave - 1; i < kNI; i += w4 ? 4 : 3) {
     const int pos = i * 1024 + lane * 16;
     const int n = pos / kRowB, jl = (pos % kRowB) >> 4;
     glds16(reinterpret_cast<const char*>(rowp(n)) + ((jl ^ (n & 15)) << 4), dst + i * 1024);
@@ -112,7 +132,8 @@ __device__ __forceinline__ void dma_panel(char* dst, RowF rowp, int wave, int la
 // columns: A (bf16 rows, K) straight to registers with sc1 loads (rows >= nr read as 0: buffer range),
 // B fragments from the LDS weight panel.
 template <int K>
-__device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[2], int wave, int lane_in) {
+__device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[2], int wave, int lane_in,
+                                     unsigned long long* stamp = nullptr) {
   constexpr int KST = K / 32;
   const int lane = opq(lane_in);
   acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -130,20 +151,34 @@ __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();  // every wave's DMA: the whole panel is in LDS
+  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // FL_STAMPS timeline only
   if (wave < ntile) {
+    // B fragments read kBP K-steps ahead of the MFMAs that consume them (a ring of registers), so the
+    // LDS latency overlaps the matrix pipe instead of one lgkmcnt(0) per MFMA
+    constexpr int kBP = 4;
+    u32x4 b0[kBP], b1[kBP];
+#pragma unroll
+    for (int p = 0; p < kBP; ++p) {
+      b0[p] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * p + q));
+      b1[p] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * p + q));
+    }
 #pragma unroll
     for (int ks = 0; ks < KST; ++ks) {
-      const u32x4 b0 = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * ks + q));
-      const u32x4 b1 = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * ks + q));
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, b0), acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, b1), acc[1], 0, 0, 0);
+      const u32x4 x0 = b0[ks % kBP], x1 = b1[ks % kBP];
+      if (ks + kBP < KST) {
+        b0[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (ks + kBP) + q));
+        b1[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (ks + kBP) + q));
+      }
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, x0), acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, x1), acc[1], 0, 0, 0);
     }
   }
 }
 
 // LayerNorm partials (mean, M2 over the slot's 32 columns) of the wave's 16 rows, from the MFMA layout
 // (lane c, q holds rows 4q + i, columns c and 16 + c): write-through 8-B stores.
-__device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int wave, int lane_in) {
+__device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int wave, int lane_in,
+                                               bool local = false) {
   const int lane = opq(lane_in);
   const int c = lane & 15, q = lane >> 4;
 #pragma unroll
@@ -155,8 +190,11 @@ __device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2
     const int row = 16 * wave + 4 * q + i;
     if (c == 0 && row < nr) {
       const float2 v = make_float2(mean, m2);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(xpart + (size_t)(r0 + row) * kSlots + s),
-                         __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (local)
+        xpart[(size_t)(r0 + row) * kSlots + s] = v;
+      else
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(xpart + (size_t)(r0 + row) * kSlots + s),
+                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -209,14 +247,17 @@ __device__ __forceinline__ void stage_tile(char* stg, const float (&v)[2][4], in
 }
 // ... then write it through with 16-B sc1 stores (rows [ra, rb) of the tile) into dst (row stride ld).
 template <typename OT>
-__device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int r0, int ra, int rb, int col0, int T) {
+__device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int r0, int ra, int rb, int col0, int T,
+                                           bool local = false) {
   constexpr int CPR = kCols * (int)sizeof(OT) / 16;  // 16-B chunks per staged row
   const __amdgpu_buffer_rsrc_t rs = rsrc(dst, (unsigned)T * ld * (unsigned)sizeof(OT));
   for (int idx = opq(threadIdx.x); idx < kMaxRows * CPR; idx += kThreads) {
     const int row = idx / CPR, ch = idx % CPR;
     if (row < ra || row >= rb) continue;
     const u32x4 v = *reinterpret_cast<const u32x4*>(stg + (row * kCols * sizeof(OT)) + ch * 16);
-    st16(rs, (unsigned)(((size_t)(r0 + row) * ld + col0) * sizeof(OT) + ch * 16), v);
+    const unsigned off = (unsigned)(((size_t)(r0 + row) * ld + col0) * sizeof(OT) + ch * 16);
+    if (local) st16p(rs, off, v);
+    else st16(rs, off, v);
   }
 }
 
@@ -231,10 +272,34 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = blockIdx.x % kGroups, s = blockIdx.x / kGroups;
-  const int T = P.T, H = kH;
+  const int T = P.T;
+  const int H = kH;
+  // Group / slot.  opt & 4: group = this workgroup's XCD (hardware register), slot = its arrival ticket
+  // on that XCD, so a group's hand-offs stay in one L2: group-local payloads are stored plainly (the
+  // line stays in the XCD's L2) and read with sc1 loads (L1 bypass, L2 hit); cross-group payloads stay
+  // write-through.  More than 32 workgroups on one XCD (not all 256 resident) aborts the solve.
+  // Otherwise group = blockIdx % 8 (the round-robin dispatch puts it on one XCD: speed only).
+  const bool xloc = (P.opt & 4) != 0;
+  int g = blockIdx.x % kGroups, s = blockIdx.x / kGroups;
+  if (xloc) {
+    int* tk = reinterpret_cast<int*>(smem + L_FLAG);
+    if (threadIdx.x == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      xcc &= kGroups - 1;
+      const int slot = __hip_atomic_fetch_add(P.ctr + CT_SLOT + 16 * xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tk[0] = (int)xcc;
+      tk[1] = slot;
+      if (slot >= kSlots) __hip_atomic_store(P.ctr + CT_ERR, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    g = tk[0];
+    s = tk[1];
+    __syncthreads();
+    if (s >= kSlots) return;
+  }
   int r0, nr;
-  group_rows(g, T, r0, nr);
+  group_rows(g, T, r0, nr, P.opt);
   const int c = lane & 15, q = lane >> 4;
   const int col0 = kCols * s;
   char* stg = smem + L_HS;  // epilogue staging (aliases the dwconv window)
@@ -258,11 +323,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   // after a GEMM phase: the next GEMM's panel goes into the buffer the finished one did not use
   auto next_w = [&](const bf16* W) {
     wb ^= 1;
-    dma_panel<kH>((smem + wb * kWPanel), [&](int n) { return W + (size_t)(col0 + n) * kH; }, wave, lane);
+    dma_panel<kH>((smem + wb * kWPanel), [&](int n) { return W + (size_t)(col0 + n) * kH; }, wave, lane, P.opt);
   };
   auto next_win = [&]() {
     wb ^= 1;
-    dma_panel<kC>((smem + wb * kWPanel), [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane);
+    dma_panel<kC>((smem + wb * kWPanel), [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane, P.opt);
   };
 
   // Euler state: thread -> tile row xr_row, channels 8 s + 2 (tid & 3) + {0, 1}
@@ -273,7 +338,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     xs1 = P.xt[(size_t)(r0 + xr_row) * kC + xch + 1];
   }
   // weights of the first GEMM (proj_in) while the state is published
-  dma_panel<kC>(smem, [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane);
+  dma_panel<kC>(smem, [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane, P.opt);
   // bf16 rows of x (proj_in's operand): 16 B per tile row, staged in LDS
   auto publish_xs = [&]() {
     bf16* t = reinterpret_cast<bf16*>(stg);
@@ -282,7 +347,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     __syncthreads();
     if (tid < nr) {
       const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)T * kC * 2);
-      st16(rs, (unsigned)(((size_t)(r0 + tid) * kC + kCh * s) * 2), *reinterpret_cast<const u32x4*>(stg + tid * 16));
+      const unsigned off = (unsigned)(((size_t)(r0 + tid) * kC + kCh * s) * 2);
+      if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
+      else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
     }
     signal(mygrp);
     ++L;
@@ -294,19 +361,21 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
   for (int step = P.s0; step < P.s1; ++step) {
     const float* md = P.mods + (size_t)step * P.MS;
+#ifdef FL_STAMPS
+    pst_k = 0;
+#endif
     // ------------------------------ proj_in (:361) ------------------------------
+    const float binv[2] = {P.bin[col0 + c], P.bin[col0 + 16 + c]};
     PST(step);
     if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
     PST(step);
-    gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+    gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
     PST(step);
     acc_to(X, acc);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const float b = P.bin[col0 + 16 * nt + c];
+    for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) X[nt][i] += b;
-    }
+      for (int i = 0; i < 4; ++i) X[nt][i] += binv[nt];
     if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
     stage_tile<float>(stg, X, wave, lane);
     __syncthreads();
@@ -332,62 +401,70 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (!wait_ge(errw, tmo, grp, 16, kGroups, 32 * L, flag)) return;  // every group: the halo rows of the neighbours
       PST(step);
       const int wa = max(r0 - kHalo, 0), wz = min(r0 + nr + kHalo, T);
+      const int cc = tid & 31, rg = tid >> 5;
+      // Everything this phase reads that does not wait on another phase goes out first, so the loads'
+      // latencies overlap: the thread's 3 window items (its 4 columns col0 + 4 (tid & 7) are the same in
+      // every item), their modulation vectors, the depthwise taps of channel cc, the row statistics.
+      constexpr int kItems = (kWin * 8 + kThreads - 1) / kThreads;
+      float4 hv[kItems];
+      {
+        const __amdgpu_buffer_rsrc_t rx = rsrc(P.ximg, (unsigned)T * H * 4);
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          const int idx = tid + k * kThreads, p = idx >> 3, r = r0 - kHalo + p;
+          const bool halo = idx < kWin * 8 && (p < kHalo || p >= kHalo + nr) && r >= 0 && r < T;
+          hv[k] = halo ? as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * (tid & 7)) * 4))) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      float hva[4], hvb[4], ova[2], ovb[2];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vab(col0 + 4 * (tid & 7) + e, hva[e], hvb[e]);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) vab(col0 + 16 * nt + c, ova[nt], ovb[nt]);
+      float w[kTaps];
+#pragma unroll
+      for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col0 + cc];
+      const float dbias = bw.dwb[col0 + cc];
       row_stats(P.xpart[0], T, wa, wz, r0 - kHalo, st);
       __syncthreads();
       // window h[p] (frame r0 - 15 + p): own rows from X (registers), halo rows from ximg, 0 outside [0, T)
-      {
-        const __amdgpu_buffer_rsrc_t rx = rsrc(P.ximg, (unsigned)T * H * 4);
-        for (int idx = tid; idx < kWin * 8; idx += kThreads) {
-          const int p = idx >> 3, ch = idx & 7, r = r0 - kHalo + p;
-          if (p >= kHalo && p < kHalo + nr) continue;  // own rows: below
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const int idx = tid + k * kThreads, p = idx >> 3, r = r0 - kHalo + p;
+        if (idx < kWin * 8 && (p < kHalo || p >= kHalo + nr)) {
           float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
           if (r >= 0 && r < T) {
-            const float4 xv = as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * ch) * 4)));
             const float mean = st[2 * p], rstd = st[2 * p + 1];
-            float va, vb;
-            vab(col0 + 4 * ch, va, vb);
-            o.x = ((xv.x - mean) * rstd) * va + vb;
-            vab(col0 + 4 * ch + 1, va, vb);
-            o.y = ((xv.y - mean) * rstd) * va + vb;
-            vab(col0 + 4 * ch + 2, va, vb);
-            o.z = ((xv.z - mean) * rstd) * va + vb;
-            vab(col0 + 4 * ch + 3, va, vb);
-            o.w = ((xv.w - mean) * rstd) * va + vb;
+            o.x = ((hv[k].x - mean) * rstd) * hva[0] + hvb[0];
+            o.y = ((hv[k].y - mean) * rstd) * hva[1] + hvb[1];
+            o.z = ((hv[k].z - mean) * rstd) * hva[2] + hvb[2];
+            o.w = ((hv[k].w - mean) * rstd) * hva[3] + hvb[3];
           }
-          *reinterpret_cast<float4*>(hs + p * kCols + 4 * ch) = o;
+          *reinterpret_cast<float4*>(hs + p * kCols + 4 * (tid & 7)) = o;
         }
-        if (wbase < nr) {
+      }
+      if (wbase < nr) {
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            float va, vb;
-            vab(col0 + 16 * nt + c, va, vb);
+        for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int row = wbase + 4 * q + i;
-              if (row < nr) {
-                const int p = row + kHalo;
-                hs[p * kCols + 16 * nt + c] = ((X[nt][i] - st[2 * p]) * st[2 * p + 1]) * va + vb;
-              }
+          for (int i = 0; i < 4; ++i) {
+            const int row = wbase + 4 * q + i;
+            if (row < nr) {
+              const int p = row + kHalo;
+              hs[p * kCols + 16 * nt + c] = ((X[nt][i] - st[2 * p]) * st[2 * p + 1]) * ova[nt] + ovb[nt];
             }
           }
-        }
       }
       __syncthreads();
       // depthwise conv (zero padding at the utterance edges): thread -> channel cc, tile rows 8 rg .. 8 rg + 7
-      const int cc = tid & 31, rg = tid >> 5;
       float d[8];
       {
-        const int col = col0 + cc;
-        float w[kTaps];
-#pragma unroll
-        for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col];
-        const float bias = bw.dwb[col];
         float win[8 + kTaps - 1];
 #pragma unroll
         for (int j = 0; j < 8 + kTaps - 1; ++j) win[j] = hs[(8 * rg + j) * kCols + cc];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          float a = bias;
+          float a = dbias;
 #pragma unroll
           for (int j = 0; j < kTaps; ++j) a = fmaf(w[j], win[k + j], a);
           d[k] = a;
@@ -427,6 +504,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       signal(gnc);
       PST(step);
       ++ndg;
+      float gwv = 0.f, gbv = 0.f;
+      if (tid < kCols) {
+        gwv = bw.gnw[col0 + tid];
+        gbv = bw.gnb[col0 + tid];
+      }
       PST(step);
       if (!wait_ge(errw, tmo, gnc, 0, 1, kGroups * ndg, flag)) return;
       PST(step);
@@ -438,8 +520,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           const float4 v = as_f4(ld16(rq, (unsigned)((k * H + col0 + tid) * 16)));
           chan_combine(n, mean, m2, v.x, v.y, v.z);
         }
-        const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * bw.gnw[col0 + tid];
-        gnv[tid] = make_float4(mean, sc, bw.gnb[col0 + tid], 0.f);
+        const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
+        gnv[tid] = make_float4(mean, sc, gbv, 0.f);
       }
       __syncthreads();
       {
@@ -449,64 +531,67 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         for (int k = 0; k < 8; ++k) t[(8 * rg + k) * kCols + cc] = (bf16)((d[k] - gv.x) * gv.y + gv.z);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T);
+      flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
 
       // -------- conv_2 (1x1) + GELU (:90-91)
+      const float b2v[2] = {bw.b2[col0 + c], bw.b2[col0 + 16 + c]};  // epilogue vectors before the wait
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
-      gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+      gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
       PST(step);
       {
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const float b = bw.b2[col0 + 16 * nt + c];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b);
+          for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b2v[nt]);
         }
         stage_tile<bf16>(stg, v, wave, lane);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T);
+      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
       next_w(bw.w3);
 
       // -------- conv_3 (1x1) + ConvNeXt residual + gated residual (:92-93, 109, 156); x * alpha for the fold
+      float g3[2], b3v[2], alv[2];  // (ova / ovb of the dwconv phase are this epilogue's LN vectors)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = col0 + 16 * nt + c;
+        g3[nt] = mb[2 * H + col];
+        b3v[nt] = bw.b3[col];
+        // alpha = w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second)
+        alv[nt] = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
+      }
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
-      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
       PST(step);
       {
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const int col = col0 + 16 * nt + c;
-          float va, vb;
-          vab(col, va, vb);
-          const float gate = mb[2 * H + col], b3 = bw.b3[col];
-          // alpha = w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second)
-          const float al = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int p = wbase + 4 * q + i + kHalo;
             const float xh = (X[nt][i] - st[2 * p]) * st[2 * p + 1];
-            const float h = xh * va + vb;
-            X[nt][i] = X[nt][i] + gate * (h + (acc[nt][i] + b3));
-            v[nt][i] = X[nt][i] * al;
+            const float h = xh * ova[nt] + ovb[nt];
+            X[nt][i] = X[nt][i] + g3[nt] * (h + (acc[nt][i] + b3v[nt]));
+            v[nt][i] = X[nt][i] * alv[nt];
           }
         }
-        if (wbase < nr) store_partials(P.xpart[1], X, r0, nr, s, wave, lane);
+        if (wbase < nr) store_partials(P.xpart[1], X, r0, nr, s, wave, lane, xloc);
         stage_tile<bf16>(stg, v, wave, lane);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T);
+      flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
@@ -514,47 +599,44 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       next_w(bw.m0);
 
       // -------- mlp.0 + SiLU, the LayerNorm folded into the epilogue (:157-158)
+      const float* fo0 = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
+      const float fa0[2] = {fo0[col0 + c], fo0[col0 + 16 + c]}, fb0[2] = {fo0[H + col0 + c], fo0[H + col0 + 16 + c]};
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
       row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
-      gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane);  // (its barrier orders the statistics)
+      gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));  // (its barrier orders the statistics)
       PST(step);
       {
-        const float* fo = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-          const int col = col0 + 16 * nt + c;
-          const float fa = fo[col], fb = fo[H + col];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int p = wbase + 4 * q + i + kHalo;
-            v[nt][i] = silu(st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa) + fb);
+            v[nt][i] = silu(st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa0[nt]) + fb0[nt]);
           }
         }
         stage_tile<bf16>(stg, v, wave, lane);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T);
+      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
       next_w(bw.m2);
 
       // -------- mlp.2 + gated residual (:159-160)
+      const float g2v[2] = {mb[5 * H + col0 + c], mb[5 * H + col0 + 16 + c]}, bm2[2] = {bw.mb2[col0 + c], bw.mb2[col0 + 16 + c]};
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
-      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
+      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
       PST(step);
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = col0 + 16 * nt + c;
-        const float gate = mb[5 * H + col], b = bw.mb2[col];
+      for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) X[nt][i] = X[nt][i] + gate * (acc[nt][i] + b);
-      }
+        for (int i = 0; i < 4; ++i) X[nt][i] = X[nt][i] + g2v[nt] * (acc[nt][i] + bm2[nt]);
       if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
       stage_tile<float>(stg, X, wave, lane);
       __syncthreads();
@@ -571,27 +653,33 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     dma_panel<kH>((smem + wb * kWPanel), [&](int n) {
       const int m = n < 24 ? n : n - 24;
       return P.wout + (size_t)((m >> 3) * kC + kCh * s + (m & 7)) * kH;
-    }, wave, lane);
-    PST(step);
-    if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
-    PST(step);
-    row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
-    gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane);
-    PST(step);
-    float* yl = reinterpret_cast<float*>(stg);  // Y of the tile: [row][24] fp32 (tap-major x 8 channels)
+    }, wave, lane, P.opt);
+    float fac[2], fbc[2];  // fold vectors of the lane's stacked columns, before the wait
     {
       const float* fo = md + P.MS0 + (size_t)P.NB * 2 * H;  // [wa (3 C), wb (3 C)]
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const int n = 16 * nt + c;
-        if (n < 24) {
-          const int ns = (n >> 3) * kC + kCh * s + (n & 7);  // stacked output column
-          const float fa = fo[ns], fb = fo[3 * kC + ns];
+        const int n = 16 * nt + c, m = n < 24 ? n : n - 24;
+        const int ns = (m >> 3) * kC + kCh * s + (m & 7);  // stacked output column
+        fac[nt] = fo[ns];
+        fbc[nt] = fo[3 * kC + ns];
+      }
+    }
+    PST(step);
+    if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+    PST(step);
+    row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
+    gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
+    PST(step);
+    float* yl = reinterpret_cast<float*>(stg);  // Y of the tile: [row][24] fp32 (tap-major x 8 channels)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = wbase + 4 * q + i, p = row + kHalo;
-            yl[row * 24 + n] = st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa) + fb;
-          }
+    for (int nt = 0; nt < 2; ++nt) {
+      const int n = 16 * nt + c;
+      if (n < 24) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wbase + 4 * q + i, p = row + kHalo;
+          yl[row * 24 + n] = st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fac[nt]) + fbc[nt];
         }
       }
     }
@@ -601,7 +689,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const __amdgpu_buffer_rsrc_t ry = rsrc(P.yb, kWGs * 16 * 4);
       const int half = tid >> 1, k = tid & 1;
       const float* src = half == 0 ? yl + (nr - 1) * 24 + 4 * k : yl + 16 + 4 * k;
-      st16(ry, (unsigned)((blockIdx.x * 16 + half * 8 + 4 * k) * 4), __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(src)));
+      st16(ry, (unsigned)(((g + kGroups * s) * 16 + half * 8 + 4 * k) * 4), __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(src)));
     }
     signal(mygrp);
     PST(step);
@@ -617,7 +705,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       int gp = 0, gn_ = 0;  // the groups owning frames r0 - 1 and r0 + nr (nearest non-empty neighbours)
       for (int k = 0; k < kGroups; ++k) {
         int a, b;
-        group_rows(k, T, a, b);
+        group_rows(k, T, a, b, P.opt);
         if (b > 0 && a + b == r0) gp = k;
         if (b > 0 && a == r0 + nr) gn_ = k;
       }
@@ -654,10 +742,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 }
 
 #ifdef FL_STAMPS
+static unsigned long long* g_pst_buf = nullptr;
+static int g_pst_step = -1;
 int persist_stamps(void* buf, int step) {
-  unsigned long long* p = reinterpret_cast<unsigned long long*>(buf);
-  FL_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pst), &p, sizeof(p)));
-  FL_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pst_step), &step, sizeof(step)));
+  g_pst_buf = reinterpret_cast<unsigned long long*>(buf);
+  g_pst_step = step;
   return kOk;
 }
 #endif
@@ -670,7 +759,12 @@ bool persist_device_ok(int device) {
   return nb >= 1;
 }
 
-int persist_launch(const Params& P, hipStream_t st) {
+int persist_launch(const Params& Pin, hipStream_t st) {
+  Params P = Pin;
+#ifdef FL_STAMPS
+  P.pst = g_pst_buf;
+  P.pst_step = g_pst_step;
+#endif
   hipLaunchKernelGGL(den_persist_kernel, dim3(kWGs), dim3(kThreads), kLds, st, P);
   FL_LAUNCH_CHECK();
   return kOk;

@@ -44,7 +44,8 @@ constexpr int L_FLAG = L_GNV + kCols * 16;
 constexpr int kLds = (L_FLAG + 16 + 15) / 16 * 16;
 static_assert(kLds <= 160 * 1024, "persistent solve LDS");
 // counters (ints, one 64-B line each); zeroed before every launch
-constexpr int CT_GRP = 0, CT_GN = 16 * kGroups, CT_ERR = CT_GN + 16 * kSlots, kCtrInts = CT_ERR + 16;
+constexpr int CT_GRP = 0, CT_GN = 16 * kGroups, CT_ERR = CT_GN + 16 * kSlots, CT_SLOT = CT_ERR + 16,
+              kCtrInts = CT_SLOT + 16 * kGroups;
 
 struct BlockW {
   const bf16 *w2, *w3, *m0, *m2;
@@ -76,6 +77,9 @@ struct Params {
   float* yb;               // conv_out boundary rows per workgroup: Y0 of its last row, Y2 of its first
   int* ctr;
   long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
+  int opt = 0;                        // experiment bits (flamed_tune persist_opt)
+  unsigned long long* pst = nullptr;  // FL_STAMPS builds: timeline of step pst_step (persist_timeline.py)
+  int pst_step = -1;
 };
 
 // Host side (persist.hip): whether this device runs the 256-workgroup grid fully resident, and the launch.

@@ -36,7 +36,7 @@ SIGNATURES = {
     "flamed_den_step": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, c_size_t, P]),
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_den_solve_chunk": (c_int, [P, c_int]),
-    "flamed_den_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "flamed_den_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_float)]),
     "flamed_den_solve_part": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, c_int, c_int, P]),
     "flamed_den_time_kernels_graph": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),

@@ -463,12 +463,14 @@ class DenoiserHIP:
                                         nat.ptr(ws), ws.numel(), nat.stream_ptr(dev)), "flamed_den_velocity")
         return v.to(x.dtype)
 
-    def persist_info(self):
-        """(completed persistent launches, broken) of this handle: whether B = 1 solves ran as one persistent
-        launch (flamed_den_persist_info)."""
-        runs, broken = ctypes.c_int(0), ctypes.c_int(0)
-        nat.check(nat.lib().flamed_den_persist_info(self.handle, ctypes.byref(runs), ctypes.byref(broken)),
+    def persist_info(self, with_ms: bool = False):
+        """(completed persistent launches, broken[, device ms of the last launch]) of this handle: whether
+        B = 1 solves ran as one persistent launch (flamed_den_persist_info)."""
+        runs, broken, ms = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_float(0.0)
+        nat.check(nat.lib().flamed_den_persist_info(self.handle, ctypes.byref(runs), ctypes.byref(broken), ctypes.byref(ms)),
                   "flamed_den_persist_info")
+        if with_ms:
+            return runs.value, bool(broken.value), float(ms.value)
         return runs.value, bool(broken.value)
 
     def solve(self, xt: torch.Tensor, ts: torch.Tensor, spk: torch.Tensor, nfe: int) -> torch.Tensor:

@@ -109,9 +109,10 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
 /* The persistent B = 1 solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken
  * by flamed_den_solve / _solve_part with use_graph != 0 for one utterance of 16..512 frames on a bf16
  * handle): *runs = launches completed on this handle, *broken = 1 once a launch timed out (the handle
- * then stays on the graph-of-launches path).  The solve checks its error word before returning (a
+ * then stays on the graph-of-launches path), *last_ms = device time of the last persistent launch (HIP
+ * events around the kernel on the launch stream).  The solve checks its error word before returning (a
  * stream sync), so it is never taken inside a stream capture. */
-FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken);
+FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, float* last_ms);
 
 /* Kernel classes of an Euler step (flamed_den_time_kernels_graph): 0 proj_in GEMM, 1 LN/mod +
  * depthwise conv (+ GroupNorm partials, + finalize by the last-arriving T-chunk), 2 standalone GroupNorm

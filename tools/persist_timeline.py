@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--nfe", type=int, default=16)
     ap.add_argument("--step", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--opt", type=int, default=None, help="flamed_tune persist_opt")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from flamed.models.synthesizer.prob_generator import ProbGenerator
@@ -42,8 +43,11 @@ def main():
     ts = torch.linspace(0, 1, nfe + 1, device=dev)
     buf = torch.zeros(256 * SLOTS, dtype=torch.int64, device=dev)
     L = nat.lib()
+    if a.opt is not None:
+        nat.check(L.flamed_tune(b"persist_opt", a.opt), "flamed_tune")
     with torch.inference_mode():
         hip.solve(x0, ts, spk, nfe)
+        print("after warm solve: persist_info", hip.persist_info(), flush=True)
         nat.check(L.flamed_persist_stamps(nat.ptr(buf), a.step), "flamed_persist_stamps")
         hip.solve(x0, ts, spk, nfe)
         torch.cuda.synchronize()
@@ -51,6 +55,9 @@ def main():
     runs, broken = hip.persist_info()
     st = buf.view(256, SLOTS).cpu().numpy().astype(np.int64)
     n = int((st[0] > 0).sum())
+    if n == 0:
+        print(f"no stamps recorded (runs={runs} broken={broken}, nonzero={(st != 0).sum()})")
+        return
     st = st[:, :n]
     t0 = st[:, 0].min()
     rel = (st - t0) * 10e-3  # microseconds
