@@ -279,9 +279,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   // line stays in the XCD's L2) and read with sc1 loads (L1 bypass, L2 hit); cross-group payloads stay
   // write-through.  More than 32 workgroups on one XCD (not all 256 resident) aborts the solve.
   // Otherwise group = blockIdx % 8 (the round-robin dispatch puts it on one XCD: speed only).
-  const bool xloc = (P.opt & 4) != 0;
+  const bool xcc_id = (P.opt & 4) != 0;
   int g = blockIdx.x % kGroups, s = blockIdx.x / kGroups;
-  if (xloc) {
+  if (xcc_id) {
     int* tk = reinterpret_cast<int*>(smem + L_FLAG);
     if (threadIdx.x == 0) {
       unsigned xcc;
@@ -298,6 +298,17 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     __syncthreads();
     if (s >= kSlots) return;
   }
+  // opt & 8: the XCDs as a 2 x 4 grid of (row half, column quarter): XCD x holds row groups
+  // 4 (x / 4) .. + 3 and column slots 8 (x % 4) .. + 7, so per GEMM phase an XCD's L2 pulls 4 row
+  // panels of A (each read by 8 of its CUs) and 8 weight panels (each read by 4) -- ~0.9 MB per XCD
+  // instead of 1 row panel + all 32 weight panels (2.1 MB): 2.3x less Infinity-Cache traffic per phase.
+  // A row group's 32 producers then span 4 XCDs, so every hand-off stays write-through.
+  if (P.opt & 8) {
+    const int x = g, j = s;
+    g = 4 * (x / 4) + (j % 4);
+    s = 8 * (x % 4) + j / 4;
+  }
+  const bool xloc = xcc_id && !(P.opt & 8);  // group-local payloads may stay in the XCD's L2
   int r0, nr;
   group_rows(g, T, r0, nr, P.opt);
   const int c = lane & 15, q = lane >> 4;
@@ -321,9 +332,16 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   int pst_k = 0;
 #endif
   // after a GEMM phase: the next GEMM's panel goes into the buffer the finished one did not use
+  int cur_step = P.s0;  // (FL_STAMPS builds: the step a helper lambda stamps)
   auto next_w = [&](const bf16* W) {
     wb ^= 1;
     dma_panel<kH>((smem + wb * kWPanel), [&](int n) { return W + (size_t)(col0 + n) * kH; }, wave, lane, P.opt);
+#ifdef FL_STAMPS
+    if (P.opt & 32) {  // diagnostic: when this wave's weight DMA has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PST(cur_step);
+    }
+#endif
   };
   auto next_win = [&]() {
     wb ^= 1;
@@ -361,6 +379,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
   for (int step = P.s0; step < P.s1; ++step) {
     const float* md = P.mods + (size_t)step * P.MS;
+    cur_step = step;
 #ifdef FL_STAMPS
     pst_k = 0;
 #endif
