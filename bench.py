@@ -222,8 +222,16 @@ def secondary_measurements(dev, nfe):
         src_len = torch.tensor([L], device=dev)
         mask = torch.zeros(1, L, dtype=torch.bool, device=dev)
         ms = _time_ms(lambda: pva.sample(enc, src_len, mask, nfe=nfe_d, temperature=0.3), dev)
+        pruns, pbroken, pms = pva.hip().persist_info()
         out["pva_flow_lr"] = {"ms": round(ms, 3), "phonemes": L, "nsteps_durgen": nfe_d,
-                              "us_per_net_eval": round(ms * 1e3 / (2 * nfe_d), 2), "dtype": "f32 (exact MFMA)"}
+                              "us_per_net_eval": round(ms * 1e3 / (2 * nfe_d), 2), "dtype": "f32 (exact MFMA)",
+                              "persistent_flow": {"runs": pruns, "broken": pbroken, "last_flow_ms": round(pms, 3)}}
+        # the 5 s utterance's phoneme count (end_to_end_5s below)
+        L5 = 285
+        enc5 = torch.randn(1, L5, 192, generator=g).to(dev)
+        ms5 = _time_ms(lambda: pva.sample(enc5, torch.tensor([L5], device=dev),
+                                          torch.zeros(1, L5, dtype=torch.bool, device=dev), nfe=nfe_d, temperature=0.3), dev)
+        out["pva_flow_lr"]["L285_ms"] = round(ms5, 3)
         T = 400
         lat = torch.randn(1, 256, T, generator=g).to(dev)
         spk = torch.randn(1, 256, generator=g).to(dev)

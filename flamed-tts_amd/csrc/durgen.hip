@@ -13,6 +13,7 @@
 // pva.py:111-112), builds the interleaved phone/silence repeat prefix sums, and gathers the frames.
 #include "flamed_hip.h"
 #include "gemm.hpp"
+#include "pvaflow.hpp"
 
 #include <mutex>
 #include <vector>
@@ -157,6 +158,23 @@ struct DurNet {
   SplitCtx split;
   char* split_mem = nullptr;
   static constexpr int kSplitTarget = 256, kSplitCounters = 1024;
+  // persistent flow of the (duration, silence) pair (pvaflow.hpp), kept on the duration net's handle:
+  // scratch (counters first, hand-off buffers of both nets, a backup of the two states), pinned error word
+  char* pmem = nullptr;
+  int* perr_host = nullptr;
+  hipEvent_t pev[2] = {nullptr, nullptr};
+  int pdev_ok[pv::kMaxRG + 1] = {-1, -1, -1, -1, -1, -1};  // per row-group count: the grid is all resident
+  bool pbroken = false;
+  int pruns = 0;
+  float plast_ms = 0.f;
+  void release_persist() {
+    if (pmem) (void)hipFree(pmem);
+    if (perr_host) (void)hipHostFree(perr_host);
+    for (hipEvent_t& e : pev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    pmem = nullptr;
+    perr_host = nullptr;
+  }
 };
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -210,6 +228,98 @@ static int net_step(DurNet* n, const float* P, const float* temb, float* xt, con
     return rc;
   hipLaunchKernelGGL(dur_head_kernel<384>, dim3((M + 3) / 4), dim3(256), 0, st, w.R2, n->g2, n->b2, n->lw, n->lb, mask, xt, M, dt, ctr_inc);
   FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+// -------- persistent flow (pvaflow.hpp) --------
+static size_t pva_persist_layout(char* base, int F, pv::Params* P, float** backup) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off = a256(off + bytes); return p; };
+  const size_t M = pv::kMaxM, CS = (size_t)F / pv::kCols;
+  char* ctr = take(4 * (size_t)pv::kCtrInts);
+  char* buf[2][3];
+  for (int n = 0; n < 2; ++n) {
+    buf[n][0] = take(M * F * 4);
+    buf[n][1] = take(M * CS * 8);
+    buf[n][2] = take(M * CS * 16);
+  }
+  char* bk = take(2 * M * 4);
+  if (P) {
+    P->ctr = reinterpret_cast<int*>(ctr);
+    for (int n = 0; n < 2; ++n) {
+      P->net[n].R1 = reinterpret_cast<float*>(buf[n][0]);
+      P->net[n].S1 = reinterpret_cast<float2*>(buf[n][1]);
+      P->net[n].S2 = reinterpret_cast<float4*>(buf[n][2]);
+    }
+  }
+  if (backup) *backup = reinterpret_cast<float*>(bk);
+  return off;
+}
+
+// Row groups of the persistent flow for M rows: as many as the grid allows (48 workgroups each), at most
+// kMaxTiles 16-row tiles per group; 0 = does not fit.
+static int pva_persist_groups(int M, int F) {
+  const int MT = (M + 15) / 16, per = 2 * F / pv::kCols;
+  const int RG = std::min(std::min(MT, pv::kMaxRG), 256 / per);
+  return (RG > 0 && MT <= RG * pv::kMaxTiles) ? RG : 0;
+}
+
+static bool pva_persist_eligible(DurNet* nd, DurNet* ns, int M, hipStream_t st) {
+  if (!tn().pva_persist || nd->pbroken || nd->D != 192 || nd->F != 384 || ns->D != 192 || ns->F != 384) return false;
+  const int RG = pva_persist_groups(M, nd->F);
+  if (RG == 0) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  if (nd->pdev_ok[RG] < 0) nd->pdev_ok[RG] = pv::pva_persist_device_ok(nd->device, 2 * (nd->F / pv::kCols) * RG) ? 1 : 0;
+  return nd->pdev_ok[RG] == 1;
+}
+
+// Every step of both flows in one launch.  *done = false: not run (timed out and rolled back; the pair
+// then stays on the graph path) -- the caller runs the graph path.
+static int pva_persist_run(DurNet* nd, DurNet* ns, const PvaWs& w, const uint8_t* mask, float* dur_t, float* sil_t, int nfe,
+                           int B, int L, float dt, hipStream_t st, bool* done) {
+  *done = false;
+  const int M = B * L, D = nd->D;
+  if (!nd->pmem) FL_HIP(hipMalloc(&nd->pmem, pva_persist_layout(nullptr, nd->F, nullptr, nullptr)));
+  if (!nd->perr_host) FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&nd->perr_host), sizeof(int), hipHostMallocDefault));
+  pv::Params P{};
+  float* backup = nullptr;
+  pva_persist_layout(nd->pmem, nd->F, &P, &backup);
+  P.M = M; P.L = L; P.MT = (M + 15) / 16; P.RG = pva_persist_groups(M, nd->F); P.nfe = nfe; P.dt = dt;
+  P.mask = mask;
+  const DurNet* nets[2] = {nd, ns};
+  const float* Pn[2] = {w.Pd, w.Ps};
+  const float* Tn[2] = {w.TEMBd, w.TEMBs};
+  float* xn[2] = {dur_t, sil_t};
+  for (int i = 0; i < 2; ++i) {
+    const DurNet* n = nets[i];
+    pv::NetP& o = P.net[i];
+    o.P = Pn[i]; o.w0 = n->w0; o.temb = Tn[i]; o.c1w = n->c1w; o.c1b = n->c1b; o.g1 = n->g1; o.b1 = n->b1;
+    o.c2w = n->c2w; o.c2b = n->c2b; o.g2 = n->g2; o.b2 = n->b2; o.lw = n->lw; o.lb = n->lb; o.xt = xn[i];
+  }
+  (void)D;
+  P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
+  FL_HIP(hipMemcpyAsync(backup, dur_t, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
+  FL_HIP(hipMemcpyAsync(backup + pv::kMaxM, sil_t, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
+  FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pv::kCtrInts, st));
+  if (!nd->pev[0]) FL_HIP(hipEventCreate(&nd->pev[0]));
+  if (!nd->pev[1]) FL_HIP(hipEventCreate(&nd->pev[1]));
+  FL_HIP(hipEventRecord(nd->pev[0], st));
+  const int lrc = pv::pva_persist_launch(P, st);
+  if (lrc) return lrc;
+  FL_HIP(hipEventRecord(nd->pev[1], st));
+  FL_HIP(hipMemcpyAsync(nd->perr_host, P.ctr + pv::CT_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
+  FL_HIP(hipStreamSynchronize(st));
+  if (*nd->perr_host != 0) {  // a wait timed out: every workgroup left; both states are rolled back
+    FL_HIP(hipMemcpyAsync(dur_t, backup, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
+    FL_HIP(hipMemcpyAsync(sil_t, backup + pv::kMaxM, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
+    nd->pbroken = true;
+    fprintf(stderr, "flamed: persistent PVA flow timed out (B*L=%d); this pair uses the graph path from now on\n", M);
+    return kOk;
+  }
+  *done = true;
+  ++nd->pruns;
+  FL_HIP(hipEventElapsedTime(&nd->plast_ms, nd->pev[0], nd->pev[1]));
   return kOk;
 }
 
@@ -311,6 +421,7 @@ FLAMED_API int flamed_dur_destroy(flamed_dur_t h) {
     std::lock_guard<std::mutex> lk(n->mu);
     DeviceGuard dg(n->device);
     n->graph.release();
+    n->release_persist();
     if (n->dev) (void)hipFree(n->dev);
     if (n->split_mem) (void)hipFree(n->split_mem);
   }
@@ -329,6 +440,8 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* w, int nw, hi
   if (n->device >= 0 && n->device != wdev) {
     DeviceGuard og(n->device);
     n->graph.release();
+    n->release_persist();
+    for (int& v : n->pdev_ok) v = -1;
     if (n->dev) { (void)hipFree(n->dev); n->dev = nullptr; }
     if (n->split_mem) { (void)hipFree(n->split_mem); n->split_mem = nullptr; }
   }
@@ -417,6 +530,11 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   int rc;
   if ((rc = net_prepare(nd, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBd, w.Pd, st))) return rc;
   if ((rc = net_prepare(ns, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBs, w.Ps, st))) return rc;
+  if (use_graph && pva_persist_eligible(nd, ns, M, st)) {
+    bool done = false;
+    if ((rc = pva_persist_run(nd, ns, w, mask, dur_t, sil_t, nfe, B, L, dt, st, &done))) return rc;
+    if (done) return kOk;
+  }
   if (!use_graph) {
     for (int i = 0; i < nfe; ++i) {  // dur then sil on every step (pva.py:104-109)
       if ((rc = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, bd, st))) return rc;
@@ -468,6 +586,16 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   }
   FL_HIP(hipMemsetAsync(gp.ctr, 0, 2 * sizeof(int), st));
   for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(gp.exec, st));
+  return kOk;
+}
+
+FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms) {
+  DurNet* n = reinterpret_cast<DurNet*>(dur);
+  FL_REQUIRE(n && runs && broken && last_ms, "flamed_pva_persist_info: bad args");
+  std::lock_guard<std::mutex> lk(n->mu);
+  *runs = n->pruns;
+  *broken = n->pbroken ? 1 : 0;
+  *last_ms = n->plast_ms;
   return kOk;
 }
 

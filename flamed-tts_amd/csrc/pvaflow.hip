@@ -1,0 +1,346 @@
+// Persistent PVA flow kernel (design notes: pvaflow.hpp).
+#include "flamed_hip.h"
+#include "pvaflow.hpp"
+
+namespace fl {
+namespace pv {
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+// sc1 (write-through) stores and sc1 loads of hand-off data (aux 16 = sc1)
+__device__ __forceinline__ void st4_wt(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 16);
+}
+__device__ __forceinline__ void st8_wt(__amdgpu_buffer_rsrc_t r, unsigned off, float a, float b) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(a), __float_as_uint(b)}, r, off, 0, 16);
+}
+__device__ __forceinline__ void st16_wt(__amdgpu_buffer_rsrc_t r, unsigned off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+}
+__device__ __forceinline__ float4 ld16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+// Every storing wave drains its write-through stores, the workgroup meets, one lane takes the ticket.
+__device__ __forceinline__ void signal(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 polls the counters of row groups rg - 1, rg, rg + 1 (those that exist) until each reaches
+// `target`; bounded by tmo, and an error word set by any workgroup ends every wait.  false: abandon.
+__device__ __forceinline__ bool wait3(int* err, long long tmo, int* base, int rg, int RG, int target, int* flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x, g = rg - 1 + lane;
+    const bool need = lane < 3 && g >= 0 && g < RG;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (unsigned it = 0;; ++it) {
+      bool mine = true;
+      if (need) mine = __hip_atomic_load(base + g * kLine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      if (__all(mine)) break;
+      if ((it & 31) == 31) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
+        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
+          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = false;
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *flag = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = *flag != 0;
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: hand-off loads stay below the poll
+  return ok;
+}
+
+// K blocks [kb0, kb1) of 16 (a multiple of 9 blocks) of one 16 x 16 fp32 tile: lane (c, q) supplies A
+// elements k = 16 kb + 4 q .. + 3 of its row (af) and reads the same four K of weight column c from the
+// resident LDS panel (row stride K floats, 16-B chunks XOR-swizzled by the column); MFMA j of a block
+// consumes element j of every lane's chunk, so both operands see one K permutation.
+template <class AF>
+__device__ __forceinline__ void kloop(f32x4& acc, const float* W, int K, int kb0, int kb1, int c, int q, AF af) {
+  constexpr int kBatch = 9;
+  for (int kb = kb0; kb < kb1; kb += kBatch) {
+    float4 a[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) a[i] = af(kb + i);
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const float4 b = *reinterpret_cast<const float4*>(W + c * K + 4 * ((4 * (kb + i) + q) ^ c));
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b.w, acc, 0, 0, 0);
+    }
+  }
+}
+
+template <int D, int F>
+__global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
+  using LY = Lds<D, F>;
+  constexpr int K1 = LY::K1, K2 = LY::K2, CS = LY::CS, NB1 = K1 / 16, NB2 = K2 / 16;
+  static_assert(NB1 % 36 == 0 && NB2 % 36 == 0, "K blocks split 1 / 2 / 4 ways in batches of 9");
+  static_assert(CS < 32 && CS % 2 == 0, "head constants, paired LN1 partial loads");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* W1 = reinterpret_cast<float*>(smem + LY::W1);
+  float* W2 = reinterpret_cast<float*>(smem + LY::W2);
+  float* vw0 = reinterpret_cast<float*>(smem + LY::W0);
+  float* vg1 = reinterpret_cast<float*>(smem + LY::G1);
+  float* vb1 = reinterpret_cast<float*>(smem + LY::B1);
+  float* vte = reinterpret_cast<float*>(smem + LY::TE);
+  float* xs = reinterpret_cast<float*>(smem + LY::XS);   // x_t of window rows r0 - 1 .. r0 + nr
+  float* st = reinterpret_cast<float*>(smem + LY::ST);   // LN1 (mean, rstd) of the same rows
+  float* gs = reinterpret_cast<float*>(smem + LY::GS);   // G_s of the CS slices, [CS] = sum b2 lw
+  float4* red = reinterpret_cast<float4*>(smem + LY::RED);
+  int* flag = reinterpret_cast<int*>(smem + LY::FLAG);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int per = CS * P.RG;
+  const int net = blockIdx.x / per, rem = blockIdx.x - net * per, rg = rem / CS, cs = rem - rg * CS;
+  const NetP& N = P.net[net];
+  const int M = P.M, L = P.L;
+  const int tb = rg * P.MT / P.RG, te = (rg + 1) * P.MT / P.RG;
+  const int r0 = 16 * tb, nr = min(16 * te, M) - r0, nt = te - tb;
+  const int col0 = cs * kCols, xa = r0 - 1, nw = nr + 2;
+  int* h1 = P.ctr + CT_H1 + net * kMaxRG * kLine;
+  int* h2 = P.ctr + CT_H2 + net * kMaxRG * kLine;
+  int* errw = P.ctr + CT_ERR;
+  const long long tmo = P.tmo;
+
+  // ---- resident state: this workgroup's weight columns of both convs, shared vectors, x_t window
+  for (int i = tid; i < kCols * K1 / 4; i += kThreads) {
+    const int n = i / (K1 / 4), j = i - n * (K1 / 4);
+    *reinterpret_cast<float4*>(W1 + n * K1 + 4 * (j ^ (n & 15))) = ld4(N.c1w + (size_t)(col0 + n) * K1 + 4 * j);
+  }
+  for (int i = tid; i < kCols * K2 / 4; i += kThreads) {
+    const int n = i / (K2 / 4), j = i - n * (K2 / 4);
+    *reinterpret_cast<float4*>(W2 + n * K2 + 4 * (j ^ (n & 15))) = ld4(N.c2w + (size_t)(col0 + n) * K2 + 4 * j);
+  }
+  for (int i = tid; i < D; i += kThreads) vw0[i] = N.w0[i];
+  for (int i = tid; i < F; i += kThreads) {
+    vg1[i] = N.g1[i];
+    vb1[i] = N.b1[i];
+  }
+  if (tid < CS) {
+    float g = 0.f;
+    for (int k = 0; k < kCols; ++k) g = fmaf(N.g2[kCols * tid + k], N.lw[kCols * tid + k], g);
+    gs[tid] = g;
+  } else if (tid == 32) {
+    float bl = 0.f;
+    for (int k = 0; k < F; ++k) bl = fmaf(N.b2[k], N.lw[k], bl);
+    gs[CS] = bl;
+  }
+  for (int i = tid; i < nw; i += kThreads) {
+    const int r = xa + i;
+    xs[i] = (r >= 0 && r < M) ? N.xt[r] : 0.f;
+  }
+  const float bias1 = N.c1b[col0 + c], bias2 = N.c2b[col0 + c];
+  const float gl = N.g2[col0 + c] * N.lw[col0 + c];
+  const float lb = N.lb[0];
+  const __amdgpu_buffer_rsrc_t rR1 = rsrc(N.R1, (unsigned)M * F * 4);
+  const __amdgpu_buffer_rsrc_t rS1 = rsrc(N.S1, (unsigned)M * CS * 8);
+  const __amdgpu_buffer_rsrc_t rS2 = rsrc(N.S2, (unsigned)M * CS * 16);
+  __syncthreads();
+
+  // waves -> (tile, K part): one tile split over 4 / 2 waves, or tiles w, w + 4 whole
+  const int KS = nt == 1 ? 4 : (nt == 2 ? 2 : 1);
+  const int part = wave % KS;
+
+  // one conv: every wave's K part of its tile(s), the K parts summed through LDS in part order, then the
+  // epilogue by the part-0 waves
+  auto conv = [&](const float* W, int K, int NB, auto af, auto epi) {
+    if (KS > 1) {
+      const int t = wave / KS;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      kloop(acc, W, K, part * NB / KS, (part + 1) * NB / KS, c, q, af(t));
+      red[wave * 64 + lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      __syncthreads();
+      if (part == 0) {
+        for (int p = 1; p < KS; ++p) {
+          const float4 o = red[(wave + p) * 64 + lane];
+          acc[0] += o.x; acc[1] += o.y; acc[2] += o.z; acc[3] += o.w;
+        }
+        epi(t, acc);
+      }
+    } else {
+      for (int t = wave; t < nt; t += 4) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        kloop(acc, W, K, 0, NB, c, q, af(t));
+        epi(t, acc);
+      }
+    }
+  };
+
+  for (int s = 0; s < P.nfe; ++s) {
+    for (int i = tid; i < D; i += kThreads) vte[i] = N.temb[(size_t)s * D + i];
+    __syncthreads();
+
+    // ---- conv1 (pva.py:221-230: proj(cat(x_t, enc)) + temb -> Conv k3 -> ReLU) + LN1 partials
+    conv(W1, K1, NB1,
+         [&](int t) {
+           const int m = r0 + 16 * t + c;
+           const bool live = m < r0 + nr;
+           const int lm = live ? m % L : 0;
+           return [=](int kb) -> float4 {
+             const int k0 = 16 * kb + 4 * q, tap = k0 / D, ch = k0 - tap * D, l = lm + tap - 1;
+             float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+             if (live && l >= 0 && l < L) {
+               const int src = m + tap - 1;
+               const float4 p = ld4(N.P + (size_t)src * D + ch);
+               const float4 w = *reinterpret_cast<const float4*>(vw0 + ch);
+               const float4 e = *reinterpret_cast<const float4*>(vte + ch);
+               const float x = xs[src - xa];
+               r.x = (p.x + w.x * x) + e.x;
+               r.y = (p.y + w.y * x) + e.y;
+               r.z = (p.z + w.z * x) + e.z;
+               r.w = (p.w + w.w * x) + e.w;
+             }
+             return r;
+           };
+         },
+         [&](int t, const f32x4& acc) {
+#pragma unroll
+           for (int i = 0; i < 4; ++i) {
+             const int row = 16 * t + 4 * q + i;
+             const float v = fmaxf(acc[i] + bias1, 0.f);
+             if (row < nr) st4_wt(rR1, (unsigned)(((r0 + row) * F + col0 + c) * 4), v);
+             const float mean = wave_sum16(v) * (1.0f / kCols);
+             const float d = v - mean;
+             const float m2 = wave_sum16(d * d);
+             if (c == 0 && row < nr) st8_wt(rS1, (unsigned)(((r0 + row) * CS + cs) * 8), mean, m2);
+           }
+         });
+    signal(h1 + rg * kLine);
+    if (!wait3(errw, tmo, h1, rg, P.RG, CS * (s + 1), flag)) return;
+
+    // LN1 statistics of the window rows from the CS partials (equal-count combine, as the launch path)
+    if (tid < nw) {
+      const int r = xa + tid;
+      float mean = 0.f, rstd = 0.f;
+      if (r >= 0 && r < M) {
+        float2 pp[CS];  // two partials per 16-B load (CS even)
+#pragma unroll
+        for (int k = 0; k < CS; k += 2) {
+          const float4 v = ld16_sc1(rS1, (unsigned)((r * CS + k) * 8));
+          pp[k] = make_float2(v.x, v.y);
+          pp[k + 1] = make_float2(v.z, v.w);
+        }
+        float sm = 0.f;
+#pragma unroll
+        for (int k = 0; k < CS; ++k) sm += pp[k].x;
+        mean = sm / (float)CS;
+        float m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < CS; ++k) {
+          const float d = pp[k].x - mean;
+          m2 += pp[k].y + (float)kCols * d * d;
+        }
+        rstd = 1.0f / sqrtf(m2 / (float)(CS * kCols) + 1e-5f);
+      }
+      st[2 * tid] = mean;
+      st[2 * tid + 1] = rstd;
+    }
+    __syncthreads();
+
+    // ---- conv2 (Conv k3 over LN1 -> ReLU) + head partials over the slice
+    conv(W2, K2, NB2,
+         [&](int t) {
+           const int m = r0 + 16 * t + c;
+           const bool live = m < r0 + nr;
+           const int lm = live ? m % L : 0;
+           return [=](int kb) -> float4 {
+             const int k0 = 16 * kb + 4 * q, tap = k0 / F, ch = k0 - tap * F, l = lm + tap - 1;
+             float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+             if (live && l >= 0 && l < L) {
+               const int src = m + tap - 1, i = src - xa;
+               const float4 v = ld16_sc1(rR1, (unsigned)((src * F + ch) * 4));
+               const float mean = st[2 * i], rstd = st[2 * i + 1];
+               const float4 g = *reinterpret_cast<const float4*>(vg1 + ch);
+               const float4 b = *reinterpret_cast<const float4*>(vb1 + ch);
+               r.x = ((v.x - mean) * rstd) * g.x + b.x;
+               r.y = ((v.y - mean) * rstd) * g.y + b.y;
+               r.z = ((v.z - mean) * rstd) * g.z + b.z;
+               r.w = ((v.w - mean) * rstd) * g.w + b.w;
+             }
+             return r;
+           };
+         },
+         [&](int t, const f32x4& acc) {
+#pragma unroll
+           for (int i = 0; i < 4; ++i) {
+             const int row = 16 * t + 4 * q + i;
+             const float v = fmaxf(acc[i] + bias2, 0.f);
+             const float mean = wave_sum16(v) * (1.0f / kCols);
+             const float d = v - mean;
+             const float m2 = wave_sum16(d * d);
+             const float sg = wave_sum16(d * gl);
+             if (c == 0 && row < nr) st16_wt(rS2, (unsigned)(((r0 + row) * CS + cs) * 16), make_float4(mean, m2, sg, 0.f));
+           }
+         });
+    signal(h2 + rg * kLine);
+    if (!wait3(errw, tmo, h2, rg, P.RG, CS * (s + 1), flag)) return;
+
+    // ---- head (LN2 . lw + lb, masked_fill) + Euler update of the window rows (pva.py:104-109, 234-238)
+    if (tid < nw) {
+      const int r = xa + tid;
+      if (r >= 0 && r < M) {
+        float4 pp[CS];
+#pragma unroll
+        for (int k = 0; k < CS; ++k) pp[k] = ld16_sc1(rS2, (unsigned)((r * CS + k) * 16));
+        float sm = 0.f;
+#pragma unroll
+        for (int k = 0; k < CS; ++k) sm += pp[k].x;
+        const float mean = sm / (float)CS;
+        float m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < CS; ++k) {
+          const float d = pp[k].x - mean;
+          m2 += pp[k].y + (float)kCols * d * d;
+        }
+        const float rstd = 1.0f / sqrtf(m2 / (float)F + 1e-5f);
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < CS; ++k) dot += pp[k].z + (pp[k].x - mean) * gs[k];
+        const float vel = P.mask[r] ? 0.f : (rstd * dot + gs[CS]) + lb;
+        xs[tid] = __fadd_rn(xs[tid], __fmul_rn(P.dt, vel));
+      }
+    }
+    __syncthreads();
+  }
+  if (cs == 0)
+    for (int i = tid; i < nr; i += kThreads) N.xt[r0 + i] = xs[i + 1];
+}
+
+size_t pva_persist_lds() { return (size_t)Lds<192, 384>::BYTES; }
+
+bool pva_persist_device_ok(int device, int grid) {
+  int cus = 0, nb = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < grid) return false;
+  const void* k = reinterpret_cast<const void*>(pva_persist_kernel<192, 384>);
+  if (set_max_lds(k) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pva_persist_kernel<192, 384>, kThreads, Lds<192, 384>::BYTES) != hipSuccess)
+    return false;
+  return nb >= 1;
+}
+
+int pva_persist_launch(const Params& P, hipStream_t st) {
+  const int grid = 2 * Lds<192, 384>::CS * P.RG;
+  auto kern = pva_persist_kernel<192, 384>;
+  constexpr unsigned lds = Lds<192, 384>::BYTES;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st, P);
+  FL_LAUNCH_CHECK();
+  return kOk;
+}
+
+}  // namespace pv
+}  // namespace fl

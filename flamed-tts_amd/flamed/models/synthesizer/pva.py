@@ -310,3 +310,12 @@ class PvaHIP:
                                      nat.ptr(ws), ws.numel(), int(bool(self.pva.hip_graph)), nat.stream_ptr(dev)),
                   "flamed_pva_flow")
         return bufs["dur"].clone(), bufs["sil"].clone()
+
+    def persist_info(self):
+        """(persistent flows completed, timed out, device ms of the last one) on this pair (pvaflow.hip)."""
+        if self.handles[0] is None:
+            return 0, False, 0.0
+        runs, broken, ms = ctypes.c_int(), ctypes.c_int(), ctypes.c_float()
+        nat.check(nat.lib().flamed_pva_persist_info(self.handles[0], ctypes.byref(runs), ctypes.byref(broken),
+                                                    ctypes.byref(ms)), "flamed_pva_persist_info")
+        return runs.value, bool(broken.value), ms.value

@@ -168,6 +168,8 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "pva_split"     — 1: the PVA nets' small-M exact-fp32 GEMMs split K over workgroups
  *                     (per-handle slabs, fixed slice order: deterministic); 0 (default: measured
  *                     no faster): one K chain;
+ *   "pva_persist"   — 1 (default): the PVA flow of both nets runs as one persistent launch when it
+ *                     fits (see flamed_pva_flow); 0: hipGraph of launches;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     FLAMED_DEN_KERNEL_CLASSES) twice per Euler step; -1 (default) = off.
@@ -215,10 +217,16 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* weights, int 
 FLAMED_API size_t flamed_pva_workspace_size(flamed_dur_t h, int B, int L, int nfe);
 /* Whole nfe-step flow of both generators, in place on dur_t / sil_t (B*L, the initial noise *
  * temperature).  enc: (B*L) x input_size encoder output; mask: uint8 B*L, 1 = padding (src_mask);
- * ts: nfe+1 fp32 time grid (torch.linspace(0, 1, nfe+1)).  use_graph != 0 replays a cached hipGraph. */
+ * ts: nfe+1 fp32 time grid (torch.linspace(0, 1, nfe+1)).  use_graph != 0: the fast path -- one
+ * persistent launch for every step of both nets (pvaflow.hpp; input 192, filter 384, B*L <= 640, all its
+ * workgroups resident, stream not capturing, knob "pva_persist"; the call then waits for the launch to
+ * check its error word), else a cached hipGraph replay; use_graph == 0: plain launches. */
 FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* enc, const uint8_t* mask, float* dur_t,
                                float* sil_t, const float* ts, int nfe, int B, int L, void* ws, size_t ws_bytes,
                                int use_graph, hipStream_t stream);
+/* (diagnostic) persistent PVA flows completed on the duration handle, whether one timed out (the pair
+ * then stays on the graph path), device ms of the last one. */
+FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms);
 /* Length regulator, phase 1: per-utterance interleaved [phone_l, silence_l] repeat counts
  * (padding phonemes -> 1 frame, 0 silence), exclusive prefix sums cum (int64 B x (2L+1)) and
  * tgt_len (int64 B).  phone/sil are frame counts, or final log-durations when log_domain != 0

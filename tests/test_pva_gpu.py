@@ -43,21 +43,69 @@ def test_pva_flow_and_sample_golden(pva):
     assert x_lr.shape == g["x_lr"].shape and np.array_equal(x_lr.cpu().numpy(), g["x_lr"])
 
 
+def _tune(key, v):
+    from flamed import _native as nat
+    nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")
+
+
 def test_pva_graph_equals_eager(pva):
+    """The hipGraph of launches (persistent flow off) replays exactly the plain launches."""
     m, _ = pva
     gen = torch.Generator().manual_seed(3)
     B, L = 3, 41
     enc = torch.randn(B, L, 192, generator=gen).to(DEV)
     mask = (torch.arange(L)[None, :] >= torch.tensor([41, 30, 7])[:, None]).to(DEV)
     outs = []
-    with torch.inference_mode():
-        for graph in (True, True, False):
-            m.hip_graph = graph
-            torch.manual_seed(5)
-            outs.append(m.flow(enc, mask, 6, 0.3))
-    m.hip_graph = True
+    try:
+        _tune("pva_persist", 0)
+        with torch.inference_mode():
+            for graph in (True, True, False):
+                m.hip_graph = graph
+                torch.manual_seed(5)
+                outs.append(m.flow(enc, mask, 6, 0.3))
+    finally:
+        m.hip_graph = True
+        _tune("pva_persist", 1)
     for o in outs[1:]:
         assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+
+
+@pytest.mark.parametrize("B,L,nfe", [(1, 60, 64), (1, 285, 64), (3, 41, 6), (2, 247, 16), (1, 1, 8), (1, 17, 4),
+                                     (5, 128, 8)])
+def test_pva_persistent_flow(pva, B, L, nfe):
+    """One persistent launch for every step of both nets (pvaflow.hip): it really ran (persist_info), two
+    runs are bitwise equal (fixed combine orders), and against the oracle and the graph of launches the
+    log-durations agree to rel-L2 <= 1e-5 with ZERO integer frame flips at positions not within 1e-4 of
+    a .5 rounding boundary.  Covers one to eight 16-row tiles per row group, K split 4 / 2 / 1 ways over
+    the waves, a single phoneme, ragged masks and utterance edges inside a row group."""
+    m, sd = pva
+    gen = torch.Generator().manual_seed(100 + B * L)
+    enc = torch.randn(B, L, 192, generator=gen)
+    lens = torch.tensor([L] + [max(1, L - 37 * i) for i in range(1, B)])
+    mask = torch.arange(L)[None, :] >= lens[:, None]
+    torch.manual_seed(7)
+    dn, sn = torch.randn((B, L)), torch.randn((B, L))
+    hp = m.hip()
+    outs = []
+    with torch.inference_mode():
+        for persist in (1, 1, 0):
+            _tune("pva_persist", persist)
+            r0 = hp.persist_info()[0] if hp.handles[0] is not None else 0
+            torch.manual_seed(7)
+            outs.append(m.flow(enc.to(DEV), mask.to(DEV), nfe, 0.3))
+            ran = hp.persist_info()[0] - r0
+            assert ran == persist, (persist, ran, hp.persist_info())
+    _tune("pva_persist", 1)
+    assert not hp.persist_info()[1]
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    rd, rs = orc.pva_flow(sd, enc, mask, nfe, 0.3, noise=(dn, sn))
+    flips = 0
+    for got, graph, ref in ((outs[0][0].cpu(), outs[2][0].cpu(), rd), (outs[0][1].cpu(), outs[2][1].cpu(), rs)):
+        assert rel_l2(got, ref) < 1e-5 and rel_l2(got, graph) < 1e-5
+        e = torch.exp(ref) - 1
+        safe = (e - e.floor() - 0.5).abs() > 1e-4
+        flips += int((orc.log_to_frames(got)[safe] != orc.log_to_frames(ref)[safe]).sum())
+    assert flips == 0
 
 
 def test_pva_flow_vs_oracle_larger(pva):
@@ -140,12 +188,14 @@ def test_pva_split_k_deterministic(pva, B, L):
     L_ = nat.lib()
     outs = []
     try:
+        nat.check(L_.flamed_tune(b"pva_persist", 0), "tune")  # the split applies to the graph of launches
         with torch.inference_mode():
             for sp in (1, 1, 0):
                 nat.check(L_.flamed_tune(b"pva_split", sp), "tune")
                 outs.append(m.hip().flow(x, mask, d0, s0, ts, 64))
     finally:
         nat.check(L_.flamed_tune(b"pva_split", 0), "tune")
+        nat.check(L_.flamed_tune(b"pva_persist", 1), "tune")
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     # the split really ran (the knob is part of the graph key): reassociated, so not bitwise equal
     assert not (torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1]))

@@ -26,6 +26,8 @@ CLASSES = [
     ("mlp2_gemm_gated_resid", [r"EpiGatedResid"]),
     ("lnmod_conv_out_gemm", [r"LoadLNMod<[^>]*false>", r"LoadLNModI\w+Lb0E", r"EpiLNFold<float", r"EpiLNFoldIf"]),
     ("conv_out_combine_euler", [r"conv3_combine_kernel"]),
+    # B = 1 persistent solve (persist.hip): one launch per solve, every step inside
+    ("den_persist_kernel", [r"den_persist_kernel"]),
 ]
 
 
@@ -43,6 +45,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--nfe", type=int, default=128)
     a = ap.parse_args()
     stats = list(csv.DictReader(open(os.path.join(a.run_dir, "prof", "run_kernel_stats.csv"))))
     shutil.copy(os.path.join(a.run_dir, "prof", "run_kernel_stats.csv"), a.out_prefix + "_kernel_stats.csv")
@@ -84,7 +87,7 @@ def main():
             traffic[cls] = hb
         lines.append(f"| {cls} | {calls} | {tot / calls / 1e3:.2f} | {'' if fm is None else f'{fm:.1f}'} | "
                      f"{'' if wm is None else f'{wm:.1f}'} | {'' if hb is None else f'{hb:.0f}'} |")
-    meta = {"batch": a.batch, "frames": a.frames, "dtype": a.dtype, "source": os.path.basename(a.out_prefix),
+    meta = {"batch": a.batch, "frames": a.frames, "dtype": a.dtype, "nfe": a.nfe, "source": os.path.basename(a.out_prefix),
             "bytes_per_launch": traffic}
     json.dump(meta, open(a.out_prefix + "_traffic.json", "w"), indent=1)
     bench = os.path.join(a.run_dir, "bench.json")
