@@ -128,12 +128,53 @@ __device__ __forceinline__ void dma_panel(char* dst, RowF rowp, int wave, int la
   }
 }
 
+// The same panel issued by all four waves (persist_opt 1) with the per-piece work cut to the bone: the j loop
+// unrolled, the row base a scalar pointer (global_load_lds with saddr) and the lane's 32-bit byte offset
+// row n * 2K + swizzled chunk; rowb(n) gives row n's byte offset from `base`.  (The generic loop above
+// spent ~1.3 us of every wave per 64 KB panel: 64-bit address math and a rolled loop per piece.)
+// w4 = false: waves 1..3 issue (wave 0 goes straight to polling the next hand-off, its vmcnt free of weights).
+template <int K, class RowB>
+__device__ __forceinline__ void dma_panel4(char* dst, const void* base, RowB rowb, int wave, int lane_in, bool w4 = true) {
+  constexpr int kRowB = 2 * K, kNI = 32 * kRowB / 1024;
+  static_assert(kNI % 4 == 0, "pieces per wave");
+  if (!w4 && wave == 0) return;
+  const int w0 = w4 ? wave : wave - 1, ws = w4 ? 4 : 3;
+  const int lane = opq(lane_in);
+  const unsigned long long b = (unsigned long long)(uintptr_t)base;
+  // (readfirstlane returns int: widen through unsigned, or a low word >= 2^31 sign-extends into the high one)
+  const unsigned blo = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)b);
+  const unsigned bhi = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const unsigned long long bs = ((unsigned long long)bhi << 32) | (unsigned long long)blo;
+  const unsigned l0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(dst)));
+#pragma unroll
+  for (int j = 0; j < (kNI + 2) / 3; ++j) {
+    const int i = w0 + ws * j;
+    if (i >= kNI) break;
+    const unsigned pos = (unsigned)i * 1024u + (unsigned)lane * 16u;
+    const int n = (int)(pos / kRowB);
+    const unsigned jl = (pos % kRowB) >> 4;
+    const unsigned off = rowb(n) + ((jl ^ (unsigned)(n & 15)) << 4);
+    const unsigned l = l0 + (unsigned)i * 1024u;
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(off), "s"(bs), "s"(l)
+                 : "memory");
+  }
+}
+
 // ---- one GEMM phase: wave w < ntile computes rows [16 w, 16 w + 16) of the group's tile x the slot's 32
 // columns: A (bf16 rows, K) straight to registers with sc1 loads (rows >= nr read as 0: buffer range),
 // B fragments from the LDS weight panel.
+// Fragment-major A image (persist_opt 64): group g's rows as [tile t < 4][K-step ks][lane][8 bf16], lane =
+// (row c, K-quarter q) exactly as a v_mfma_f32_16x16x32_bf16 A operand takes it, so a wave's 16-B/lane load
+// of one K-step is ONE contiguous 1 KB (8 full lines) instead of 16 half-lines of 16 rows; rows past the
+// group's last row are stored as zeros.
+__device__ __forceinline__ unsigned frag_group_bytes(int KST) { return (unsigned)(4 * KST * 1024); }
+
 template <int K>
 __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[2], int wave, int lane_in,
-                                     unsigned long long* stamp = nullptr) {
+                                     unsigned long long* stamp = nullptr, int g = 0, bool frag = false) {
   constexpr int KST = K / 32;
   const int lane = opq(lane_in);
   acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -142,10 +183,18 @@ __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* 
   const int c = lane & 15, q = lane >> 4;
   u32x4 a[KST];
   if (wave < ntile) {
-    const __amdgpu_buffer_rsrc_t rs = rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
-    const unsigned base = (unsigned)(((16 * wave + c) * K + q * 8) * 2);
+    if (frag) {
+      const __amdgpu_buffer_rsrc_t rs =
+          rsrc(reinterpret_cast<const char*>(A) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST));
+      const unsigned base = (unsigned)(((wave * KST) * 64 + lane) * 16);
 #pragma unroll
-    for (int ks = 0; ks < KST; ++ks) a[ks] = ld16(rs, base + ks * 64);
+      for (int ks = 0; ks < KST; ++ks) a[ks] = ld16(rs, base + ks * 1024);
+    } else {
+      const __amdgpu_buffer_rsrc_t rs = rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
+      const unsigned base = (unsigned)(((16 * wave + c) * K + q * 8) * 2);
+#pragma unroll
+      for (int ks = 0; ks < KST; ++ks) a[ks] = ld16(rs, base + ks * 64);
+    }
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KST) : "memory");  // this wave's (older) weight DMA landed
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -261,6 +310,20 @@ __device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int
   }
 }
 
+// ... or, fragment-major (persist_opt 64): the staged bf16 tile (rows x this slot's 32 columns = K-step s of
+// the consumer) as group g's fragments (t, s): one contiguous 1 KB per 16-row tile, rows >= nr as zeros.
+__device__ __forceinline__ void flush_frag(const char* stg, bf16* dst, int g, int s, int nr, int KST, bool local) {
+  const int ntile = (nr + 15) >> 4;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(reinterpret_cast<char*>(dst) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST));
+  for (int idx = opq(threadIdx.x); idx < ntile * 64; idx += kThreads) {
+    const int t = idx >> 6, ln = idx & 63, row = 16 * t + (ln & 15), q = ln >> 4;
+    const u32x4 v = row < nr ? *reinterpret_cast<const u32x4*>(stg + row * (kCols * 2) + q * 16) : u32x4{0u, 0u, 0u, 0u};
+    const unsigned off = (unsigned)(((t * KST + s) * 64 + ln) * 16);
+    if (local) st16p(rs, off, v);
+    else st16(rs, off, v);
+  }
+}
+
 __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) {
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
@@ -309,6 +372,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     s = 8 * (x % 4) + j / 4;
   }
   const bool xloc = xcc_id && !(P.opt & 8);  // group-local payloads may stay in the XCD's L2
+  const bool frag = (P.opt & 64) != 0;        // fragment-major GEMM A images (a2, u, xa, xs)
   int r0, nr;
   group_rows(g, T, r0, nr, P.opt);
   const int c = lane & 15, q = lane >> 4;
@@ -333,9 +397,14 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #endif
   // after a GEMM phase: the next GEMM's panel goes into the buffer the finished one did not use
   int cur_step = P.s0;  // (FL_STAMPS builds: the step a helper lambda stamps)
+  const bool fastdma = !(P.opt & 256);  // persist_opt 256: the generic issue loop (A/B)
+  const bool w4 = (P.opt & 1) != 0;
   auto next_w = [&](const bf16* W) {
     wb ^= 1;
-    dma_panel<kH>((smem + wb * kWPanel), [&](int n) { return W + (size_t)(col0 + n) * kH; }, wave, lane, P.opt);
+    if (fastdma)
+      dma_panel4<kH>((smem + wb * kWPanel), W + (size_t)col0 * kH, [](int n) { return (unsigned)(n * 2 * kH); }, wave, lane, w4);
+    else
+      dma_panel<kH>((smem + wb * kWPanel), [&](int n) { return W + (size_t)(col0 + n) * kH; }, wave, lane, P.opt);
 #ifdef FL_STAMPS
     if (P.opt & 32) {  // diagnostic: when this wave's weight DMA has landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -345,7 +414,24 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   };
   auto next_win = [&]() {
     wb ^= 1;
-    dma_panel<kC>((smem + wb * kWPanel), [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane, P.opt);
+    if (fastdma)
+      dma_panel4<kC>((smem + wb * kWPanel), P.win + (size_t)col0 * kC, [](int n) { return (unsigned)(n * 2 * kC); }, wave, lane, w4);
+    else
+      dma_panel<kC>((smem + wb * kWPanel), [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane, P.opt);
+  };
+  auto issue_out = [&]() {  // the conv_out panel (taps stacked): panel row n < 24 is tap n / 8 of channel 8 s + n % 8
+    if (fastdma) {
+      const int s8 = kCh * s;
+      dma_panel4<kH>((smem + (wb ^ 1) * kWPanel), P.wout, [s8](int n) {
+        const int m = n < 24 ? n : n - 24;
+        return (unsigned)(((m >> 3) * kC + s8 + (m & 7)) * 2 * kH);
+      }, wave, lane, w4);
+    } else {
+      dma_panel<kH>((smem + (wb ^ 1) * kWPanel), [&](int n) {
+        const int m = n < 24 ? n : n - 24;
+        return P.wout + (size_t)((m >> 3) * kC + kCh * s + (m & 7)) * kH;
+      }, wave, lane, P.opt);
+    }
   };
 
   // Euler state: thread -> tile row xr_row, channels 8 s + 2 (tid & 3) + {0, 1}
@@ -363,7 +449,17 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     t[xr_row * kCh + 2 * (tid & 3)] = (bf16)xs0;
     t[xr_row * kCh + 2 * (tid & 3) + 1] = (bf16)xs1;
     __syncthreads();
-    if (tid < nr) {
+    if (frag) {  // channels 8 s .. 8 s + 7 = K-step s / 4, quarter s % 4 of proj_in's fragments
+      if (tid < 16 * ((nr + 15) >> 4)) {
+        const __amdgpu_buffer_rsrc_t rs =
+            rsrc(reinterpret_cast<char*>(P.xs) + (size_t)g * frag_group_bytes(kC / 32), frag_group_bytes(kC / 32));
+        const int t = tid >> 4, ln = (tid & 15) + 16 * (s & 3);
+        const u32x4 v = tid < nr ? *reinterpret_cast<const u32x4*>(stg + tid * 16) : u32x4{0u, 0u, 0u, 0u};
+        const unsigned off = (unsigned)(((t * (kC / 32) + (s >> 2)) * 64 + ln) * 16);
+        if (xloc) st16p(rs, off, v);
+        else st16(rs, off, v);
+      }
+    } else if (tid < nr) {
       const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)T * kC * 2);
       const unsigned off = (unsigned)(((size_t)(r0 + tid) * kC + kCh * s) * 2);
       if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
@@ -388,7 +484,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     PST(step);
     if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
     PST(step);
-    gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
+    gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     PST(step);
     acc_to(X, acc);
 #pragma unroll
@@ -550,7 +646,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         for (int k = 0; k < 8; ++k) t[(8 * rg + k) * kCols + cc] = (bf16)((d[k] - gv.x) * gv.y + gv.z);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T, xloc);
+      if (frag) flush_frag(stg, P.a2, g, s, nr, kH / 32, xloc);
+      else flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
@@ -560,7 +657,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
-      gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
+      gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
       {
         float v[2][4];
@@ -572,7 +669,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         stage_tile<bf16>(stg, v, wave, lane);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
+      if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
+      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
@@ -591,7 +689,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
-      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
+      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
       {
         float v[2][4];
@@ -610,7 +708,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         stage_tile<bf16>(stg, v, wave, lane);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T, xloc);
+      if (frag) flush_frag(stg, P.xa, g, s, nr, kH / 32, xloc);
+      else flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
@@ -624,7 +723,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
       row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
-      gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));  // (its barrier orders the statistics)
+      gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);  // (its barrier orders the statistics)
       PST(step);
       {
         float v[2][4];
@@ -639,7 +738,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         stage_tile<bf16>(stg, v, wave, lane);
       }
       __syncthreads();
-      flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
+      if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
+      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
       signal(mygrp);
       PST(step);
       ++L;
@@ -650,7 +750,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
       PST(step);
-      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
+      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
@@ -668,11 +768,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
     // -------- conv_out k3 (taps stacked; LayerNorm + modulate folded; :238-245, 264).  Panel row n < 24 is
     // tap n / 8 of latent channel 8 s + n % 8; rows 24..31 repeat rows 0..7 (ignored)
+    issue_out();
     wb ^= 1;
-    dma_panel<kH>((smem + wb * kWPanel), [&](int n) {
-      const int m = n < 24 ? n : n - 24;
-      return P.wout + (size_t)((m >> 3) * kC + kCh * s + (m & 7)) * kH;
-    }, wave, lane, P.opt);
     float fac[2], fbc[2];  // fold vectors of the lane's stacked columns, before the wait
     {
       const float* fo = md + P.MS0 + (size_t)P.NB * 2 * H;  // [wa (3 C), wb (3 C)]
@@ -688,7 +785,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
     PST(step);
     row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
-    gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step));
+    gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     PST(step);
     float* yl = reinterpret_cast<float*>(stg);  // Y of the tile: [row][24] fp32 (tap-major x 8 channels)
 #pragma unroll

@@ -11,6 +11,11 @@
 //   * the Euler state x of its (frames x 8 channels), in registers across ALL steps (fp32);
 //   * each GEMM phase's weight panel (32 output columns x K, bf16), LDS-DMA'd into one of two LDS
 //     buffers by the previous GEMM phase, so a phase only waits for its activations.
+// GEMM A operands (bf16 x_t, GroupNorm output, conv_2 / mlp.0 outputs, x * alpha) are handed over
+// fragment-major (persist_opt 64, default): group g's rows as [16-row tile][32-wide K-step][lane][8 bf16],
+// the exact register image of a v_mfma_f32_16x16x32_bf16 A operand, so each consumer wave's load of one
+// K-step is one contiguous 1 KB (8 full lines) instead of 16 rows x 64 B (16 half-lines): the per-XCD L2
+// request rate, not bytes, was what the A fetch waited on (2.4 -> 1.2 us per GEMM phase, 26.4 -> 22.8 ms).
 // Every activation handed to another workgroup (bf16 GEMM operands, LayerNorm row partials, halo rows,
 // GroupNorm partials, conv_out boundary rows) is stored write-through (sc1), drained by every storing
 // wave, then one lane adds to a counter; consumers poll with sc1 loads and read the data with sc1

@@ -5,6 +5,21 @@
 namespace fl {
 namespace pv {
 
+// Diagnostic build only (FL_STAMPS, libflamed_hip_stamps.so; tools/pva_timeline.py): thread 0 of every
+// workgroup records s_memrealtime at fixed points of step pst_step.
+#ifdef FL_STAMPS
+#define PVST()                                                                                   \
+  do {                                                                                           \
+    if (s == P.pst_step && P.pst && threadIdx.x == 0 && pst_k < kStampSlots)                     \
+      P.pst[blockIdx.x * kStampSlots + pst_k] = __builtin_amdgcn_s_memrealtime();                 \
+    ++pst_k;                                                                                     \
+  } while (0)
+static unsigned long long* g_pva_pst = nullptr;
+static int g_pva_pst_step = -1;
+#else
+#define PVST() ((void)0)
+#endif
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
 }
@@ -182,8 +197,12 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   };
 
   for (int s = 0; s < P.nfe; ++s) {
+#ifdef FL_STAMPS
+    int pst_k = 0;
+#endif
     for (int i = tid; i < D; i += kThreads) vte[i] = N.temb[(size_t)s * D + i];
     __syncthreads();
+    PVST();
 
     // ---- conv1 (pva.py:221-230: proj(cat(x_t, enc)) + temb -> Conv k3 -> ReLU) + LN1 partials
     conv(W1, K1, NB1,
@@ -220,8 +239,11 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
              if (c == 0 && row < nr) st8_wt(rS1, (unsigned)(((r0 + row) * CS + cs) * 8), mean, m2);
            }
          });
+    PVST();
     signal(h1 + rg * kLine);
+    PVST();
     if (!wait3(errw, tmo, h1, rg, P.RG, CS * (s + 1), flag)) return;
+    PVST();
 
     // LN1 statistics of the window rows from the CS partials (equal-count combine, as the launch path)
     if (tid < nw) {
@@ -251,6 +273,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
       st[2 * tid + 1] = rstd;
     }
     __syncthreads();
+    PVST();
 
     // ---- conv2 (Conv k3 over LN1 -> ReLU) + head partials over the slice
     conv(W2, K2, NB2,
@@ -287,8 +310,11 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
              if (c == 0 && row < nr) st16_wt(rS2, (unsigned)(((r0 + row) * CS + cs) * 16), make_float4(mean, m2, sg, 0.f));
            }
          });
+    PVST();
     signal(h2 + rg * kLine);
+    PVST();
     if (!wait3(errw, tmo, h2, rg, P.RG, CS * (s + 1), flag)) return;
+    PVST();
 
     // ---- head (LN2 . lw + lb, masked_fill) + Euler update of the window rows (pva.py:104-109, 234-238)
     if (tid < nw) {
@@ -316,6 +342,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
       }
     }
     __syncthreads();
+    PVST();
   }
   if (cs == 0)
     for (int i = tid; i < nr; i += kThreads) N.xt[r0 + i] = xs[i + 1];
@@ -333,7 +360,12 @@ bool pva_persist_device_ok(int device, int grid) {
   return nb >= 1;
 }
 
-int pva_persist_launch(const Params& P, hipStream_t st) {
+int pva_persist_launch(const Params& Pin, hipStream_t st) {
+  Params P = Pin;
+#ifdef FL_STAMPS
+  P.pst = g_pva_pst;
+  P.pst_step = g_pva_pst_step;
+#endif
   const int grid = 2 * Lds<192, 384>::CS * P.RG;
   auto kern = pva_persist_kernel<192, 384>;
   constexpr unsigned lds = Lds<192, 384>::BYTES;
@@ -344,3 +376,11 @@ int pva_persist_launch(const Params& P, hipStream_t st) {
 
 }  // namespace pv
 }  // namespace fl
+
+#ifdef FL_STAMPS
+extern "C" FLAMED_API int flamed_pva_stamps(void* buf, int step) {
+  fl::pv::g_pva_pst = reinterpret_cast<unsigned long long*>(buf);
+  fl::pv::g_pva_pst_step = step;
+  return fl::kOk;
+}
+#endif

@@ -51,7 +51,10 @@ struct Params {
   NetP net[2];
   int* ctr;
   long long tmo;  // poll timeout, s_memrealtime ticks (100 MHz)
+  unsigned long long* pst = nullptr;  // FL_STAMPS builds: per-workgroup timeline of step pst_step
+  int pst_step = -1;
 };
+constexpr int kStampSlots = 16;
 
 // LDS carve (bytes) for input size D, filter size F
 template <int D, int F>

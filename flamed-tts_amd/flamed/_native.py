@@ -95,6 +95,7 @@ DIAG_SIGNATURES = {
     "flamed_probe_mx_gemm": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "flamed_stamp_buffer": (c_int, [P]),
     "flamed_persist_stamps": (c_int, [P, c_int]),
+    "flamed_pva_stamps": (c_int, [P, c_int]),
 }
 
 FLAMED_F32, FLAMED_BF16, FLAMED_FP8 = 0, 1, 2

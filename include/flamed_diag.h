@@ -49,6 +49,9 @@ FLAMED_API int flamed_stamp_buffer(void* buf);
  * s_memrealtime at every wait / compute / signal point of Euler step `step` into buf[wg * 160 + k]
  * (device memory, 256 x 160 uint64); buf = NULL turns it off.  tools/persist_timeline.py. */
 FLAMED_API int flamed_persist_stamps(void* buf, int step);
+/* Persistent PVA flow timeline (libflamed_hip_stamps.so only): thread 0 of every workgroup writes
+ * s_memrealtime at fixed points of Euler step `step` into buf[wg * 16 + k]; tools/pva_timeline.py. */
+FLAMED_API int flamed_pva_stamps(void* buf, int step);
 
 #ifdef __cplusplus
 }

@@ -131,3 +131,18 @@ def test_persist_knob_off_uses_launch_path(pgb):
     x2, spk2 = _inputs(8, 2, 64)  # B = 2: never persistent
     _solve(pg, x2, spk2, 4)
     assert _runs(pg) == r0
+
+
+@pytest.mark.parametrize("T", [400, 131, 16])
+def test_persist_fragment_layout_bitwise(pgb, T):
+    """The fragment-major A images (persist_opt 64, default 73) only change where the bf16 operands sit in
+    memory, not any arithmetic: the solve equals the row-major hand-off variant (opt 9) bitwise, for full,
+    partial-tile and nearly-empty row groups (rows past a group's end are stored as zeros)."""
+    pg, _ = pgb
+    x0, spk = _inputs(11, 1, T)
+    r0 = _runs(pg)
+    a = _solve(pg, x0, spk, 8)
+    with knob("persist_opt", 9, 73):
+        b = _solve(pg, x0, spk, 8)
+    assert _runs(pg) == r0 + 2
+    assert torch.equal(a, b)
