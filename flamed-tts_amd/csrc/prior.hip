@@ -5,8 +5,11 @@
 // (Decoder); Layers.py:11-30 (FFTBlock); SubLayers.py:8-57 (MultiHeadAttention, post-norm), :60-95
 // (PositionwiseFeedForward); Modules.py:6-25 (ScaledDotProductAttention).
 //
-// Exact fp32 throughout (f32 MFMA GEMMs = fp32 FMA chains; the encoder output feeds the duration flow,
-// whose rounded frame counts must match the reference).  Rows are channels-last (B*n, D).  Per FFT block
+// Exact fp32 by default (f32 MFMA GEMMs = fp32 FMA chains; the encoder output feeds the duration flow,
+// whose rounded frame counts must match the reference, so the ENCODER always stays fp32).  The decoder
+// side (bridge, shared decoder, the six prompt-prefixed decoders, head) may run its GEMMs on bf16
+// operands with fp32 accumulation (flamed_prior_set_dtype: weights converted once into a second arena,
+// fp32 activations rounded to bf16 in the GEMM A loaders; LayerNorm, softmax, residuals stay fp32).  Rows are channels-last (B*n, D).  Per FFT block
 // (7 launches):
 //   qkv GEMM   X -> [Q|K|V] (M x 3D), w_qs/w_ks/w_vs packed as one (3D x D) weight
 //   attention  one workgroup per (64 queries, head, utterance): K/V staged through LDS in 64-key chunks,
@@ -22,6 +25,7 @@
 #include "xfmr.hpp"
 
 #include <cmath>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -39,6 +43,11 @@ __global__ void prior_taps_kernel(const float* __restrict__ src, float* __restri
   int c = t % Cin;
   int n = t / Cin;
   dst[((size_t)n * KT + k) * Cin + c] = src[i];
+}
+
+__global__ void prior_f32_to_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (bf16)src[i];
 }
 
 // Encoder input: src_word_emb(ids) + position_enc[l] (Models.py:88-92).
@@ -129,6 +138,7 @@ struct EpiHead {
 
 struct FftLayer {
   const float *wqkv, *bqkv, *wfc, *bfc, *g1, *b1, *w1, *c1b, *w2, *c2b, *g2, *b2;
+  const bf16 *wqkv16 = nullptr, *wfc16 = nullptr, *w1_16 = nullptr, *w2_16 = nullptr;  // decoder side, bf16 mode
 };
 struct FftStack {
   int D = 0, H = 0, F = 0, k0 = 0, k1 = 0, maxseq = 0;
@@ -147,6 +157,9 @@ struct Prior {
   const float *prompt_emb = nullptr, *target_emb = nullptr, *q_emb = nullptr, *head_w = nullptr, *head_b = nullptr;
   int head_n = 0;  // padded head rows (multiple of 64)
   CapGraph genc, gdec;
+  int dec_dt = FLAMED_F32;  // decoder-side GEMM operands (flamed_prior_set_dtype)
+  char* dev16 = nullptr;    // bf16 copies of the decoder-side GEMM weights (made on first bf16 decode)
+  const bf16 *bridge_w16 = nullptr, *head_w16 = nullptr;
 };
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -184,21 +197,44 @@ static size_t prior_ws_layout(const Prior* p, int B, int L, int T, int P, void* 
 
 // One FFTBlock stack (Models.py:94-98 / :160-169) in place on X (M = B*n rows).  `embs` (decoders): the
 // last block's LN also writes the target rows into prior_embs[:, q].
+// The GEMM weights of a layer in the stack's operand type.
+template <typename DT> struct LW;
+template <> struct LW<float> {
+  static const float* qkv(const FftLayer& l) { return l.wqkv; }
+  static const float* fc(const FftLayer& l) { return l.wfc; }
+  static const float* c1(const FftLayer& l) { return l.w1; }
+  static const float* c2(const FftLayer& l) { return l.w2; }
+};
+template <> struct LW<bf16> {
+  static const bf16* qkv(const FftLayer& l) { return l.wqkv16; }
+  static const bf16* fc(const FftLayer& l) { return l.wfc16; }
+  static const bf16* c1(const FftLayer& l) { return l.w1_16; }
+  static const bf16* c2(const FftLayer& l) { return l.w2_16; }
+};
+// fp32: the transformer stacks' config choice (xf_gemm); bf16: the shape-driven bf16 configs.
+template <typename DT, class AL, class EP>
+static int pr_gemm(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
+  if constexpr (std::is_same<DT, float>::value) return xf_gemm(al, W, ldw, ep, M, N, K, st);
+  else return launch_gemm<bf16>(al, W, ldw, ep, M, N, K, st);
+}
+
+template <typename DT>
 static int fft_forward(const FftStack& s, float* X, const uint8_t* mask, int B, int n, const PriorWs& w, hipStream_t st,
                        float* embs = nullptr, int P = 0, int T = 0, int nq = 0, int q = 0) {
   const int M = B * n, D = s.D, F = s.F;
   int rc;
   for (size_t li = 0; li < s.layers.size(); ++li) {
     const FftLayer& Ly = s.layers[li];
-    if ((rc = xf_gemm(LoadF32<float>{X, D}, Ly.wqkv, D, EpiBiasAct<float, 0>{Ly.bqkv, w.QKV, 3 * D}, M, 3 * D, D, st))) return rc;
-    if ((rc = attention(D / s.H, w.QKV, mask, B, n, D, s.H, w.O, st))) return rc;
-    if ((rc = xf_gemm(LoadF32<float>{w.O, D}, Ly.wfc, D, EpiBiasRes{Ly.bfc, X, w.R, D}, M, D, D, st))) return rc;
-    if ((rc = ln_mask(D, w.R, Ly.g1, Ly.b1, mask, X, M, n, nullptr, 0, 0, 0, 0, st))) return rc;
-    if ((rc = xf_gemm(LoadConvRows<float, false>{X, D, n, s.k0, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, Ly.w1,
-                                 s.k0 * D, EpiBiasAct<float, 3>{Ly.c1b, w.Hf, F}, M, F, s.k0 * D, st)))
+    if ((rc = pr_gemm<DT>(LoadF32<DT>{X, D}, LW<DT>::qkv(Ly), D, EpiBiasAct<float, 0>{Ly.bqkv, w.QKV, 3 * D}, M, 3 * D, D, st)))
       return rc;
-    if ((rc = xf_gemm(LoadConvRows<float, false>{w.Hf, F, n, s.k1, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, Ly.w2,
-                                 s.k1 * F, EpiBiasRes{Ly.c2b, X, w.R, D}, M, D, s.k1 * F, st)))
+    if ((rc = attention(D / s.H, w.QKV, mask, B, n, D, s.H, w.O, st))) return rc;
+    if ((rc = pr_gemm<DT>(LoadF32<DT>{w.O, D}, LW<DT>::fc(Ly), D, EpiBiasRes{Ly.bfc, X, w.R, D}, M, D, D, st))) return rc;
+    if ((rc = ln_mask(D, w.R, Ly.g1, Ly.b1, mask, X, M, n, nullptr, 0, 0, 0, 0, st))) return rc;
+    if ((rc = pr_gemm<DT>(LoadConvRows<DT, false>{X, D, n, s.k0, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, LW<DT>::c1(Ly),
+                          s.k0 * D, EpiBiasAct<float, 3>{Ly.c1b, w.Hf, F}, M, F, s.k0 * D, st)))
+      return rc;
+    if ((rc = pr_gemm<DT>(LoadConvRows<DT, false>{w.Hf, F, n, s.k1, 1, nullptr, 0, 0, 0.f, nullptr, nullptr}, LW<DT>::c2(Ly),
+                          s.k1 * F, EpiBiasRes{Ly.c2b, X, w.R, D}, M, D, s.k1 * F, st)))
       return rc;
     const bool last = li + 1 == s.layers.size();
     if ((rc = ln_mask(D, w.R, Ly.g2, Ly.b2, mask, X, M, n, last ? embs : nullptr, P, T, nq, q, st))) return rc;
@@ -212,18 +248,26 @@ static int run_encode(Prior* p, const int64_t* texts, const uint8_t* mask, int B
   hipLaunchKernelGGL(embed_pos_kernel, dim3((M * (D / 4) + 255) / 256), dim3(256), 0, st, texts, p->src_emb,
                      pos ? pos : p->enc.pos, M, L, D, out);
   FL_LAUNCH_CHECK();
-  return fft_forward(p->enc, out, mask, B, L, w, st);
+  return fft_forward<float>(p->enc, out, mask, B, L, w, st);
 }
 
+template <typename DT> static const DT* bridge_of(const Prior* p);
+template <> const float* bridge_of<float>(const Prior* p) { return p->bridge_w; }
+template <> const bf16* bridge_of<bf16>(const Prior* p) { return p->bridge_w16; }
+template <typename DT> static const DT* head_of(const Prior* p);
+template <> const float* head_of<float>(const Prior* p) { return p->head_w; }
+template <> const bf16* head_of<bf16>(const Prior* p) { return p->head_w16; }
+
+template <typename DT>
 static int run_decode(Prior* p, const float* x, const uint8_t* tmask, const int64_t* prompts, int B, int T, int P,
                       const float* pos, float* embs, float* logits, const PriorWs& w, hipStream_t st) {
   const int De = p->enc.D, D = p->shared.D, nq = p->nq;
   int rc;
   // bridge + shared decoder (prior_generator.py:165-168)
-  if ((rc = xf_gemm(LoadF32<float>{x, De}, p->bridge_w, De, EpiBiasPos{p->bridge_b, pos ? pos : p->shared.pos, T, w.Xs, D},
-                               B * T, D, De, st)))
+  if ((rc = pr_gemm<DT>(LoadF32<DT>{x, De}, bridge_of<DT>(p), De,
+                        EpiBiasPos{p->bridge_b, pos ? pos : p->shared.pos, T, w.Xs, D}, B * T, D, De, st)))
     return rc;
-  if ((rc = fft_forward(p->shared, w.Xs, tmask, B, T, w, st))) return rc;
+  if ((rc = fft_forward<DT>(p->shared, w.Xs, tmask, B, T, w, st))) return rc;
   // six chained prompt-prefixed decoders (:172-182)
   const int n = P + T, G = B * n * (D / 4);
   for (int q = 0; q < nq; ++q) {
@@ -233,11 +277,44 @@ static int run_decode(Prior* p, const float* x, const uint8_t* tmask, const int6
                        p->prompt_emb, p->target_emb, p->q_emb + (size_t)q * D, pos ? pos : p->dec[q].pos, tmask, B, P, T,
                        D, nq, q, w.X, w.dmask);
     FL_LAUNCH_CHECK();
-    if ((rc = fft_forward(p->dec[q], w.X, w.dmask, B, n, w, st, embs, P, T, nq, q))) return rc;
+    if ((rc = fft_forward<DT>(p->dec[q], w.X, w.dmask, B, n, w, st, embs, P, T, nq, q))) return rc;
   }
   // code head over (B, nq, T) rows, masked and permuted (:186-188)
-  return xf_gemm(LoadF32<float>{embs, D}, p->head_w, D, EpiHead{p->head_b, tmask, logits, p->vocab + 1, nq, T},
-                            B * nq * T, p->head_n, D, st);
+  return pr_gemm<DT>(LoadF32<DT>{embs, D}, head_of<DT>(p), D, EpiHead{p->head_b, tmask, logits, p->vocab + 1, nq, T},
+                     B * nq * T, p->head_n, D, st);
+}
+
+// bf16 copies of every decoder-side GEMM weight (bridge, shared + per-quantizer decoder layers, padded
+// head), converted once from the fp32 arena into a second one.
+static int ensure_bf16(Prior* p, hipStream_t st) {
+  if (p->dev16) return kOk;
+  struct Item { const float* src; size_t n; const bf16** dst; };
+  std::vector<Item> items;
+  const size_t D = p->shared.D, F = p->shared.F, De = p->enc.D;
+  items.push_back({p->bridge_w, D * De, &p->bridge_w16});
+  auto stack = [&](FftStack& s) {
+    for (FftLayer& L : s.layers) {
+      items.push_back({L.wqkv, 3 * D * D, &L.wqkv16});
+      items.push_back({L.wfc, D * D, &L.wfc16});
+      items.push_back({L.w1, F * s.k0 * D, &L.w1_16});
+      items.push_back({L.w2, D * s.k1 * F, &L.w2_16});
+    }
+  };
+  stack(p->shared);
+  for (FftStack& s : p->dec) stack(s);
+  items.push_back({p->head_w, (size_t)p->head_n * D, &p->head_w16});
+  size_t total = 0;
+  for (const Item& it : items) total += a256(2 * it.n);
+  FL_HIP(hipMalloc(&p->dev16, total));
+  size_t off = 0;
+  for (const Item& it : items) {
+    bf16* dst = reinterpret_cast<bf16*>(p->dev16 + off);
+    hipLaunchKernelGGL(prior_f32_to_bf16_kernel, dim3((unsigned)((it.n + 255) / 256)), dim3(256), 0, st, it.src, dst, it.n);
+    FL_LAUNCH_CHECK();
+    *it.dst = dst;
+    off += a256(2 * it.n);
+  }
+  return kOk;
 }
 
 }  // namespace fl
@@ -286,6 +363,7 @@ FLAMED_API int flamed_prior_destroy(flamed_prior_t h) {
     p->genc.release();
     p->gdec.release();
     if (p->dev) (void)hipFree(p->dev);
+    if (p->dev16) (void)hipFree(p->dev16);
   }
   delete p;
   return kOk;
@@ -310,12 +388,14 @@ FLAMED_API int flamed_prior_load(flamed_prior_t h, const float* const* w, int nw
     p->genc.release();
     p->gdec.release();
     if (p->dev) { (void)hipFree(p->dev); p->dev = nullptr; }
+    if (p->dev16) { (void)hipFree(p->dev16); p->dev16 = nullptr; }
   }
   p->device = wdev;
   FL_ON_DEVICE(wdev);
   p->genc.release();
   p->gdec.release();
   if (p->dev) { FL_HIP(hipFree(p->dev)); p->dev = nullptr; }
+  if (p->dev16) { FL_HIP(hipFree(p->dev16)); p->dev16 = nullptr; }  // stale copies: remade on the next bf16 decode
 
   // arena layout: packed items (qkv concat, conv taps, padded head) + plain copies (VecCopies)
   struct Pack { int kind; const float* src[3]; size_t n; int N, Cin, KT; const float** dst; size_t off; };
@@ -429,10 +509,27 @@ FLAMED_API int flamed_prior_decode(flamed_prior_t h, const float* x, const uint8
   }
   PriorWs w;
   prior_ws_layout(p, B, 0, T, P, ws, &w);
+  const bool b16 = p->dec_dt == FLAMED_BF16;
+  if (b16 && !p->dev16) {
+    int rc = ensure_bf16(p, st);
+    if (rc) return rc;
+  }
   std::vector<const void*> key = {x, tgt_mask, prompts, pos, embs, logits, ws, (const void*)(intptr_t)B,
-                                  (const void*)(intptr_t)T, (const void*)(intptr_t)P, p->dev};
-  return with_graph(p->gdec, key, use_graph != 0, st,
-                    [&](hipStream_t s) { return run_decode(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s); });
+                                  (const void*)(intptr_t)T, (const void*)(intptr_t)P, p->dev,
+                                  (const void*)(intptr_t)p->dec_dt, p->dev16};
+  return with_graph(p->gdec, key, use_graph != 0, st, [&](hipStream_t s) {
+    return b16 ? run_decode<bf16>(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s)
+               : run_decode<float>(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s);
+  });
+}
+
+FLAMED_API int flamed_prior_set_dtype(flamed_prior_t h, int dtype) {
+  Prior* p = reinterpret_cast<Prior*>(h);
+  FL_REQUIRE(p, "flamed_prior_set_dtype: null handle");
+  FL_REQUIRE(dtype == FLAMED_F32 || dtype == FLAMED_BF16, "flamed_prior_set_dtype: dtype must be FLAMED_F32 or FLAMED_BF16");
+  std::lock_guard<std::mutex> lk(p->mu);
+  p->dec_dt = dtype;
+  return kOk;
 }
 
 }  // extern "C"

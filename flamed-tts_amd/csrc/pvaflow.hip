@@ -2,6 +2,8 @@
 #include "flamed_hip.h"
 #include "pvaflow.hpp"
 
+#include <type_traits>
+
 namespace fl {
 namespace pv {
 
@@ -76,19 +78,22 @@ __device__ __forceinline__ bool wait3(int* err, long long tmo, int* base, int rg
   return ok;
 }
 
-// K blocks [kb0, kb1) of 16 (a multiple of 9 blocks) of one 16 x 16 fp32 tile: lane (c, q) supplies A
+// K blocks [kb0, kb1) of 16 (a multiple of kBatch blocks) of one 16 x 16 fp32 tile: lane (c, q) supplies A
 // elements k = 16 kb + 4 q .. + 3 of its row (af) and reads the same four K of weight column c from the
 // resident LDS panel (row stride K floats, 16-B chunks XOR-swizzled by the column); MFMA j of a block
-// consumes element j of every lane's chunk, so both operands see one K permutation.
-template <class AF>
-__device__ __forceinline__ void kloop(f32x4& acc, const float* W, int K, int kb0, int kb1, int c, int q, AF af) {
-  constexpr int kBatch = 9;
+// consumes element j of every lane's chunk, so both operands see one K permutation.  A batch's A loads
+// all go out before its MFMAs, so a wave pays one hand-off read latency per batch: the batch is the whole
+// K range of the wave up to 18 blocks (72 VGPRs; 36 spilled at 512 VGPRs).  (Batches of 9 blocks
+// made conv2 six serial sc1 latencies: 6.9 us of a 19.6 us step at L = 60.)
+template <int kBatch, class AF>
+__device__ __forceinline__ void kloop(f32x4& acc, const float* W, int K, int kb0, int kb1, int c, int q, const AF& af) {
   for (int kb = kb0; kb < kb1; kb += kBatch) {
     float4 a[kBatch];
 #pragma unroll
-    for (int i = 0; i < kBatch; ++i) a[i] = af(kb + i);
+    for (int i = 0; i < kBatch; ++i) a[i] = af.raw(kb + i);  // global loads only: one latency per batch
 #pragma unroll
     for (int i = 0; i < kBatch; ++i) {
+      a[i] = af.fin(kb + i, a[i]);  // the transform's LDS vectors are read block by block
       const float4 b = *reinterpret_cast<const float4*>(W + c * K + 4 * ((4 * (kb + i) + q) ^ c));
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b.x, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b.y, acc, 0, 0, 0);
@@ -98,11 +103,106 @@ __device__ __forceinline__ void kloop(f32x4& acc, const float* W, int K, int kb0
   }
 }
 
+// conv1's A element of this lane's row m (tap gather over proj + time embedding, pva.py:227-230):
+// P[src] + w0 * x_t[src] + temb, zero outside the utterance.
+template <int D>
+struct AConv1 {
+  const float* P;
+  const float *w0, *te, *xs;
+  int m, lm, L, xa, q;
+  bool live;
+  __device__ bool valid(int kb, int& src, int& ch) const {
+    const int k0 = 16 * kb + 4 * q, tap = k0 / D, l = lm + tap - 1;
+    ch = k0 - tap * D;
+    src = m + tap - 1;
+    return live && l >= 0 && l < L;
+  }
+  __device__ float4 raw(int kb) const {
+    int src, ch;
+    return valid(kb, src, ch) ? ld4(P + (size_t)src * D + ch) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __device__ float4 fin(int kb, float4 p) const {
+    int src, ch;
+    if (!valid(kb, src, ch)) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 w = *reinterpret_cast<const float4*>(w0 + ch);
+    const float4 e = *reinterpret_cast<const float4*>(te + ch);
+    const float x = xs[src - xa];
+    return make_float4((p.x + w.x * x) + e.x, (p.y + w.y * x) + e.y, (p.z + w.z * x) + e.z, (p.w + w.w * x) + e.w);
+  }
+};
+// conv2's A element: LayerNorm_1(R1[src]) (statistics of the window rows in LDS), zero outside.
+template <int F>
+struct AConv2 {
+  __amdgpu_buffer_rsrc_t r1;
+  const float *st, *g, *b;
+  int m, lm, L, xa, q;
+  bool live;
+  __device__ bool valid(int kb, int& src, int& ch) const {
+    const int k0 = 16 * kb + 4 * q, tap = k0 / F, l = lm + tap - 1;
+    ch = k0 - tap * F;
+    src = m + tap - 1;
+    return live && l >= 0 && l < L;
+  }
+  __device__ float4 raw(int kb) const {
+    int src, ch;
+    return valid(kb, src, ch) ? ld16_sc1(r1, (unsigned)((src * F + ch) * 4)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __device__ float4 fin(int kb, float4 v) const {
+    int src, ch;
+    if (!valid(kb, src, ch)) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const int i = src - xa;
+    const float mean = st[2 * i], rstd = st[2 * i + 1];
+    const float4 gg = *reinterpret_cast<const float4*>(g + ch);
+    const float4 bb = *reinterpret_cast<const float4*>(b + ch);
+    return make_float4(((v.x - mean) * rstd) * gg.x + bb.x, ((v.y - mean) * rstd) * gg.y + bb.y,
+                       ((v.z - mean) * rstd) * gg.z + bb.z, ((v.w - mean) * rstd) * gg.w + bb.w);
+  }
+};
+
+// One-tile row groups (B * L <= 80): the window's A rows are staged in LDS by coalesced 16-B loads (a wave
+// instruction = 1 KB of consecutive rows) instead of each lane gathering 16 rows x 64 B per instruction
+// straight from the hand-off buffer, and read back per block (rows padded by 16 B: conflict-free).
+// conv1: P rows (w0 x + temb added per block); conv2: LayerNorm_1(R1) rows (applied while staging).
+template <int D, int F>
+struct AConv1S {
+  const float *sa, *w0, *te, *xs;
+  int m, lm, L, xa, q;
+  bool live;
+  __device__ bool valid(int kb, int& src, int& ch) const {
+    const int k0 = 16 * kb + 4 * q, tap = k0 / D, l = lm + tap - 1;
+    ch = k0 - tap * D;
+    src = m + tap - 1;
+    return live && l >= 0 && l < L;
+  }
+  __device__ float4 raw(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ float4 fin(int kb, float4) const {
+    int src, ch;
+    if (!valid(kb, src, ch)) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 p = *reinterpret_cast<const float4*>(sa + (src - xa) * (F + 4) + ch);
+    const float4 w = *reinterpret_cast<const float4*>(w0 + ch);
+    const float4 e = *reinterpret_cast<const float4*>(te + ch);
+    const float x = xs[src - xa];
+    return make_float4((p.x + w.x * x) + e.x, (p.y + w.y * x) + e.y, (p.z + w.z * x) + e.z, (p.w + w.w * x) + e.w);
+  }
+};
+template <int F>
+struct AConv2S {
+  const float* sa;
+  int m, lm, L, xa, q;
+  bool live;
+  __device__ float4 raw(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ float4 fin(int kb, float4) const {
+    const int k0 = 16 * kb + 4 * q, tap = k0 / F, l = lm + tap - 1, ch = k0 - tap * F;
+    if (!(live && l >= 0 && l < L)) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(sa + (m + tap - 1 - xa) * (F + 4) + ch);
+  }
+};
+
 template <int D, int F>
 __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   using LY = Lds<D, F>;
   constexpr int K1 = LY::K1, K2 = LY::K2, CS = LY::CS, NB1 = K1 / 16, NB2 = K2 / 16;
-  static_assert(NB1 % 36 == 0 && NB2 % 36 == 0, "K blocks split 1 / 2 / 4 ways in batches of 9");
+  static_assert(NB1 % 36 == 0 && NB2 % 36 == 0, "K blocks split 1 / 2 / 4 ways");
   static_assert(CS < 32 && CS % 2 == 0, "head constants, paired LN1 partial loads");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* W1 = reinterpret_cast<float*>(smem + LY::W1);
@@ -115,6 +215,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   float* st = reinterpret_cast<float*>(smem + LY::ST);   // LN1 (mean, rstd) of the same rows
   float* gs = reinterpret_cast<float*>(smem + LY::GS);   // G_s of the CS slices, [CS] = sum b2 lw
   float4* red = reinterpret_cast<float4*>(smem + LY::RED);
+  float* sa = reinterpret_cast<float*>(smem + LY::SA);  // staged A window (one-tile groups)
   int* flag = reinterpret_cast<int*>(smem + LY::FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -173,11 +274,15 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
 
   // one conv: every wave's K part of its tile(s), the K parts summed through LDS in part order, then the
   // epilogue by the part-0 waves
-  auto conv = [&](const float* W, int K, int NB, auto af, auto epi) {
+  auto conv = [&](const float* W, int K, auto nbtag, auto af, auto afs, auto epi) {
+    constexpr int NB = decltype(nbtag)::value;
+    constexpr int B4 = NB / 4 < 18 ? NB / 4 : 18, B2 = NB / 2 < 18 ? NB / 2 : 18, B1 = NB < 18 ? NB : 18;
+    static_assert((NB / 4) % B4 == 0 && (NB / 2) % B2 == 0 && NB % B1 == 0, "K blocks per wave");
     if (KS > 1) {
       const int t = wave / KS;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      kloop(acc, W, K, part * NB / KS, (part + 1) * NB / KS, c, q, af(t));
+      if (KS == 4) kloop<B4>(acc, W, K, part * NB / 4, (part + 1) * NB / 4, c, q, afs(t));
+      else kloop<B2>(acc, W, K, part * NB / 2, (part + 1) * NB / 2, c, q, af(t));
       red[wave * 64 + lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
       __syncthreads();
       if (part == 0) {
@@ -190,7 +295,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
     } else {
       for (int t = wave; t < nt; t += 4) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        kloop(acc, W, K, 0, NB, c, q, af(t));
+        kloop<B1>(acc, W, K, 0, NB, c, q, af(t));
         epi(t, acc);
       }
     }
@@ -201,31 +306,26 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
     int pst_k = 0;
 #endif
     for (int i = tid; i < D; i += kThreads) vte[i] = N.temb[(size_t)s * D + i];
+    if (nt == 1)  // conv1's P window rows (constant, but the staging area is shared with conv2's rows)
+      for (int i = tid; i < nw * (D / 4); i += kThreads) {
+        const int row = i / (D / 4), c4 = i - row * (D / 4), rr = xa + row;
+        *reinterpret_cast<float4*>(sa + row * (F + 4) + 4 * c4) =
+            (rr >= 0 && rr < M) ? ld4(N.P + (size_t)rr * D + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     __syncthreads();
     PVST();
 
     // ---- conv1 (pva.py:221-230: proj(cat(x_t, enc)) + temb -> Conv k3 -> ReLU) + LN1 partials
-    conv(W1, K1, NB1,
+    conv(W1, K1, std::integral_constant<int, NB1>{},
          [&](int t) {
            const int m = r0 + 16 * t + c;
            const bool live = m < r0 + nr;
-           const int lm = live ? m % L : 0;
-           return [=](int kb) -> float4 {
-             const int k0 = 16 * kb + 4 * q, tap = k0 / D, ch = k0 - tap * D, l = lm + tap - 1;
-             float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-             if (live && l >= 0 && l < L) {
-               const int src = m + tap - 1;
-               const float4 p = ld4(N.P + (size_t)src * D + ch);
-               const float4 w = *reinterpret_cast<const float4*>(vw0 + ch);
-               const float4 e = *reinterpret_cast<const float4*>(vte + ch);
-               const float x = xs[src - xa];
-               r.x = (p.x + w.x * x) + e.x;
-               r.y = (p.y + w.y * x) + e.y;
-               r.z = (p.z + w.z * x) + e.z;
-               r.w = (p.w + w.w * x) + e.w;
-             }
-             return r;
-           };
+           return AConv1<D>{N.P, vw0, vte, xs, m, live ? m % L : 0, L, xa, q, live};
+         },
+         [&](int t) {
+           const int m = r0 + 16 * t + c;
+           const bool live = m < r0 + nr;
+           return AConv1S<D, F>{sa, vw0, vte, xs, m, live ? m % L : 0, L, xa, q, live};
          },
          [&](int t, const f32x4& acc) {
 #pragma unroll
@@ -273,30 +373,35 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
       st[2 * tid + 1] = rstd;
     }
     __syncthreads();
+    if (nt == 1) {  // conv2's window rows, LayerNorm_1 applied (Layers: Conv -> ReLU -> LN -> Conv)
+      for (int i = tid; i < nw * (F / 4); i += kThreads) {
+        const int row = i / (F / 4), c4 = i - row * (F / 4), rr = xa + row;
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rr >= 0 && rr < M) {
+          const float4 v = ld16_sc1(rR1, (unsigned)((rr * F + 4 * c4) * 4));
+          const float mean = st[2 * row], rstd = st[2 * row + 1];
+          const float4 g = *reinterpret_cast<const float4*>(vg1 + 4 * c4);
+          const float4 b = *reinterpret_cast<const float4*>(vb1 + 4 * c4);
+          o = make_float4(((v.x - mean) * rstd) * g.x + b.x, ((v.y - mean) * rstd) * g.y + b.y,
+                          ((v.z - mean) * rstd) * g.z + b.z, ((v.w - mean) * rstd) * g.w + b.w);
+        }
+        *reinterpret_cast<float4*>(sa + row * (F + 4) + 4 * c4) = o;
+      }
+      __syncthreads();
+    }
     PVST();
 
     // ---- conv2 (Conv k3 over LN1 -> ReLU) + head partials over the slice
-    conv(W2, K2, NB2,
+    conv(W2, K2, std::integral_constant<int, NB2>{},
          [&](int t) {
            const int m = r0 + 16 * t + c;
            const bool live = m < r0 + nr;
-           const int lm = live ? m % L : 0;
-           return [=](int kb) -> float4 {
-             const int k0 = 16 * kb + 4 * q, tap = k0 / F, ch = k0 - tap * F, l = lm + tap - 1;
-             float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-             if (live && l >= 0 && l < L) {
-               const int src = m + tap - 1, i = src - xa;
-               const float4 v = ld16_sc1(rR1, (unsigned)((src * F + ch) * 4));
-               const float mean = st[2 * i], rstd = st[2 * i + 1];
-               const float4 g = *reinterpret_cast<const float4*>(vg1 + ch);
-               const float4 b = *reinterpret_cast<const float4*>(vb1 + ch);
-               r.x = ((v.x - mean) * rstd) * g.x + b.x;
-               r.y = ((v.y - mean) * rstd) * g.y + b.y;
-               r.z = ((v.z - mean) * rstd) * g.z + b.z;
-               r.w = ((v.w - mean) * rstd) * g.w + b.w;
-             }
-             return r;
-           };
+           return AConv2<F>{rR1, st, vg1, vb1, m, live ? m % L : 0, L, xa, q, live};
+         },
+         [&](int t) {
+           const int m = r0 + 16 * t + c;
+           const bool live = m < r0 + nr;
+           return AConv2S<F>{sa, m, live ? m % L : 0, L, xa, q, live};
          },
          [&](int t, const f32x4& acc) {
 #pragma unroll

@@ -62,7 +62,8 @@ struct Lds {
   static constexpr int K1 = 3 * D, K2 = 3 * F, CS = F / kCols, XR = kMaxRowsWG + 4;
   static constexpr int W1 = 0, W2 = W1 + kCols * K1 * 4, W0 = W2 + kCols * K2 * 4, G1 = W0 + D * 4, B1 = G1 + F * 4,
                        TE = B1 + F * 4, XS = TE + D * 4, ST = XS + XR * 4, GS = ST + 2 * XR * 4, RED = GS + 32 * 4,
-                       FLAG = RED + 4 * 64 * 16, BYTES = FLAG + 16;
+                       FLAG = RED + 4 * 64 * 16, SA = FLAG + 16, SAS = F + 4 /* staged row stride (floats) */,
+                       BYTES = SA + 18 * SAS * 4;  // one-tile groups: the conv A window (18 rows) staged in LDS
   static_assert(K1 % 64 == 0 && K2 % 64 == 0 && D % 16 == 0 && F % kCols == 0, "pva persist dims");
   static_assert(RED % 16 == 0 && BYTES <= 160 * 1024, "pva persist LDS");
 };

@@ -204,6 +204,191 @@ __global__ __launch_bounds__(512) void attn_kernel(const float* __restrict__ QKV
   }
 }
 
+// The same attention on the fp32 matrix cores (v_mfma_f32_16x16x4_f32).  Per workgroup 64 queries of one
+// (utterance, head); 8 waves = 2 key groups x 4 query waves: wave (g, w) owns queries [16 w, 16 w + 16)
+// and the 64-key chunks c = g (mod 2).  Transposed products keep every operand where the next MFMA wants
+// it without a shuffle: S^T (keys x queries) = K . Q^T leaves lane (c, r) holding P^T[key 4 r + i][query c],
+// which is exactly that lane's B operand of O^T (dims x queries) = V^T . P^T when the MFMA's four K slots
+// are mapped to keys {4 r + i} (the same permutation on V^T's A operand, read from a transposed V chunk).
+// Online softmax per query column (max / sum over the 4 lanes of a column by two xor shuffles), the two
+// key groups merged through LDS at the end.  Chunks are staged K row-major and V transposed, rows padded
+// by 16 B, the next chunk's global loads in registers while the current one is computed.
+template <int DK>
+struct AttnM {
+  static constexpr int KC = 64, KS = DK + 4, VS = KC + 4;         // padded LDS row strides (floats)
+  static constexpr int BUF = KC * KS + DK * VS;                   // K chunk + V^T chunk
+  static constexpr int V4 = KC * DK / 4;                          // float4s per operand chunk
+  static constexpr int PT = (2 * V4 + 255) / 256;                 // float4s per thread (a group's 256 threads)
+  static constexpr size_t lds() { return (size_t)4 * BUF * 4 + 4 * KC + (size_t)4 * 64 * (2 + 4 * (DK / 16)) * 4; }
+};
+template <int DK>
+__global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict__ QKV, const uint8_t* __restrict__ kmask,
+                                                        int n, int D, float temp, float* __restrict__ O) {
+  using A = AttnM<DK>;
+  constexpr int KC = A::KC, NT = KC / 16, SB = DK / 16, DT = DK / 16, PT = A::PT;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  // buffers: [group][2] x (K [KC][KS], V^T [DK][VS]); masks [group][2][KC] bytes; merge area after
+  uint8_t* msk = reinterpret_cast<uint8_t*>(sm + 4 * A::BUF);
+  float* mrg = reinterpret_cast<float*>(msk + 4 * KC);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), grp = w >> 2, wq = w & 3, gt = tid & 255;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int c = lane & 15, r = lane >> 4;
+  const int ld = 3 * D;
+  const float* base = QKV + (size_t)b * n * ld;
+  const int qi = blockIdx.x * 64 + wq * 16 + c;  // this lane's query (column of every MFMA tile)
+  float4 qr[SB];
+  {
+    const float* qp = base + (size_t)(qi < n ? qi : n - 1) * ld + h * DK;
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) qr[sb] = ld4(qp + 16 * sb + 4 * r);
+  }
+  float4 pf[PT];
+  uint8_t pm = 1;
+  auto fetch = [&](int k0) {  // this group's next chunk into registers
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = gt + j * 256;
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < 2 * A::V4) {
+        const int op = i / A::V4, rr = i - op * A::V4;
+        const int key = rr / (DK / 4), cc = (rr - key * (DK / 4)) * 4;
+        if (k0 + key < n) t = ld4(base + (size_t)(k0 + key) * ld + (op + 1) * D + h * DK + cc);
+      }
+      pf[j] = t;
+    }
+    if (gt < KC) {
+      const int kk = k0 + gt;
+      pm = kk < n ? (kmask ? kmask[(size_t)b * n + kk] : 0) : 1;
+    }
+  };
+  auto stash = [&](int buf) {  // registers -> this group's LDS buffer (K row-major, V transposed)
+    float* Kb = sm + (grp * 2 + buf) * A::BUF;
+    float* Vt = Kb + KC * A::KS;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = gt + j * 256;
+      if (i < 2 * A::V4) {
+        const int op = i / A::V4, rr = i - op * A::V4;
+        const int key = rr / (DK / 4), cc = (rr - key * (DK / 4)) * 4;
+        if (op == 0) {
+          *reinterpret_cast<float4*>(Kb + key * A::KS + cc) = pf[j];
+        } else {
+          Vt[(cc + 0) * A::VS + key] = pf[j].x;
+          Vt[(cc + 1) * A::VS + key] = pf[j].y;
+          Vt[(cc + 2) * A::VS + key] = pf[j].z;
+          Vt[(cc + 3) * A::VS + key] = pf[j].w;
+        }
+      }
+    }
+    if (gt < KC) msk[(grp * 2 + buf) * KC + gt] = pm;
+  };
+
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = (n + KC - 1) / KC, iters = (nch + 1) / 2;
+  fetch(grp * KC);
+  stash(0);
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    const int buf = it & 1, ch = 2 * it + grp;
+    if (it + 1 < iters) fetch((ch + 2) * KC);  // in flight during this chunk's math
+    const float* Kb = sm + (grp * 2 + buf) * A::BUF;
+    const float* Vt = Kb + KC * A::KS;
+    const uint8_t* mk = msk + (grp * 2 + buf) * KC;
+    if (ch < nch) {
+      f32x4 s[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+          const float4 kf = *reinterpret_cast<const float4*>(Kb + (16 * t + c) * A::KS + 16 * sb + 4 * r);
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf.x, qr[sb].x, s[t], 0, 0, 0);
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf.y, qr[sb].y, s[t], 0, 0, 0);
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf.z, qr[sb].z, s[t], 0, 0, 0);
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf.w, qr[sb].w, s[t], 0, 0, 0);
+        }
+      }
+      // S^T lane (c, r): keys 16 t + 4 r + i of query c; scale, mask, chunk max over the query's 64 keys
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = mk[16 * t + 4 * r + i] ? -INFINITY : s[t][i] / temp;
+          s[t][i] = v;
+          cmax = fmaxf(cmax, v);
+        }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+      const float nm = fmaxf(m, cmax);
+      float rs = 0.f;
+      if (nm != -INFINITY) {  // (per query: a column whose keys so far are all padding keeps m = -inf)
+        const float sc = __expf(m - nm);  // m = -inf: 0
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __expf(s[t][i] - nm);
+            s[t][i] = p;
+            rs += p;
+          }
+        l *= sc;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= sc;
+        m = nm;
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      l += rs;
+      // O^T += V^T . P^T: MFMA (t, i) maps K slot r to key 16 t + 4 r + i on both operands
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float4 vf = *reinterpret_cast<const float4*>(Vt + (16 * dt + c) * A::VS + 16 * t + 4 * r);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf.x, s[t][0], o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf.y, s[t][1], o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf.z, s[t][2], o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf.w, s[t][3], o[dt], 0, 0, 0);
+        }
+    }
+    if (it + 1 < iters) stash(buf ^ 1);  // that buffer's last readers finished before the previous barrier
+    __syncthreads();
+  }
+  // merge the two key groups: group 1 leaves (m, l, o) per lane, group 0 combines and writes
+  float* mw = mrg + (wq * 64 + lane) * (2 + 4 * DT);
+  if (grp == 1) {
+    mw[0] = m;
+    mw[1] = l;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mw[2 + 4 * dt + i] = o[dt][i];
+  }
+  __syncthreads();
+  if (grp == 1) return;
+  const float m1 = mw[0], l1 = mw[1];
+  const float M = fmaxf(m, m1);
+  const float f0 = __expf(m - M), f1 = __expf(m1 - M);  // all keys padded: M = -inf -> NaN, as the reference's softmax
+  const float L = l * f0 + l1 * f1;
+  if (qi >= n) return;
+  float* op = O + ((size_t)b * n + qi) * D + h * DK;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (o[dt][i] * f0 + mw[2 + 4 * dt + i] * f1) / L;
+    *reinterpret_cast<float4*>(op + 16 * dt + 4 * r) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // ------------------------------------------------------------------ epilogues
 
 // (acc + bias) + residual  (fc(out) + residual, SubLayers.py:54-55; w_2(...) + residual, :91-93)
@@ -250,6 +435,14 @@ static int ln_mask(int D, const float* R, const float* g, const float* b, const 
 }
 template <int DK>
 static int launch_attn(const float* QKV, const uint8_t* mask, int B, int n, int D, int H, float temp, float* O, hipStream_t st) {
+  if (tn().attn_mfma) {
+    const size_t lds = AttnM<DK>::lds();
+    auto kern = attn_mfma_kernel<DK>;
+    if (lds > 64 * 1024) FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
+    hipLaunchKernelGGL(kern, dim3((n + 63) / 64, H, B), dim3(512), lds, st, QKV, mask, n, D, temp, O);
+    FL_LAUNCH_CHECK();
+    return kOk;
+  }
   const size_t lds = attn_lds_bytes(DK);
   auto kern = attn_kernel<DK>;
   if (lds > 64 * 1024) FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));

@@ -81,6 +81,7 @@ SIGNATURES = {
     "flamed_prior_workspace_size": (c_size_t, [P, c_int, c_int, c_int, c_int]),
     "flamed_prior_encode": (c_int, [P, P, P, c_int, c_int, P, P, P, c_size_t, c_int, P]),
     "flamed_prior_decode": (c_int, [P, P, P, P, c_int, c_int, c_int, P, P, P, P, c_size_t, c_int, P]),
+    "flamed_prior_set_dtype": (c_int, [P, c_int]),
 }
 
 # include/flamed_diag.h: probes in libflamed_diag.so, phase stamps in libflamed_hip_stamps.so (tools only)

@@ -56,6 +56,9 @@ class PriorGenerator(nn.Module):
         self.prior_decoder = nn.ModuleList([Decoder(config, tc["decoder_layers"][i]) for i in range(nq)])
         self.head = nn.Linear(tc["decoder_hidden"], vocab + 1)
         self.hip_graph = True
+        # decoder-side GEMM operands on the HIP path: "bf16" (fp32 accumulation; the encoder, which feeds the
+        # rounded durations, always stays fp32) or "f32" (exact, the reference's arithmetic)
+        self.hip_dec_dtype = "bf16"
         self._hip = None
 
     # -- HIP dispatch (inference on ROCm tensors)
@@ -249,6 +252,10 @@ class PriorHIP:
         if P:
             bufs["prompts"].copy_(prompts)
         L = nat.lib()
+        if pg.hip_dec_dtype not in ("bf16", "f32"):
+            raise ValueError(f"PriorGenerator.hip_dec_dtype must be 'bf16' or 'f32' (got {pg.hip_dec_dtype!r})")
+        nat.check(L.flamed_prior_set_dtype(self.handle, nat.FLAMED_BF16 if pg.hip_dec_dtype == "bf16" else nat.FLAMED_F32),
+                  "flamed_prior_set_dtype")
         ws = self.ws.get(L.flamed_prior_workspace_size(self.handle, B, 0, T, P), dev)
         nat.check(L.flamed_prior_decode(self.handle, nat.ptr(bufs["x"]), nat.ptr(bufs["mask"]), nat.ptr(bufs["prompts"]),
                                         B, T, P, nat.ptr(bufs["pos"]), nat.ptr(bufs["embs"]), nat.ptr(bufs["logits"]),

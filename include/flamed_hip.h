@@ -170,6 +170,8 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     no faster): one K chain;
  *   "pva_persist"   — 1 (default): the PVA flow of both nets runs as one persistent launch when it
  *                     fits (see flamed_pva_flow); 0: hipGraph of launches;
+ *   "attn_mfma"     — 1 (default): transformer attention (prior stack, timbre encoder) on fp32 MFMA;
+ *                     0: the LDS-broadcast FMA kernel;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     FLAMED_DEN_KERNEL_CLASSES) twice per Euler step; -1 (default) = off.
@@ -324,6 +326,10 @@ FLAMED_API int flamed_prior_encode(flamed_prior_t h, const int64_t* texts, const
 FLAMED_API int flamed_prior_decode(flamed_prior_t h, const float* x, const uint8_t* tgt_mask, const int64_t* prompts,
                                    int B, int T, int P, const float* pos, float* embs, float* logits, void* ws,
                                    size_t ws_bytes, int use_graph, hipStream_t stream);
+/* Operand type of the decoder-side GEMMs (bridge, shared decoder, per-quantizer decoders, head):
+ * FLAMED_F32 (default: exact fp32 MFMA) or FLAMED_BF16 (bf16 operands, fp32 accumulation; the weights
+ * are converted once on the first bf16 decode).  The encoder always runs fp32 (it feeds the durations). */
+FLAMED_API int flamed_prior_set_dtype(flamed_prior_t h, int dtype);
 
 /* ============== prompt-side quantizers + timbre encoder (once per prompt) ==============
  * Replaces FACodecDecoder.forward(vq=True) (facodec.py:470-533) after the encoder

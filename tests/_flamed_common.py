@@ -17,6 +17,7 @@ def build_flamed(device="cpu", dtype="f32"):
     dec = FACodecDecoder(in_channels=256, upsample_initial_channel=1024, up_ratios=[5, 5, 4, 2], vq_dim=256).eval()
     dec.load_state_dict(seeded("facodec_decoder"))
     m.prob_generator.denoiser.hip_dtype = dtype
+    m.prior_generator.hip_dec_dtype = dtype  # decoder-side prior GEMMs (the prior encoder is always fp32)
     dec.hip_dtype = dtype
     return m.to(device), dec.to(device)
 

@@ -1,7 +1,9 @@
 """GPU end to end: Flamed.sample_batch with every hot-path piece on the HIP library (PVA flow +
 length regulator, AdaLN + Euler solve, FaCodec decode) vs the reference's fixture.
-Tolerances: f32 mode tgt_mask bit-exact, latents rel-L2 <= 1e-4, waveform rel-L2 <= 2e-3 (chaotic
-random-weight decoder amplifies fp32 reassociation noise); bf16 mode tgt_mask exact, latents <= 2e-2."""
+Tolerances: f32 mode tgt_mask bit-exact, prior embeddings and latents rel-L2 <= 1e-4, waveform rel-L2
+<= 2e-3 (chaotic random-weight decoder amplifies fp32 reassociation noise); bf16 mode (bf16 denoiser,
+decoder-side prior GEMMs and FaCodec convs) tgt_mask exact (the prior encoder and the duration flow stay
+fp32), prior embeddings <= 2e-2, latents <= 2e-2."""
 import numpy as np
 import pytest
 import torch
@@ -13,8 +15,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-@pytest.mark.parametrize("dtype,lat_tol", [("f32", 1e-4), ("bf16", 2e-2)])
-def test_sample_batch_gpu(dtype, lat_tol):
+@pytest.mark.parametrize("dtype,lat_tol,emb_tol", [("f32", 1e-4, 1e-4), ("bf16", 2e-2, 2e-2)])
+def test_sample_batch_gpu(dtype, lat_tol, emb_tol):
     m, dec = build_flamed(DEV, dtype)
     g = golden("flamed_sample")
     with torch.inference_mode():
@@ -23,7 +25,9 @@ def test_sample_batch_gpu(dtype, lat_tol):
                              timbres=t32(g["timbres"]), codec_decoder=dec, temp_durgen=0.3, temp_denoiser=0.3,
                              nsteps_durgen=4, nsteps_denoiser=4)
     assert np.array_equal(out["tgt_mask"].cpu().numpy(), g["sb_tgt_mask"])
-    assert rel_l2(out["prior_embs"].cpu(), g["sb_prior_embs"]) < 1e-4
+    e = rel_l2(out["prior_embs"].cpu(), g["sb_prior_embs"])
+    print(f"{dtype}: prior_embs rel-L2 {e:.3e}")
+    assert e < emb_tol
     assert rel_l2(out["latents"].cpu(), g["sb_latents"]) < lat_tol
     assert out["wav"].shape == g["sb_wav"].shape
     if dtype == "f32":

@@ -107,3 +107,62 @@ def test_graph_equals_eager(model):
         assert torch.equal(a, b)
     for a, b in zip(outs[0], outs[2]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,T,P,tl", [(1, 400, 240, [400]), (3, 37, 0, [37, 5, 30])])
+def test_decode_bf16_vs_oracle(model, B, T, P, tl):
+    """Decoder-side GEMMs on bf16 operands (PriorGenerator.hip_dec_dtype = "bf16", the package default; fp32
+    accumulation, LayerNorm / softmax / residuals fp32) against the fp32 oracle: embeddings rel-L2 <= 1e-2
+    and logits rel-L2 <= 1e-2 after 22 FFT blocks (measured 5.0-5.7e-3); the masked-logit zeros stay exact.  The fp32 handle is
+    restored after (the module fixture runs the exact path)."""
+    pg, sd = model
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, T, 192, generator=g)
+    tgt = torch.tensor(tl)
+    prompts = torch.randint(0, 1025, (B, 6, P), generator=g)
+    mask = orc.mask_from_lengths(tgt, T)
+    x = x.masked_fill(mask.unsqueeze(-1), 0)
+    try:
+        pg.hip_dec_dtype = "bf16"
+        with torch.inference_mode():
+            pe, pl = pg.hip().decode(x.to(DEV), mask.to(DEV), prompts.to(DEV), P)
+    finally:
+        pg.hip_dec_dtype = "f32"
+    with torch.inference_mode():
+        re, rl, _ = orc.prior_decode(sd, x, tgt, prompts)
+        pe32, _ = pg.hip().decode(x.to(DEV), mask.to(DEV), prompts.to(DEV), P)
+    pe, pl = pe.cpu(), pl.cpu()
+    ee, el = rel_l2(pe, re), rel_l2(pl, rl)
+    print(f"bf16 decoders B={B} T={T} P={P}: embs rel-L2 {ee:.3e}, logits rel-L2 {el:.3e}")
+    assert ee < 1e-2 and el < 1e-2  # measured 5.0-5.7e-3
+    assert torch.all(pl.permute(0, 2, 3, 1)[mask.unsqueeze(1).expand(-1, 6, -1)] == 0)
+    assert rel_l2(pe32.cpu(), re) < 1e-4  # switching back re-runs the exact path
+
+
+def test_attention_mfma_matches_fma_kernel(model):
+    """The fp32-MFMA attention (flamed_tune attn_mfma = 1, default; xfmr.hpp attn_mfma_kernel) against the
+    LDS-broadcast FMA kernel (attn_mfma = 0) on the encoder (48-wide heads, key-padding mask) and the
+    decoders (32-wide heads, prompt-prefixed masks): both exact fp32, so they agree to summation order
+    (rel-L2 <= 1e-5)."""
+    from flamed import _native as nat
+    pg, _ = model
+    g = torch.Generator().manual_seed(9)
+    B, T, P = 2, 150, 70
+    x = torch.randn(B, T, 192, generator=g).to(DEV)
+    mask = orc.mask_from_lengths(torch.tensor([150, 97]), T).to(DEV)
+    prompts = torch.randint(0, 1025, (B, 6, P), generator=g).to(DEV)
+    ids = _ids(B, 131, 6).to(DEV)
+    smask = orc.mask_from_lengths(torch.tensor([131, 64]), 131).to(DEV)
+    outs = []
+    L = nat.lib()
+    try:
+        for v in (1, 0):
+            nat.check(L.flamed_tune(b"attn_mfma", v), "flamed_tune")
+            with torch.inference_mode():
+                outs.append((pg.hip().encode(ids, smask), *pg.hip().decode(x, mask, prompts, P)))
+    finally:
+        nat.check(L.flamed_tune(b"attn_mfma", 1), "flamed_tune")
+    for a, b in zip(outs[0], outs[1]):
+        valid = torch.isfinite(b)
+        assert torch.equal(torch.isfinite(a), valid)
+        assert rel_l2(a[valid].cpu(), b[valid].cpu()) < 1e-5
