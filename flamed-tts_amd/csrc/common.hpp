@@ -125,8 +125,9 @@ struct Tune {
   int dwgn_small = 1;      // small-M bf16 path: one-workgroup-per-8-channels depthwise conv + GroupNorm (T <= 576)
   int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in
   int persist = 1;         // B = 1 bf16 solves: one persistent launch for all steps (persist.hpp)
-  int persist_opt = 73;    // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
-                           // 64 = fragment-major GEMM A images (measured: 26.4 -> 22.8 ms per B = 1 T = 400 solve)
+  int persist_opt = 585;   // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
+                           // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
+                           // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms)
   int pva_split = 0;       // PVA nets: split-K of their small-M fp32 GEMMs (fixed slice order); measured
                            // neutral (L = 60 / 247, 64 steps: 2.70 / 2.94 vs 2.61 / 2.92 ms), so off
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)

@@ -2218,6 +2218,7 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, i
   const size_t xbytes = (size_t)T * pk::kC * 4;
   FL_HIP(hipMemcpyAsync(backup, xt, xbytes, hipMemcpyDeviceToDevice, st));
   FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pk::kCtrInts, st));
+  if (P.opt & 512) FL_HIP(hipMemsetAsync(P.gnp, 0, (size_t)pk::kGroups * pk::kH * 16, st));  // granule tags
   if (!d->pev[0]) FL_HIP(hipEventCreate(&d->pev[0]));
   if (!d->pev[1]) FL_HIP(hipEventCreate(&d->pev[1]));
   FL_HIP(hipEventRecord(d->pev[0], st));

@@ -373,6 +373,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   }
   const bool xloc = xcc_id && !(P.opt & 8);  // group-local payloads may stay in the XCD's L2
   const bool frag = (P.opt & 64) != 0;        // fragment-major GEMM A images (a2, u, xa, xs)
+  const bool gran = (P.opt & 512) != 0;       // GroupNorm partials as tagged granules (gnp zeroed per launch)
   int r0, nr;
   group_rows(g, T, r0, nr, P.opt);
   const int c = lane & 15, q = lane >> 4;
@@ -612,11 +613,18 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           float m2t = 0.f;
 #pragma unroll
           for (int k = 0; k < 8; ++k) m2t += red[k * kCols + cc];
-          const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
-          st16(rq, (unsigned)((g * H + col0 + cc) * 16), __builtin_bit_cast(u32x4, make_float4((float)nr, mg, m2t, 0.f)));
+          if (gran) {  // (mean, M2) as two tagged granules: the data is the flag (no drain, no counter)
+            unsigned long long* gq = reinterpret_cast<unsigned long long*>(P.gnp) + ((size_t)g * H + col0 + cc) * 2;
+            const unsigned long long tag = (unsigned long long)(ndg + 1) << 32;
+            __hip_atomic_store(gq, tag | __float_as_uint(mg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gq + 1, tag | __float_as_uint(m2t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
+            st16(rq, (unsigned)((g * H + col0 + cc) * 16), __builtin_bit_cast(u32x4, make_float4((float)nr, mg, m2t, 0.f)));
+          }
         }
       }
-      signal(gnc);
+      if (!gran) signal(gnc);
       PST(step);
       ++ndg;
       float gwv = 0.f, gbv = 0.f;
@@ -625,6 +633,56 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         gbv = bw.gnb[col0 + tid];
       }
       PST(step);
+      if (gran) {
+        // wave 0: lane cc < 32 re-reads the 8 groups' granules of channel col0 + cc until every tag is this
+        // hand-off's, then Chan-combines them in group order (group k's row count from group_rows)
+        bool ok = true;
+        if (tid < 64) {
+          const unsigned long long* gq = reinterpret_cast<const unsigned long long*>(P.gnp) + (size_t)(col0 + (tid & 31)) * 2;
+          float mv[kGroups], qv[kGroups];
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          for (unsigned it = 0;; ++it) {
+            bool mine = true;
+            if (tid < kCols) {
+#pragma unroll
+              for (int k = 0; k < kGroups; ++k) {
+                const unsigned long long a = __hip_atomic_load(gq + (size_t)k * H * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long b = __hip_atomic_load(gq + (size_t)k * H * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                mine = mine && (unsigned)(a >> 32) == (unsigned)ndg && (unsigned)(b >> 32) == (unsigned)ndg;
+                mv[k] = __uint_as_float((unsigned)a);
+                qv[k] = __uint_as_float((unsigned)b);
+              }
+            }
+            if (__all(mine)) break;
+            if ((it & 31) == 31) {
+              if (__hip_atomic_load(errw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
+              if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
+                if (tid == 0) __hip_atomic_store(errw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+              }
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (tid == 0) *flag = ok ? 1 : 0;
+          if (ok && tid < kCols) {
+            float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < kGroups; ++k) {
+              int ka, kn;
+              group_rows(k, T, ka, kn, P.opt);
+              chan_combine(n, mean, m2, (float)kn, kn > 0 ? mv[k] : 0.f, kn > 0 ? qv[k] : 0.f);
+            }
+            const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
+            gnv[tid] = make_float4(mean, sc, gbv, 0.f);
+          }
+        }
+        __syncthreads();
+        const bool okw = *flag != 0;
+        __syncthreads();
+        if (!okw) return;
+        PST(step);
+      } else {
       if (!wait_ge(errw, tmo, gnc, 0, 1, kGroups * ndg, flag)) return;
       PST(step);
       if (tid < kCols) {  // the 8 groups' partials of this channel, Chan-combined in group order
@@ -637,6 +695,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         }
         const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
         gnv[tid] = make_float4(mean, sc, gbv, 0.f);
+      }
       }
       __syncthreads();
       {

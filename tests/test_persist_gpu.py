@@ -134,15 +134,19 @@ def test_persist_knob_off_uses_launch_path(pgb):
 
 
 @pytest.mark.parametrize("T", [400, 131, 16])
-def test_persist_fragment_layout_bitwise(pgb, T):
-    """The fragment-major A images (persist_opt 64, default 73) only change where the bf16 operands sit in
-    memory, not any arithmetic: the solve equals the row-major hand-off variant (opt 9) bitwise, for full,
-    partial-tile and nearly-empty row groups (rows past a group's end are stored as zeros)."""
+@pytest.mark.parametrize("opt", [9, 73])
+def test_persist_variants_bitwise(pgb, T, opt):
+    """Hand-off variants change where and how data moves, never the arithmetic: the default (persist_opt 585:
+    fragment-major A images + tagged-granule GroupNorm exchange) equals the row-major, counter-based variant
+    (opt 9) and the counter-based GroupNorm exchange (opt 73) bitwise, for full, partial-tile and nearly-empty
+    row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
     pg, _ = pgb
     x0, spk = _inputs(11, 1, T)
+    from flamed import _native as nat
+    nat.check(nat.lib().flamed_tune(b"persist_opt", 585), "flamed_tune")
     r0 = _runs(pg)
     a = _solve(pg, x0, spk, 8)
-    with knob("persist_opt", 9, 73):
+    with knob("persist_opt", opt, 585):
         b = _solve(pg, x0, spk, 8)
     assert _runs(pg) == r0 + 2
     assert torch.equal(a, b)
