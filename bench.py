@@ -263,7 +263,8 @@ def secondary_measurements(dev, nfe):
         tmask = torch.zeros(1, Tp, dtype=torch.bool, device=dev)
         tl = torch.tensor([Tp], device=dev)
         pcodes = torch.randint(0, 1024, (1, 6, Pp), generator=g).to(dev)
-        row = {"phonemes": Lp, "frames": Tp, "prompt_frames": Pp, "dtype": "f32 (exact MFMA)"}
+        row = {"phonemes": Lp, "frames": Tp, "prompt_frames": Pp,
+               "dtype": f"encoder f32 (exact MFMA), decoders {pr.hip_dec_dtype} GEMMs (fp32 accumulation), fp32-MFMA attention"}
         row["encode_ms"] = round(_time_ms(lambda: pr.hip().encode(ids, smask), dev), 3)
         row["decode_ms"] = round(_time_ms(lambda: pr.hip().decode(xlr, tmask, pcodes, Pp), dev), 3)
         row["torch_encode_ms"] = round(_time_ms(lambda: pr.encoder(ids, smask), dev), 3)

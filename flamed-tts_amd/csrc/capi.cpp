@@ -89,6 +89,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"pva_persist", &Tune::pva_persist, 0, 1, nullptr},
       {"attn_mfma", &Tune::attn_mfma, 0, 1, nullptr},
+      {"prior_split", &Tune::prior_split, 0, 1, nullptr},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(k.name, key) != 0) continue;

@@ -132,6 +132,7 @@ struct Tune {
                            // neutral (L = 60 / 247, 64 steps: 2.70 / 2.94 vs 2.61 / 2.92 ms), so off
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)
   int attn_mfma = 1;       // transformer attention (prior stack, timbre encoder) on fp32 MFMA (xfmr.hpp)
+  int prior_split = 1;     // bf16 prior decoders: split-K of the GEMMs with small tile grids
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)
 Tune tune_snapshot(int* epoch);                       // process defaults + their epoch

@@ -160,6 +160,11 @@ struct Prior {
   int dec_dt = FLAMED_F32;  // decoder-side GEMM operands (flamed_prior_set_dtype)
   char* dev16 = nullptr;    // bf16 copies of the decoder-side GEMM weights (made on first bf16 decode)
   const bf16 *bridge_w16 = nullptr, *head_w16 = nullptr;
+  // bf16 decoders: split-K of the GEMMs whose tile grid leaves CUs idle (conv2 and fc: N = 384 at 640
+  // rows, 240 tiles of K = 1536 / 384), slices summed by the last arriver in a fixed order
+  SplitCtx split;
+  char* split_mem = nullptr;
+  static constexpr int kSplitTarget = 512, kSplitCounters = 2048;
 };
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -211,11 +216,17 @@ template <> struct LW<bf16> {
   static const bf16* c1(const FftLayer& l) { return l.w1_16; }
   static const bf16* c2(const FftLayer& l) { return l.w2_16; }
 };
-// fp32: the transformer stacks' config choice (xf_gemm); bf16: the shape-driven bf16 configs.
+// fp32: the transformer stacks' config choice (xf_gemm); bf16: the shape-driven bf16 configs, with the
+// same 32 x 32 tiles when 32 x 64 would leave CUs idle (N = 384 at 640 rows: 120 -> 240 workgroups).
 template <typename DT, class AL, class EP>
 static int pr_gemm(const AL& al, const DT* W, int ldw, const EP& ep, int M, int N, int K, hipStream_t st) {
-  if constexpr (std::is_same<DT, float>::value) return xf_gemm(al, W, ldw, ep, M, N, K, st);
-  else return launch_gemm<bf16>(al, W, ldw, ep, M, N, K, st);
+  if constexpr (std::is_same<DT, float>::value) {
+    return xf_gemm(al, W, ldw, ep, M, N, K, st);
+  } else {
+    if (M < 2048 && (size_t)(N / 64) * ((M + 31) / 32) < 256 && N % 32 == 0)
+      return launch_gemm_cfg<32, 32, 3, bf16>(al, W, ldw, ep, M, N, K, st);
+    return launch_gemm<bf16>(al, W, ldw, ep, M, N, K, st);
+  }
 }
 
 template <typename DT>
@@ -303,6 +314,17 @@ static int ensure_bf16(Prior* p, hipStream_t st) {
   stack(p->shared);
   for (FftStack& s : p->dec) stack(s);
   items.push_back({p->head_w, (size_t)p->head_n * D, &p->head_w16});
+  if (!p->split_mem) {  // slab: up to kSplitTarget workgroups of 32 x 64 fp32 tiles; zeroed tile counters
+    const size_t slab_floats = (size_t)Prior::kSplitTarget * 32 * 64;
+    FL_HIP(hipMalloc(&p->split_mem, 4 * slab_floats + 4 * Prior::kSplitCounters));
+    FL_HIP(hipMemsetAsync(p->split_mem + 4 * slab_floats, 0, 4 * Prior::kSplitCounters, st));
+    p->split.slab = reinterpret_cast<float*>(p->split_mem);
+    p->split.slab_floats = slab_floats;
+    p->split.cnt = reinterpret_cast<int*>(p->split_mem + 4 * slab_floats);
+    p->split.cnt_n = Prior::kSplitCounters;
+    p->split.target = Prior::kSplitTarget;
+    p->split.max_split = 4;
+  }
   size_t total = 0;
   for (const Item& it : items) total += a256(2 * it.n);
   FL_HIP(hipMalloc(&p->dev16, total));
@@ -364,6 +386,7 @@ FLAMED_API int flamed_prior_destroy(flamed_prior_t h) {
     p->gdec.release();
     if (p->dev) (void)hipFree(p->dev);
     if (p->dev16) (void)hipFree(p->dev16);
+    if (p->split_mem) (void)hipFree(p->split_mem);
   }
   delete p;
   return kOk;
@@ -518,8 +541,9 @@ FLAMED_API int flamed_prior_decode(flamed_prior_t h, const float* x, const uint8
                                   (const void*)(intptr_t)T, (const void*)(intptr_t)P, p->dev,
                                   (const void*)(intptr_t)p->dec_dt, p->dev16};
   return with_graph(p->gdec, key, use_graph != 0, st, [&](hipStream_t s) {
-    return b16 ? run_decode<bf16>(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s)
-               : run_decode<float>(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s);
+    if (!b16) return run_decode<float>(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s);
+    SplitScope sc(tn().prior_split ? &p->split : nullptr);
+    return run_decode<bf16>(p, x, tgt_mask, prompts, B, T, P, pos, embs, logits, w, s);
   });
 }
 

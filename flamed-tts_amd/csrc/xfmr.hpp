@@ -204,39 +204,45 @@ __global__ __launch_bounds__(512) void attn_kernel(const float* __restrict__ QKV
   }
 }
 
-// The same attention on the fp32 matrix cores (v_mfma_f32_16x16x4_f32).  Per workgroup 64 queries of one
-// (utterance, head); 8 waves = 2 key groups x 4 query waves: wave (g, w) owns queries [16 w, 16 w + 16)
-// and the 64-key chunks c = g (mod 2).  Transposed products keep every operand where the next MFMA wants
+// The same attention on the fp32 matrix cores (v_mfma_f32_16x16x4_f32).  Per workgroup 16 QW queries of one
+// (utterance, head); 8 waves = KG key groups x QW query waves: wave (g, w) owns queries [16 w, 16 w + 16)
+// and the 64-key chunks c = g (mod KG).  Transposed products keep every operand where the next MFMA wants
 // it without a shuffle: S^T (keys x queries) = K . Q^T leaves lane (c, r) holding P^T[key 4 r + i][query c],
 // which is exactly that lane's B operand of O^T (dims x queries) = V^T . P^T when the MFMA's four K slots
 // are mapped to keys {4 r + i} (the same permutation on V^T's A operand, read from a transposed V chunk).
 // Online softmax per query column (max / sum over the 4 lanes of a column by two xor shuffles), the two
 // key groups merged through LDS at the end.  Chunks are staged K row-major and V transposed, rows padded
 // by 16 B, the next chunk's global loads in registers while the current one is computed.
-template <int DK>
+// QW query waves x KG key groups = 8 waves: 16 QW queries per workgroup; key group g takes chunks c = g
+// (mod KG).  Two configs: (4, 2) and, where the LDS of four double-buffered groups fits (32-wide heads, the
+// prior decoders at n = 640: 120 -> 240 workgroups), (2, 4).
+template <int DK, int QW>
 struct AttnM {
+  static constexpr int KG = 8 / QW, GT = 64 * QW;                 // key groups, threads per group
   static constexpr int KC = 64, KS = DK + 4, VS = KC + 4;         // padded LDS row strides (floats)
   static constexpr int BUF = KC * KS + DK * VS;                   // K chunk + V^T chunk
   static constexpr int V4 = KC * DK / 4;                          // float4s per operand chunk
-  static constexpr int PT = (2 * V4 + 255) / 256;                 // float4s per thread (a group's 256 threads)
-  static constexpr size_t lds() { return (size_t)4 * BUF * 4 + 4 * KC + (size_t)4 * 64 * (2 + 4 * (DK / 16)) * 4; }
+  static constexpr int PT = (2 * V4 + GT - 1) / GT;               // float4s per thread of a group
+  static constexpr size_t lds() {
+    return (size_t)2 * KG * BUF * 4 + 2 * KG * KC + (size_t)(KG - 1) * QW * 64 * (2 + 4 * (DK / 16)) * 4;
+  }
 };
-template <int DK>
+template <int DK, int QW>
 __global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict__ QKV, const uint8_t* __restrict__ kmask,
                                                         int n, int D, float temp, float* __restrict__ O) {
-  using A = AttnM<DK>;
-  constexpr int KC = A::KC, NT = KC / 16, SB = DK / 16, DT = DK / 16, PT = A::PT;
+  using A = AttnM<DK, QW>;
+  constexpr int KC = A::KC, NT = KC / 16, SB = DK / 16, DT = DK / 16, PT = A::PT, KG = A::KG, GT = A::GT;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   // buffers: [group][2] x (K [KC][KS], V^T [DK][VS]); masks [group][2][KC] bytes; merge area after
-  uint8_t* msk = reinterpret_cast<uint8_t*>(sm + 4 * A::BUF);
-  float* mrg = reinterpret_cast<float*>(msk + 4 * KC);
+  uint8_t* msk = reinterpret_cast<uint8_t*>(sm + 2 * KG * A::BUF);
+  float* mrg = reinterpret_cast<float*>(msk + 2 * KG * KC);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), grp = w >> 2, wq = w & 3, gt = tid & 255;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), grp = w / QW, wq = w % QW, gt = tid % GT;
   const int h = blockIdx.y, b = blockIdx.z;
   const int c = lane & 15, r = lane >> 4;
   const int ld = 3 * D;
   const float* base = QKV + (size_t)b * n * ld;
-  const int qi = blockIdx.x * 64 + wq * 16 + c;  // this lane's query (column of every MFMA tile)
+  const int qi = blockIdx.x * (16 * QW) + wq * 16 + c;  // this lane's query (column of every MFMA tile)
   float4 qr[SB];
   {
     const float* qp = base + (size_t)(qi < n ? qi : n - 1) * ld + h * DK;
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict_
   auto fetch = [&](int k0) {  // this group's next chunk into registers
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
-      const int i = gt + j * 256;
+      const int i = gt + j * GT;
       float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
       if (i < 2 * A::V4) {
         const int op = i / A::V4, rr = i - op * A::V4;
@@ -267,7 +273,7 @@ __global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict_
     float* Vt = Kb + KC * A::KS;
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
-      const int i = gt + j * 256;
+      const int i = gt + j * GT;
       if (i < 2 * A::V4) {
         const int op = i / A::V4, rr = i - op * A::V4;
         const int key = rr / (DK / 4), cc = (rr - key * (DK / 4)) * 4;
@@ -288,13 +294,13 @@ __global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict_
   f32x4 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nch = (n + KC - 1) / KC, iters = (nch + 1) / 2;
+  const int nch = (n + KC - 1) / KC, iters = (nch + KG - 1) / KG;
   fetch(grp * KC);
   stash(0);
   __syncthreads();
   for (int it = 0; it < iters; ++it) {
-    const int buf = it & 1, ch = 2 * it + grp;
-    if (it + 1 < iters) fetch((ch + 2) * KC);  // in flight during this chunk's math
+    const int buf = it & 1, ch = KG * it + grp;
+    if (it + 1 < iters) fetch((ch + KG) * KC);  // in flight during this chunk's math
     const float* Kb = sm + (grp * 2 + buf) * A::BUF;
     const float* Vt = Kb + KC * A::KS;
     const uint8_t* mk = msk + (grp * 2 + buf) * KC;
@@ -362,9 +368,10 @@ __global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict_
     if (it + 1 < iters) stash(buf ^ 1);  // that buffer's last readers finished before the previous barrier
     __syncthreads();
   }
-  // merge the two key groups: group 1 leaves (m, l, o) per lane, group 0 combines and writes
-  float* mw = mrg + (wq * 64 + lane) * (2 + 4 * DT);
-  if (grp == 1) {
+  // merge the key groups: groups 1.. leave (m, l, o) per lane, group 0 combines them in group order
+  constexpr int MS = 2 + 4 * DT;
+  if (grp > 0) {
+    float* mw = mrg + (((grp - 1) * QW + wq) * 64 + lane) * MS;
     mw[0] = m;
     mw[1] = l;
 #pragma unroll
@@ -373,18 +380,31 @@ __global__ __launch_bounds__(512) void attn_mfma_kernel(const float* __restrict_
       for (int i = 0; i < 4; ++i) mw[2 + 4 * dt + i] = o[dt][i];
   }
   __syncthreads();
-  if (grp == 1) return;
-  const float m1 = mw[0], l1 = mw[1];
-  const float M = fmaxf(m, m1);
-  const float f0 = __expf(m - M), f1 = __expf(m1 - M);  // all keys padded: M = -inf -> NaN, as the reference's softmax
-  const float L = l * f0 + l1 * f1;
+  if (grp > 0) return;
+  float M = m;
+#pragma unroll
+  for (int g = 1; g < KG; ++g) M = fmaxf(M, mrg[(((g - 1) * QW + wq) * 64 + lane) * MS]);
+  float f[KG];
+  f[0] = __expf(m - M);  // all keys padded: M = -inf -> NaN, as the reference's softmax
+  float L = l * f[0];
+#pragma unroll
+  for (int g = 1; g < KG; ++g) {
+    const float* mw = mrg + (((g - 1) * QW + wq) * 64 + lane) * MS;
+    f[g] = __expf(mw[0] - M);
+    L += mw[1] * f[g];
+  }
   if (qi >= n) return;
   float* op = O + ((size_t)b * n + qi) * D + h * DK;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
     float v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = (o[dt][i] * f0 + mw[2 + 4 * dt + i] * f1) / L;
+    for (int i = 0; i < 4; ++i) {
+      float a = o[dt][i] * f[0];
+#pragma unroll
+      for (int g = 1; g < KG; ++g) a += mrg[(((g - 1) * QW + wq) * 64 + lane) * MS + 2 + 4 * dt + i] * f[g];
+      v[i] = a / L;
+    }
     *reinterpret_cast<float4*>(op + 16 * dt + 4 * r) = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
@@ -436,10 +456,11 @@ static int ln_mask(int D, const float* R, const float* g, const float* b, const 
 template <int DK>
 static int launch_attn(const float* QKV, const uint8_t* mask, int B, int n, int D, int H, float temp, float* O, hipStream_t st) {
   if (tn().attn_mfma) {
-    const size_t lds = AttnM<DK>::lds();
-    auto kern = attn_mfma_kernel<DK>;
+    constexpr int QW = AttnM<DK, 2>::lds() <= 160 * 1024 ? 2 : 4;
+    const size_t lds = AttnM<DK, QW>::lds();
+    auto kern = attn_mfma_kernel<DK, QW>;
     if (lds > 64 * 1024) FL_HIP(set_max_lds(reinterpret_cast<const void*>(kern)));
-    hipLaunchKernelGGL(kern, dim3((n + 63) / 64, H, B), dim3(512), lds, st, QKV, mask, n, D, temp, O);
+    hipLaunchKernelGGL(kern, dim3((n + 16 * QW - 1) / (16 * QW), H, B), dim3(512), lds, st, QKV, mask, n, D, temp, O);
     FL_LAUNCH_CHECK();
     return kOk;
   }

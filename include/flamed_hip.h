@@ -172,6 +172,8 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     fits (see flamed_pva_flow); 0: hipGraph of launches;
  *   "attn_mfma"     — 1 (default): transformer attention (prior stack, timbre encoder) on fp32 MFMA;
  *                     0: the LDS-broadcast FMA kernel;
+ *   "prior_split"   — 1 (default): bf16 prior decoders split K of the GEMMs whose tile grid leaves CUs
+ *                     idle (per-handle slabs, fixed slice order); 0: one K chain;
  *   "noctr"         — diagnostic: kernels ignore the device step counter (wrong modulation rows);
  *   "dup_class"     — ablation: launch every denoiser kernel of this class (see
  *                     FLAMED_DEN_KERNEL_CLASSES) twice per Euler step; -1 (default) = off.

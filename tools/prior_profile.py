@@ -29,23 +29,27 @@ def main():
     tmask = torch.zeros(1, T, dtype=torch.bool, device=dev)
     codes = torch.randint(0, 1024, (1, 6, P), generator=g).to(dev)
     h = pg.hip()
+    dts = sys.argv[1:] or ["bf16"]  # decoder-side GEMM operand types to time (bf16, f32)
     with torch.inference_mode():
-        for graph in (False, True):
-            pg.hip_graph = graph
-            for _ in range(3):
-                h.encode(ids, smask)
-                h.decode(x, tmask, codes, P)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(10):
-                h.encode(ids, smask)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(10):
-                h.decode(x, tmask, codes, P)
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            print(f"graph={graph} encode {(t1 - t0) * 100:.3f} ms decode {(t2 - t1) * 100:.3f} ms", flush=True)
+        for dt in dts:
+            pg.hip_dec_dtype = dt
+            for graph in (False, True):
+                pg.hip_graph = graph
+                for _ in range(3):
+                    h.encode(ids, smask)
+                    h.decode(x, tmask, codes, P)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(10):
+                    h.encode(ids, smask)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(10):
+                    h.decode(x, tmask, codes, P)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                print(f"decoders {dt} graph={graph} encode {(t1 - t0) * 100:.3f} ms decode {(t2 - t1) * 100:.3f} ms",
+                      flush=True)
 
 
 if __name__ == "__main__":
