@@ -324,6 +324,17 @@ __device__ __forceinline__ void flush_frag(const char* stg, bf16* dst, int g, in
   }
 }
 
+// The fp32 residual rows other groups read: only the kHalo rows at each end of a group (the depthwise
+// halo of its neighbours), written through; the middle rows never leave the workgroup's registers.
+__device__ __forceinline__ void flush_halo(const char* stg, float* ximg, int r0, int nr, int col0, int T) {
+  if (nr <= 2 * kHalo) {
+    flush_tile<float>(stg, ximg, kH, r0, 0, nr, col0, T);
+    return;
+  }
+  flush_tile<float>(stg, ximg, kH, r0, 0, kHalo, col0, T);
+  flush_tile<float>(stg, ximg, kH, r0, nr - kHalo, nr, col0, T);
+}
+
 __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) {
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
     stage_tile<float>(stg, X, wave, lane);
     __syncthreads();
-    flush_tile<float>(stg, P.ximg, H, r0, 0, nr, col0, T);
+    flush_halo(stg, P.ximg, r0, nr, col0, T);
     signal(mygrp);
     PST(step);
     ++L;
@@ -818,7 +829,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
       stage_tile<float>(stg, X, wave, lane);
       __syncthreads();
-      flush_tile<float>(stg, P.ximg, H, r0, 0, nr, col0, T);
+      flush_halo(stg, P.ximg, r0, nr, col0, T);
       signal(mygrp);
       PST(step);
       ++L;
