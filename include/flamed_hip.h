@@ -228,6 +228,9 @@ FLAMED_API size_t flamed_pva_workspace_size(flamed_dur_t h, int B, int L, int nf
 FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* enc, const uint8_t* mask, float* dur_t,
                                float* sil_t, const float* ts, int nfe, int B, int L, void* ws, size_t ws_bytes,
                                int use_graph, hipStream_t stream);
+/* 1 when a flamed_pva_flow(use_graph != 0) of B x L rows on this pair would run as the persistent launch
+ * (the caller may then pass its own buffers: no graph keyed on their addresses), 0 otherwise. */
+FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int B, int L);
 /* (diagnostic) persistent PVA flows completed on the duration handle, whether one timed out (the pair
  * then stays on the graph path), device ms of the last one. */
 FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms);
