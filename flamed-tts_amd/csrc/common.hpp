@@ -36,6 +36,17 @@ enum Status : int {
     }                                                                                    \
   } while (0)
 
+// Destroy a cached graph exec that earlier calls may still have in flight (re-capture on a changed key,
+// handle reload or destroy): drain the device first.  The exec owns the replay's kernel-argument and
+// node storage; freeing it under a queued replay is a use-after-free in the runtime.  Re-captures are
+// rare (new shapes / buffers / knobs), so the full drain costs nothing on the steady path.
+inline void retire_graph(hipGraphExec_t& ex) {
+  if (!ex) return;
+  (void)hipDeviceSynchronize();
+  (void)hipGraphExecDestroy(ex);
+  ex = nullptr;
+}
+
 #define FL_REQUIRE(cond, ...)        \
   do {                               \
     if (!(cond)) {                   \

@@ -1705,7 +1705,7 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
   {
     std::lock_guard<std::recursive_mutex> lk(d->mu);
     DeviceGuard dg(d->device);
-    if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
+    retire_graph(d->gexec);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     if (d->ctr) (void)hipFree(d->ctr);
     if (d->scnt) (void)hipFree(d->scnt);
@@ -1755,7 +1755,7 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   std::lock_guard<std::recursive_mutex> lk(d->mu);
   if (d->device >= 0 && d->device != wdev) {  // re-load onto another device: drop the old device's state
     DeviceGuard og(d->device);
-    if (d->gexec) { (void)hipGraphExecDestroy(d->gexec); d->gexec = nullptr; }
+    retire_graph(d->gexec);
     if (d->cap_stream) { (void)hipStreamDestroy(d->cap_stream); d->cap_stream = nullptr; }
     if (d->ctr) { (void)hipFree(d->ctr); d->ctr = nullptr; }
     if (d->scnt) { (void)hipFree(d->scnt); d->scnt = nullptr; }
@@ -1879,7 +1879,7 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   FL_HIP(hipMemsetAsync(d->scnt, 0, sizeof(int) * Den::kSplitCounters, st));
   if (!d->gcnt) FL_HIP(hipMalloc(&d->gcnt, sizeof(int) * Den::kGnCounters));
   FL_HIP(hipMemsetAsync(d->gcnt, 0, sizeof(int) * Den::kGnCounters, st));
-  if (d->gexec) { (void)hipGraphExecDestroy(d->gexec); d->gexec = nullptr; }
+  retire_graph(d->gexec);
   return kOk;
 }
 
@@ -2344,7 +2344,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   const bool hit = d->gexec && d->g_B == B && d->g_T == T && d->g_nfe == nfe && d->g_xt == xt && d->g_mods == mods && d->g_ws == ws &&
                    d->g_epoch == d->tune_ver;
   if (!hit) {
-    if (d->gexec) { FL_HIP(hipGraphExecDestroy(d->gexec)); d->gexec = nullptr; }
+    retire_graph(d->gexec);
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
     int rc = kOk;

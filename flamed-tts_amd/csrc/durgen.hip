@@ -135,7 +135,7 @@ struct PvaGraph {
   std::vector<const void*> key;
   int* ctr = nullptr;  // device Euler step counters: [0] duration chain, [1] silence chain
   void release() {
-    if (exec) (void)hipGraphExecDestroy(exec);
+    retire_graph(exec);
     if (cap) (void)hipStreamDestroy(cap);
     if (cap2) (void)hipStreamDestroy(cap2);
     if (fork) (void)hipEventDestroy(fork);
@@ -555,7 +555,7 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
                                   (const void*)(intptr_t)B, (const void*)(intptr_t)L, nd->dev, ns->dev,
                                   (const void*)(intptr_t)tune_ep};  // knobs (pva_split) are baked into the graph
   if (!gp.exec || gp.key != key) {
-    if (gp.exec) { FL_HIP(hipGraphExecDestroy(gp.exec)); gp.exec = nullptr; }
+    retire_graph(gp.exec);
     if (!gp.cap) FL_HIP(hipStreamCreateWithFlags(&gp.cap, hipStreamNonBlocking));
     if (!gp.cap2) FL_HIP(hipStreamCreateWithFlags(&gp.cap2, hipStreamNonBlocking));
     if (!gp.fork) FL_HIP(hipEventCreateWithFlags(&gp.fork, hipEventDisableTiming));

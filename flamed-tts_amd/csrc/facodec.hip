@@ -257,7 +257,7 @@ struct Fac {
   hipStream_t cap = nullptr;
   std::vector<const void*> gkey;
   void release() {
-    if (gexec) (void)hipGraphExecDestroy(gexec);
+    retire_graph(gexec);
     if (cap) (void)hipStreamDestroy(cap);
     if (dev) (void)hipFree(dev);
     gexec = nullptr; cap = nullptr; dev = nullptr;
@@ -484,7 +484,7 @@ FLAMED_API int flamed_fac_load(flamed_fac_t h, const float* const* w, int nw, hi
     }
   }
   FL_HIP(hipStreamSynchronize(st));  // the fold scratch is reused per conv on the same stream; drain before returning
-  if (f->gexec) { (void)hipGraphExecDestroy(f->gexec); f->gexec = nullptr; }
+  retire_graph(f->gexec);
   return kOk;
 }
 
@@ -516,7 +516,7 @@ FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const flo
   if (!use_graph) return run(st);
   std::vector<const void*> key = {latents, spk, wav, ws, (const void*)(intptr_t)B, (const void*)(intptr_t)T, f->dev};
   if (!f->gexec || f->gkey != key) {
-    if (f->gexec) { FL_HIP(hipGraphExecDestroy(f->gexec)); f->gexec = nullptr; }
+    retire_graph(f->gexec);
     if (!f->cap) FL_HIP(hipStreamCreateWithFlags(&f->cap, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(f->cap, hipStreamCaptureModeRelaxed));
     int r = run(f->cap);
@@ -642,7 +642,7 @@ struct Enc {
   hipStream_t cap = nullptr;
   std::vector<const void*> gkey;
   void release() {
-    if (gexec) (void)hipGraphExecDestroy(gexec);
+    retire_graph(gexec);
     if (cap) (void)hipStreamDestroy(cap);
     if (dev) (void)hipFree(dev);
     gexec = nullptr; cap = nullptr; dev = nullptr;
@@ -860,7 +860,7 @@ FLAMED_API int flamed_enc_load(flamed_enc_t h, const float* const* w, int nw, hi
   }
   e->wfin = e->dev + convs[ifin].off;
   FL_HIP(hipStreamSynchronize(st));  // fold scratch reused per conv
-  if (e->gexec) { (void)hipGraphExecDestroy(e->gexec); e->gexec = nullptr; }
+  retire_graph(e->gexec);
   return kOk;
 }
 
@@ -892,7 +892,7 @@ FLAMED_API int flamed_enc_encode(flamed_enc_t h, const float* wav, int B, int n,
   if (!use_graph) return run(st);
   std::vector<const void*> key = {wav, out, ws, (const void*)(intptr_t)B, (const void*)(intptr_t)n, e->dev};
   if (!e->gexec || e->gkey != key) {
-    if (e->gexec) { FL_HIP(hipGraphExecDestroy(e->gexec)); e->gexec = nullptr; }
+    retire_graph(e->gexec);
     if (!e->cap) FL_HIP(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(e->cap, hipStreamCaptureModeRelaxed));
     int r = run(e->cap);

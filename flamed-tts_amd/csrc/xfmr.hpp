@@ -490,7 +490,7 @@ struct CapGraph {
   hipStream_t cap = nullptr;
   std::vector<const void*> key;
   void release() {
-    if (exec) (void)hipGraphExecDestroy(exec);
+    retire_graph(exec);
     if (cap) (void)hipStreamDestroy(cap);
     *this = CapGraph();
   }
@@ -503,7 +503,7 @@ static int with_graph(CapGraph& g, const std::vector<const void*>& key_in, bool 
   std::vector<const void*> key = key_in;
   key.push_back((const void*)(intptr_t)tune_epoch());
   if (!g.exec || g.key != key) {
-    if (g.exec) { FL_HIP(hipGraphExecDestroy(g.exec)); g.exec = nullptr; }
+    retire_graph(g.exec);
     if (!g.cap) FL_HIP(hipStreamCreateWithFlags(&g.cap, hipStreamNonBlocking));
     FL_HIP(hipStreamBeginCapture(g.cap, hipStreamCaptureModeRelaxed));
     int r = body(g.cap);
