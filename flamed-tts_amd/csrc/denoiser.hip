@@ -757,8 +757,18 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
   const int pp = tid % NP, rg = tid / NP, c = c0 + 2 * pp;  // channels c, c + 1
   const int nch = (T + TC - 1) / TC;
   mod = mod.at();
-  float4 xv[2][NX];  // tiles of chunks ch and ch + 1 in flight
-  auto load_x = [&](float4* xs, int t0) __attribute__((always_inline)) {
+  // tiles of chunks ch and ch + 1 in flight, held RAW (bf16 pairs or fp32): converting at load time
+  // would make the compiler wait for each prefetch right after issuing it
+  using XR = typename std::conditional<std::is_same<XT, bf16>::value, uint2, float4>::type;
+  XR xv[2][NX];
+  auto cvt = [](const XR& r) __attribute__((always_inline)) -> float4 {
+    if constexpr (std::is_same<XT, bf16>::value)
+      return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+                         __uint_as_float(r.y & 0xffff0000u));
+    else
+      return r;
+  };
+  auto load_x = [&](XR* xs, int t0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int q = tid + j * NTH;
@@ -767,11 +777,11 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
       // unconditional load from a clamped row (rows outside the utterance are zeroed when staged): no
       // branches around the loads, so the wait before staging chunk ch leaves chunk ch + 1's in flight
       const int tc = min(max(t, 0), T - 1), c4c = q < SR * C4 ? c4 : 0;
-      xs[j] = ldx4<XT>(X + ((size_t)b * T + tc) * H + c0 + 4 * c4c);
+      xs[j] = *reinterpret_cast<const XR*>(X + ((size_t)b * T + tc) * H + c0 + 4 * c4c);
     }
   };
   load_x(xv[0], 0);
-  if (nch > 1) load_x(xv[1], TC);
+  load_x(xv[1], min(TC, (nch - 1) * TC));
   for (int t = tid; t < T; t += NTH) row_stats_from_partials(S, b * T + t, NT, tw, eps_ln, rs[2 * t], rs[2 * t + 1]);
   dg_f2 w[KS];
 #pragma unroll
@@ -794,7 +804,7 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
     if (ch >= nch) break;
     const int t0 = ch * TC;
     float* h = hs[ch & 1];
-    float4* xc = xv[ch & 1];
+    XR* xr = xv[ch & 1];
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int q = tid + j * NTH;
@@ -802,16 +812,19 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
         const int r = q / C4, c4 = q - r * C4;
         const int t = t0 - HALO + r;
         dg_f2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+        const float4 xcj = cvt(xr[j]);
         if (t >= 0 && t < T) {
           const dg_f2 mean = rs[2 * t], rstd = rs[2 * t + 1];
           const float4 a4 = *reinterpret_cast<const float4*>(va + 4 * c4), b4 = *reinterpret_cast<const float4*>(vb + 4 * c4);
-          lo = ((dg_f2{xc[j].x, xc[j].y} - mean) * rstd) * dg_f2{a4.x, a4.y} + dg_f2{b4.x, b4.y};
-          hi = ((dg_f2{xc[j].z, xc[j].w} - mean) * rstd) * dg_f2{a4.z, a4.w} + dg_f2{b4.z, b4.w};
+          lo = ((dg_f2{xcj.x, xcj.y} - mean) * rstd) * dg_f2{a4.x, a4.y} + dg_f2{b4.x, b4.y};
+          hi = ((dg_f2{xcj.z, xcj.w} - mean) * rstd) * dg_f2{a4.z, a4.w} + dg_f2{b4.z, b4.w};
         }
         *reinterpret_cast<float4*>(h + r * LDH + 4 * c4) = make_float4(lo.x, lo.y, hi.x, hi.y);
       }
     }
-    if (ch + 2 < nch) load_x(xc, t0 + 2 * TC);  // two chunks ahead, in flight during the next two convs
+    // two chunks ahead, in flight during the next two convs; issued unconditionally (past the end: the
+    // last chunk again) so every path has the same loads in flight and the waits stay counted
+    load_x(xr, min(t0 + 2 * TC, (nch - 1) * TC));
     __syncthreads();  // h staged; the other buffer (chunk ch-1) is no longer read
     dg_f2 win[WIN];
 #pragma unroll
