@@ -826,15 +826,22 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
     // last chunk again) so every path has the same loads in flight and the waits stay counted
     load_x(xr, min(t0 + 2 * TC, (nch - 1) * TC));
     __syncthreads();  // h staged; the other buffer (chunk ch-1) is no longer read
-    dg_f2 win[WIN];
+    // sliding window: staged row r feeds frames q = r - j of this thread's RPT (each frame's taps still
+    // accumulate in tap order j = 0..KS-1), so only a few window rows are live at a time
+    dg_f2 acc[RPT];
 #pragma unroll
-    for (int j = 0; j < WIN; ++j) win[j] = *reinterpret_cast<const dg_f2*>(h + (rg * RPT + j) * LDH + 2 * pp);
+    for (int q = 0; q < RPT; ++q) acc[q] = bias;
+#pragma unroll
+    for (int r = 0; r < WIN; ++r) {
+      const dg_f2 row = *reinterpret_cast<const dg_f2*>(h + (rg * RPT + r) * LDH + 2 * pp);
+#pragma unroll
+      for (int q = 0; q < RPT; ++q)
+        if (r - q >= 0 && r - q < KS) acc[q] = __builtin_elementwise_fma(w[r - q], row, acc[q]);
+    }
     const int nv = T - (t0 + rg * RPT);  // valid frames of this thread in the chunk (may be <= 0)
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-      dg_f2 a = bias;
-#pragma unroll
-      for (int j = 0; j < KS; ++j) a = __builtin_elementwise_fma(w[j], win[q + j], a);
+      const dg_f2 a = acc[q];
       dv[ch][q] = a;
       if (ch == 0 && q == 0) K = a;
       if (q < nv) {
