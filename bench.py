@@ -36,7 +36,7 @@ KERNEL_NAMES = ["proj_in_gemm", "lnmod_dwconv_gnpartials", "gn_finalize", "gnapp
                 "conv_out_combine_euler"]
 N_CLASSES = len(KERNEL_NAMES)
 HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md chip table (spec)
-MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}   # dense peaks
+MFMA_PEAK_TFS = {"bf16": 2500.0, "fp8": 5000.0, "f32": 157.3}   # dense peaks
 FOLD = None  # LayerNorm fold active (set in main: bf16 and flamed_tune lnfold != 0)
 
 
@@ -45,10 +45,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
-    ap.add_argument("--frames", type=int, default=400, help="latent frames per utterance (80 Hz)")
-    ap.add_argument("--nfe", type=int, default=128)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"], help="denoiser handle dtype (fp8: MX-fp8 pointwise GEMMs at large M)")
+    ap.add_argument("--config", type=int, default=None, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i] per-GPU workload (default: 1 = B=1 T=400 nfe=128 bf16); "
+                         "--batch/--frames/--nfe/--dtype override its fields")
+    ap.add_argument("--batch", type=int, default=None, help="utterances per GPU")
+    ap.add_argument("--frames", type=int, default=None, help="latent frames per utterance (80 Hz)")
+    ap.add_argument("--nfe", type=int, default=None)
+    ap.add_argument("--dtype", default=None, choices=["bf16", "f32", "fp8"], help="denoiser handle dtype (fp8: MX-fp8 pointwise GEMMs at large M)")
+    ap.add_argument("--no-configs3", action="store_true",
+                    help="N > 1: skip the extra configs[3] leg (64 utterances per GPU on every rank)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -82,7 +87,50 @@ def parse():
                     help="CPU rehearsal of the launcher/timing harness over gloo (no GPU; tests/test_bench_cpu.py)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary rows (PVA flow + LR, FaCodec decode / prompt encode, end-to-end RTF)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config or 1]
+    for k in ("batch", "frames", "nfe", "dtype"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg[k])
+    return args
+
+
+# BASELINE.json configs[i] as per-GPU workloads (configs[0] is the CPU plumbing case: --plumbing)
+CONFIGS = {
+    1: {"batch": 1, "frames": 400, "nfe": 128, "dtype": "bf16"},
+    2: {"batch": 64, "frames": 400, "nfe": 128, "dtype": "bf16"},
+    3: {"batch": 64, "frames": 400, "nfe": 128, "dtype": "bf16"},   # per GPU; global batch 64 x N (512 at N = 8)
+    4: {"batch": 16, "frames": 2400, "nfe": 256, "dtype": "fp8"},
+}
+
+
+def workload_label(args, world: int) -> tuple:
+    """(configs index, label) of what this run measures: --config when given, else inferred from the per-GPU
+    shape and the rank count (one rank: B = 1 -> configs[1], T = 2400 -> configs[4], else configs[2]; several
+    ranks: the configs[3] utterance-sharded layout).  The label states the shape that actually ran."""
+    B, T, nfe, dt = args.batch, args.frames, args.nfe, args.dtype
+    if args.config is not None:
+        i = args.config
+    elif world > 1:
+        i = 3
+    elif B == 1 and T <= 800:
+        i = 1
+    elif T >= 2400:
+        i = 4
+    else:
+        i = 2
+    ref = CONFIGS[i]
+    exact = (B, T, nfe) == (ref["batch"], ref["frames"], ref["nfe"])
+    audio = T * 200 / 16000.0
+    shape = f"{B} utterance(s) x {T} frames ({audio:.1f} s audio) per GPU, nsteps-denoiser={nfe}, {dt}"
+    if i == 3:
+        text = (f"BASELINE configs[3]: {shape}, utterance-sharded over {world} GPU(s) (global batch {B * world}; "
+                f"configs[3] is 64 per GPU = 512 on 8)")
+    else:
+        text = f"BASELINE configs[{i}]: {shape}"
+    if not exact:
+        text += f" [configs[{i}] layout at a non-reference size: reference is B={ref['batch']} T={ref['frames']} nfe={ref['nfe']}]"
+    return i, text
 
 
 def kernel_costs(cls: int, B: int, T: int, H: int, C: int, NB: int, es: int, fold: bool | None = None,
@@ -324,28 +372,26 @@ def secondary_measurements(dev, nfe):
 
 
 def duration_flips(pr, phon, nfe_d, dev, temperature=0.3):
-    """Integer duration flip rate of an end-to-end run (SURVEY.md §7 hard part 2): the same encoder
-    output and the same CPU-RNG noise (seed 0, as the timed e2e run draws it) through the HIP PVA flow
-    (exact-fp32 MFMA) and through the package's own fp32 torch-CPU PVA modules (the reference op order,
-    pva.py:97-112); frames = clamp(round(exp(d) - 1), 0) compared per phoneme."""
-    from flamed.models.synthesizer.pva import PVA
+    """Integer duration flip rate of an end-to-end run (SURVEY.md §7 hard part 2), a checker beside the
+    timed run: the same encoder output and the same CPU-RNG noise (seed 0, as the timed e2e run draws it)
+    through the HIP PVA flow (exact-fp32 MFMA) and through the oracle's fp32 restatement of PVA.sample's
+    Euler loop (oracle.pva_flow, reference pva.py:97-109); frames = clamp(round(exp(d) - 1), 0)
+    (pva.py:111-112) compared per phoneme."""
+    from oracle import flamed_oracle as orc  # checker only
     L = phon.shape[1]
     smask = torch.zeros(1, L, dtype=torch.bool, device=dev)
     with torch.inference_mode():
         enc = pr.hip().encode(phon, smask)
         torch.manual_seed(0)
         d_g, s_g = pr.pva.flow(enc, smask, nfe_d, temperature)
-        cpu = PVA(pr.config["variance_adaptor"]).eval()
-        cpu.load_state_dict({k: v.detach().cpu() for k, v in pr.pva.state_dict().items()})
+        sd = {"prior_generator.pva." + k: v.detach().float().cpu() for k, v in pr.pva.state_dict().items()}
         torch.manual_seed(0)
-        d_c, s_c = cpu.flow(enc.cpu(), smask.cpu(), nfe_d, temperature)
-
-    def frames(d):
-        return torch.clamp(torch.round(torch.exp(d.float().cpu()) - 1), min=0)
-    flips = int((frames(d_g) != frames(d_c)).sum()) + int((frames(s_g) != frames(s_c)).sum())
+        d_c, s_c = orc.pva_flow(sd, enc.float().cpu(), smask.cpu(), nfe_d, temperature)
+    f = orc.log_to_frames
+    flips = int((f(d_g.float().cpu()) != f(d_c)).sum()) + int((f(s_g.float().cpu()) != f(s_c)).sum())
     return {"phonemes": L, "durations_compared": 2 * L, "flips": flips, "flip_rate": flips / (2.0 * L),
             "max_abs_log_dur_diff": float(max((d_g.cpu() - d_c).abs().max(), (s_g.cpu() - s_c).abs().max())),
-            "vs": "package fp32 torch-CPU PVA modules, same encoder output and noise"}
+            "vs": "oracle.pva_flow (fp32 restatement of pva.py:97-109), same encoder output and CPU-RNG noise"}
 
 
 def long_form(pg, dev, args, C, T=2400, nfe=256):
@@ -453,6 +499,41 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
             "kernels": ks, "fp8": fp8}
 
 
+def configs3_leg(pg, dev, dist, world, rank, args, C):
+    """BASELINE configs[3] on every rank at once: 64 utterances x 400 frames per GPU, nfe = 128, bf16, seed + rank
+    (the scaling curve's own per-GPU workload), timed after warm-up as max over ranks, with every rank's
+    frames/s and the efficiency against rank 0 running the same per-GPU workload alone."""
+    cfg = CONFIGS[3]
+    B, T, nfe = cfg["batch"], cfg["frames"], cfg["nfe"]
+    hip = pg.denoiser.hip()
+    g = torch.Generator().manual_seed(args.seed + 1000 + rank)
+    x0 = (torch.randn(B, T, C, generator=g) * 0.3 + torch.randn(B, T, C, generator=g)).to(dev)
+    spk = torch.randn(B, C, generator=g).to(dev)
+    ts = torch.linspace(0, 1, nfe + 1, device=dev)
+    steps = 2
+
+    def step():
+        hip.solve(x0, ts, spk, nfe)
+
+    def sync():
+        torch.cuda.synchronize(dev)
+    with torch.inference_mode():
+        step()
+        sync()
+        dist.barrier()
+        solo = _timed(step, steps, sync) if rank == 0 else None
+        dist.barrier()
+        sync()
+        dist.barrier()
+        sec = _timed(step, steps, sync)
+        dist.barrier()
+    sec, per_rank, eff = scaling_stats(dist, world, rank, B * T, sec, solo, dev)
+    return {"workload": f"BASELINE configs[3]: {B} utterances x {T} frames per GPU, nsteps-denoiser={nfe}, bf16, "
+                        f"utterance-sharded over {world} GPUs (global batch {B * world})",
+            "value": round(world * B * T / sec, 2), "unit": "latent frames/s", "ms_per_step": round(sec * 1e3, 3),
+            "steps": steps, "global_batch": B * world, "per_rank_frames_per_s": per_rank, "scaling_detail": eff}
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) outside a torchrun job: start N ranks of this same script under
     torch.distributed.run as a CHILD process (nothing here has touched the GPU: no exec from a process
@@ -471,11 +552,42 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def scaling_stats(dist, world, rank, frames_per_rank, sec, solo_sec, dev=None):
+    """Max-over-ranks step time (the contract's clock), every rank's own frames/s, and the efficiency of the
+    whole job against N x the same per-GPU workload timed on rank 0 alone in the same process tree (the
+    other ranks idle at a barrier meanwhile).  One rank: (sec, [frames/s], None)."""
+    if world == 1:
+        return sec, [round(frames_per_rank / sec, 3)], None
+    import torch.distributed  # noqa: F401
+    tt = torch.tensor([sec], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    per = torch.zeros(world, dtype=torch.float64, device=dev)
+    per[rank] = frames_per_rank / sec
+    dist.all_reduce(per)
+    smax = float(tt.item())
+    solo = torch.tensor([solo_sec if rank == 0 else 0.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(solo)
+    solo_fps = frames_per_rank / float(solo.item())
+    value = world * frames_per_rank / smax
+    return smax, [round(float(v), 3) for v in per.cpu()], {
+        "solo_rank0_frames_per_s": round(solo_fps, 3), "efficiency_vs_n1": round(value / (world * solo_fps), 4),
+        "n1_reference": "the same per-GPU workload timed on rank 0 alone (other ranks idle), same process tree"}
+
+
+def _timed(fn, steps, sync):
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    return (time.perf_counter() - t0) / steps
+
+
 def plumbing(args, rank, world):
     """--plumbing: the launcher / timing / reporting harness on CPU over gloo (CI rehearsal of the
     multi-rank path; no GPU): each rank runs ProbGenerator.sample on its own tiny synthetic shard with
     the module's torch ops (the reference's --device cpu path, BASELINE configs[0]) and rank 0 prints
-    the same JSON line shape as the GPU bench."""
+    the same JSON line shape as the GPU bench (label, global batch, per-rank frames/s, efficiency)."""
     import torch.distributed as dist
     from flamed.models.synthesizer.prob_generator import ProbGenerator
     from flamed.utils.seeded_init import randomize_module
@@ -490,30 +602,36 @@ def plumbing(args, rank, world):
     cond = torch.randn(B, cfg["n_quantizers"], T, cfg["cond_dim"], generator=g)
     spk = torch.randn(B, cfg["target_dim"], generator=g)
     mask = torch.ones(B, T, 1, dtype=torch.bool)
+    res = {}
+
+    def step():
+        res["out"] = pg.sample(cond, spk, mask, nfe=nfe, temperature=0.3)
+
+    def nosync():
+        pass
     with torch.inference_mode():
         for _ in range(max(1, args.warmup)):
-            pg.sample(cond, spk, mask, nfe=nfe, temperature=0.3)
+            step()
+        solo = None
         if world > 1:
             dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = pg.sample(cond, spk, mask, nfe=nfe, temperature=0.3)
-        sec = (time.perf_counter() - t0) / args.steps
+            if rank == 0:
+                solo = _timed(step, args.steps, nosync)
+            dist.barrier()
+        sec = _timed(step, args.steps, nosync)
         if world > 1:
             dist.barrier()
-            tt = torch.tensor([sec], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            sec = float(tt.item())
-            per = torch.zeros(world, dtype=torch.float64)
-            per[rank] = B * T / sec
-            dist.all_reduce(per)
+        sec, per_rank, eff = scaling_stats(dist if world > 1 else None, world, rank, B * T, sec, solo)
+    out = res["out"]
+    _, label = workload_label(args, world)
     line = {"metric": "latent frames/s (plumbing: CPU torch path over gloo)", "value": round(world * B * T / sec, 3),
             "unit": "latent frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(sec * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic", "plumbing": True, "finite": bool(torch.isfinite(out).all()),
-            "config": {"workload": f"CPU plumbing: {B} x {T} frames per rank, nfe={nfe}", "batch_per_gpu": B,
+            "config": {"workload": "CPU plumbing of " + label, "batch_per_gpu": B,
                        "frames": T, "nfe": nfe, "global_batch": world * B,
-                       "parallelism": f"utterance-sharded x{world} (no collectives)"}}
+                       "parallelism": f"utterance-sharded x{world} (no collectives)"},
+            "per_rank_frames_per_s": per_rank, "scaling_detail": eff}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -571,31 +689,41 @@ def main():
     def step():
         return hip.solve(xt0, ts, spk, nfe)
 
+    def sync():
+        torch.cuda.synchronize(dev)
+
     with torch.inference_mode():
         for _ in range(max(1, args.warmup)):
             out = step()
+        torch.cuda.synchronize()
+        solo = None
+        if dist:  # the N = 1 reference of the efficiency figure: rank 0 alone, the other ranks idle
+            dist.barrier()
+            if rank == 0:
+                solo = _timed(step, args.steps, sync)
+            dist.barrier()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         runs0 = hip.persist_info()[0] if args.dtype == "bf16" else 0
         t0 = time.perf_counter()
-        pms = []  # device time of each persistent launch (HIP events around the kernel, launch stream)
         for _ in range(args.steps):
             out = step()
-            if args.dtype == "bf16":
-                pms.append(hip.persist_info(with_ms=True)[2])
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         persist_runs = (hip.persist_info()[0] - runs0) if args.dtype == "bf16" else 0
+        # device time of each persistent launch of the timed region: HIP events around the kernel on its
+        # launch stream, recorded by the library (flamed_den_persist_times), read after the region
+        pms = hip.persist_times(args.steps) if persist_runs >= args.steps else []
         if dist:
             dist.barrier()
         sec = (t1 - t0) / args.steps
-        if dist:
-            tt = torch.tensor([sec], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            sec = float(tt.item())
+        sec, per_rank, eff = scaling_stats(dist, world, rank, B * T, sec, solo, dev)
         finite = bool(torch.isfinite(out).all().item())
+        configs3 = None
+        if dist and not args.no_configs3 and B != CONFIGS[3]["batch"]:
+            configs3 = configs3_leg(pg, dev, dist, world, rank, args, C)
 
         # ---- live per-kernel timing, dominant kernel roofline: in-graph cost per launch of each kernel
         # class (graph of 4 Euler steps replayed as captured vs with that class doubled; HIP events on
@@ -610,7 +738,7 @@ def main():
         nat.check(L.flamed_den_time_kernels_graph(hip.handle, nat.ptr(xs), nat.ptr(mods), B, T, nat.ptr(ws), ws.numel(),
                                                   args.kernel_iters, ms, nat.stream_ptr(dev)), "flamed_den_time_kernels_graph")
         torch.cuda.synchronize()
-    es = 2 if args.dtype == "bf16" else 4
+    es = 4 if args.dtype == "f32" else 2
     # small-M solve graphs fuse the conv_out combine + Euler update into the next proj_in (flamed_tune
     # fuse_euler; 25 launches per step): the timing graph then has no combine launches (class cost 0)
     fused = ms[N_CLASSES - 1] <= 0.0
@@ -732,22 +860,24 @@ def main():
 
     audio_s = T * 200 / 16000.0
     value = world * B * T / sec
+    cfg_i, label = workload_label(args, world)
+    label += " (one persistent launch per solve)" if persist_runs >= args.steps else " (hipGraph Euler solve)"
     line = {
         "metric": "latent frames/s (RTF at nsteps-denoiser=128)", "value": round(value, 2),
         "unit": "latent frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(sec * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.dtype, "data": "synthetic (seeded random-init weights, N(0,1) condition/speaker)",
-        "config": {"workload": f"BASELINE configs[1]: {B} utterance(s) x {T} frames ({audio_s:.1f} s audio) per GPU, "
-                               f"nsteps-denoiser={nfe}, hipGraph Euler solve",
+        "config": {"workload": label, "baseline_config": cfg_i,
                    "batch_per_gpu": B, "frames": T, "nfe": nfe, "global_batch": world * B,
                    "parallelism": f"utterance-sharded x{world} (no collectives)"},
+        "per_rank_frames_per_s": per_rank, "scaling_detail": eff, "configs3": configs3,
         "rtf_denoiser": round(sec / audio_s, 6),
         "roofline": roof,
         "kernels": [{k: v for k, v in kk.items() if k not in ("bytes", "flops")} for kk in kernels],
         "kernel_timing": "graph-of-launches path (B > 1, and the B = 1 fallback): in-graph per-launch cost "
                          "(4-step graph with the class doubled minus as captured, HIP events)",
         "persistent": {"runs": persist_runs, "solves": args.steps,
-                       "launch_ms": [round(x, 3) for x in pms] if persist_runs else None},
+                       "launch_ms": [round(x, 3) for x in pms] if pms else None},
         "step_us_graph": round(ms[N_CLASSES] * 1e3, 2),
         "cpu_baseline": cpu,
         "peaks": {"hbm_spec_GBps": HBM_PEAK_GBS, "bf16_dense_spec_TFs": MFMA_PEAK_TFS["bf16"], **(peaks or {})},

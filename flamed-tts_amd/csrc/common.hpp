@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -36,13 +37,49 @@ enum Status : int {
     }                                                                                    \
   } while (0)
 
-// Destroy a cached graph exec that earlier calls may still have in flight (re-capture on a changed key,
-// handle reload or destroy): drain the device first.  The exec owns the replay's kernel-argument and
-// node storage; freeing it under a queued replay is a use-after-free in the runtime.  Re-captures are
-// rare (new shapes / buffers / knobs), so the full drain costs nothing on the steady path.
+// Completion events of cached graph execs: note_graph_use records one after a call's last replay of an exec
+// (outside stream capture), retire_graph waits for it before destroying the exec.  The exec owns the
+// replay's kernel-argument and node storage; freeing it under a queued replay is a use-after-free in the
+// runtime.  Waiting on that exec's own event (not hipDeviceSynchronize) leaves other streams and any
+// concurrent global-mode capture alone.
+struct GraphEvents {
+  std::mutex mu;
+  std::map<hipGraphExec_t, hipEvent_t> ev;
+};
+inline GraphEvents& graph_events() {
+  static GraphEvents g;
+  return g;
+}
+inline void note_graph_use(hipGraphExec_t ex, hipStream_t st) {
+  if (!ex) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;  // nested in a capture
+  GraphEvents& g = graph_events();
+  std::lock_guard<std::mutex> lk(g.mu);
+  hipEvent_t& e = g.ev[ex];
+  if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    e = nullptr;
+    (void)hipStreamSynchronize(st);  // no event: fall back to draining this stream
+    return;
+  }
+  (void)hipEventRecord(e, st);
+}
 inline void retire_graph(hipGraphExec_t& ex) {
   if (!ex) return;
-  (void)hipDeviceSynchronize();
+  hipEvent_t e = nullptr;
+  {
+    GraphEvents& g = graph_events();
+    std::lock_guard<std::mutex> lk(g.mu);
+    auto it = g.ev.find(ex);
+    if (it != g.ev.end()) {
+      e = it->second;
+      g.ev.erase(it);
+    }
+  }
+  if (e) {
+    (void)hipEventSynchronize(e);
+    (void)hipEventDestroy(e);
+  }
   (void)hipGraphExecDestroy(ex);
   ex = nullptr;
 }
@@ -136,6 +173,7 @@ struct Tune {
   int dwgn_small = 1;      // small-M bf16 path: one-workgroup-per-8-channels depthwise conv + GroupNorm (T <= 576)
   int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in
   int persist = 1;         // B = 1 bf16 solves: one persistent launch for all steps (persist.hpp)
+  int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_opt = 585;   // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
                            // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms)

@@ -1587,17 +1587,41 @@ struct Den {
   static constexpr int kSplitCounters = 16384;
   int* gcnt = nullptr;  // fused GroupNorm-finalize counters, one per (utterance, 64-channel group)
   static constexpr int kGnCounters = 65536;
-  // persistent B = 1 solve (persist.hpp): scratch (counters first), pinned error word, device verdict
+  // persistent B = 1 solve (persist.hpp): scratch (counters first), device verdict, failure bookkeeping
   char* pmem = nullptr;
-  int* perr_host = nullptr;
+  int* pfail = nullptr;      // device: failed persistent launches so far (sticky, written by the kernel)
+  int* pfail_host = nullptr; // pinned copy of it, refreshed asynchronously after every uncaptured launch
+  int pfails_seen = 0;       // failures the host has acted on
+  static constexpr int kPersistRetry = 3;  // failed launches before the handle gives up the persistent path
   int pdev_ok = -1;          // 1: 256 CUs and one 256-thread workgroup per CU fits; 0: not on this device
-  bool pbroken = false;      // a persistent solve timed out on this handle: launch path from then on
-  int pruns = 0;             // persistent launches completed
-  float plast_ms = 0.f;      // device time of the last one (HIP events around the kernel)
-  hipEvent_t pev[2] = {nullptr, nullptr};
+  bool pbroken = false;      // kPersistRetry launches failed on this handle: launch path from then on
+  int pruns = 0;             // persistent launches enqueued
+  int ppath = -1;            // path of the solve whose step 0 ran last: 1 persistent, 0 graph of launches
+  int ppath_key[3] = {-1, -1, -1};  // its (B, T, nfe)
+  // device time of the most recent uncaptured persistent launches: a ring of HIP event pairs around the kernel
+  static constexpr int kPRing = 64;
+  hipEvent_t pring[kPRing][2] = {};
+  int pring_n = 0;           // pairs recorded so far (slot = n % kPRing)
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Wait for the last uncaptured persistent launch of the handle (its end event), then free the persistent
+// scratch, the pinned failure word and the timing events (handle destroy / re-load on another device).
+static void persist_release(Den* d) {
+  if (d->pring_n > 0) {
+    hipEvent_t last = d->pring[(d->pring_n - 1) % Den::kPRing][1];
+    if (last) (void)hipEventSynchronize(last);
+  }
+  if (d->pmem) { (void)hipFree(d->pmem); d->pmem = nullptr; }
+  d->pfail = nullptr;
+  if (d->pfail_host) { (void)hipHostFree(d->pfail_host); d->pfail_host = nullptr; }
+  for (auto& pr : d->pring)
+    for (hipEvent_t& e : pr)
+      if (e) { (void)hipEventDestroy(e); e = nullptr; }
+  d->pring_n = 0;
+}
+static int persist_alloc(Den* d, hipStream_t st);
 
 // Active knobs of a handle call: the process defaults (re-snapshotted when flamed_tune moved the epoch)
 // unless flamed_den_tune gave the handle its own.
@@ -1730,10 +1754,7 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
     if (d->ctr) (void)hipFree(d->ctr);
     if (d->scnt) (void)hipFree(d->scnt);
     if (d->gcnt) (void)hipFree(d->gcnt);
-    if (d->pmem) (void)hipFree(d->pmem);
-    if (d->perr_host) (void)hipHostFree(d->perr_host);
-    for (hipEvent_t e : d->pev)
-      if (e) (void)hipEventDestroy(e);
+    persist_release(d);
     if (d->dev) (void)hipFree(d->dev);
   }
   delete d;
@@ -1780,9 +1801,7 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     if (d->ctr) { (void)hipFree(d->ctr); d->ctr = nullptr; }
     if (d->scnt) { (void)hipFree(d->scnt); d->scnt = nullptr; }
     if (d->gcnt) { (void)hipFree(d->gcnt); d->gcnt = nullptr; }
-    if (d->pmem) { (void)hipFree(d->pmem); d->pmem = nullptr; }
-    for (hipEvent_t& e : d->pev)
-      if (e) { (void)hipEventDestroy(e); e = nullptr; }
+    persist_release(d);
     if (d->dev) { (void)hipFree(d->dev); d->dev = nullptr; }
     d->pdev_ok = -1;
   }
@@ -1899,6 +1918,11 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   FL_HIP(hipMemsetAsync(d->scnt, 0, sizeof(int) * Den::kSplitCounters, st));
   if (!d->gcnt) FL_HIP(hipMalloc(&d->gcnt, sizeof(int) * Den::kGnCounters));
   FL_HIP(hipMemsetAsync(d->gcnt, 0, sizeof(int) * Den::kGnCounters, st));
+  if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));  // graph-replay step counter (never allocated inside a capture)
+  if (d->dt == FLAMED_BF16 && !d->f8 && H == pk::kH && C == pk::kC && KS == pk::kTaps && NB <= pk::kMaxNB) {
+    const int prc = persist_alloc(d, st);
+    if (prc) return prc;
+  }
   retire_graph(d->gexec);
   return kOk;
 }
@@ -2161,12 +2185,14 @@ static bool den_fused_ok(const Den* d, int B, int T) {
 // ------------------------------ persistent B = 1 solve (persist.hpp) ------------------------------
 
 // Scratch of the persistent solve, sized for T <= pk::kMaxT: the counters first (the per-launch memset
-// block starts the allocation and is a multiple of 16 B), then the hand-off buffers and a copy of x.
-static size_t persist_layout(char* base, pk::Params* P, float** backup) {
+// block starts the allocation and is a multiple of 16 B), then the sticky failure word (never zeroed by a
+// launch) and the hand-off buffers.
+static size_t persist_layout(char* base, pk::Params* P) {
   size_t off = 0;
   auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off = align256(off + bytes); return p; };
   const size_t T = pk::kMaxT, H = pk::kH, C = pk::kC;
   char* ctr = take(4 * (size_t)pk::kCtrInts);
+  char* fails = take(16);
   char* xp0 = take(T * pk::kSlots * 8);
   char* xp1 = take(T * pk::kSlots * 8);
   char* ximg = take(T * H * 4);
@@ -2176,9 +2202,9 @@ static size_t persist_layout(char* base, pk::Params* P, float** backup) {
   char* xs = take(T * C * 2);
   char* gnp = take((size_t)pk::kGroups * H * 16);
   char* yb = take((size_t)pk::kWGs * 16 * 4);
-  char* bk = take(T * C * 4);
   if (P) {
     P->ctr = reinterpret_cast<int*>(ctr);
+    P->fails = reinterpret_cast<int*>(fails);
     P->xpart[0] = reinterpret_cast<float2*>(xp0);
     P->xpart[1] = reinterpret_cast<float2*>(xp1);
     P->ximg = reinterpret_cast<float*>(ximg);
@@ -2189,33 +2215,65 @@ static size_t persist_layout(char* base, pk::Params* P, float** backup) {
     P->gnp = reinterpret_cast<float4*>(gnp);
     P->yb = reinterpret_cast<float*>(yb);
   }
-  if (backup) *backup = reinterpret_cast<float*>(bk);
   return off;
 }
 
+// Persistent scratch + pinned failure word, allocated once when the handle is loaded (so a solve inside a
+// stream capture never allocates); the failure word starts at 0 and only the kernel writes it after that.
+static int persist_alloc(Den* d, hipStream_t st) {
+  if (d->pmem) return kOk;
+  const size_t bytes = persist_layout(nullptr, nullptr);
+  FL_HIP(hipMalloc(&d->pmem, bytes));
+  FL_HIP(hipMemsetAsync(d->pmem, 0, bytes, st));
+  FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&d->pfail_host), 16, hipHostMallocDefault));
+  *d->pfail_host = 0;
+  d->pfails_seen = 0;
+  return kOk;
+}
+
+static bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
+
+// Failed launches the kernel has counted since the handle's last look (the pinned copy is refreshed by an
+// async copy behind every uncaptured launch, so this never blocks; it may lag one launch).  After
+// kPersistRetry failures the handle stays on the graph-of-launches path.
+static void persist_poll_fails(Den* d) {
+  if (!d->pfail_host) return;
+  const int f = __atomic_load_n(d->pfail_host, __ATOMIC_RELAXED);
+  if (f <= d->pfails_seen) return;
+  d->pfails_seen = f;
+  if (f >= Den::kPersistRetry && !d->pbroken) {
+    d->pbroken = true;
+    fprintf(stderr, "flamed: %d persistent solves failed (output NaN-poisoned); this handle uses the launch path from now on\n", f);
+  } else {
+    fprintf(stderr, "flamed: a persistent solve failed (%d of %d allowed); its output was NaN-poisoned\n", f, Den::kPersistRetry);
+  }
+}
+
 // The persistent solve covers one utterance of 16..512 frames on a bf16 handle with the LayerNorm fold and
-// the shipped dims, on a device where all 256 workgroups are resident at once (one per CU: the grid-wide
-// hand-offs need every producer running), and never inside a stream capture (its error check syncs).
-static bool persist_eligible(Den* d, int B, int T, hipStream_t st) {
+// the shipped dims, on a device where all 256 workgroups are resident at once (one per CU: the cooperative
+// launch checks it again).  Stream capture is allowed: nothing on the call path waits on the device.
+static bool persist_eligible(Den* d, int B, int T) {
   const Tune& tu = tn();
+  persist_poll_fails(d);
   if (!tu.persist || d->pbroken || d->dt != FLAMED_BF16 || d->f8 || !d->fold || !tu.lnfold) return false;
   if (B != 1 || T < 16 || T > pk::kMaxT || d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps)
     return false;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
   if (d->pdev_ok < 0) d->pdev_ok = pk::persist_device_ok(d->device) ? 1 : 0;
   return d->pdev_ok == 1;
 }
 
-// Steps [s0, s1) of a B = 1 solve in one launch.  *done = false: not run (timed out and rolled back, the
-// handle then stays on the launch path) -- the caller runs the launch path.
-static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, int s0, int s1, hipStream_t st, bool* done) {
-  *done = false;
-  if (!d->pmem) FL_HIP(hipMalloc(&d->pmem, persist_layout(nullptr, nullptr, nullptr)));
-  if (!d->perr_host) FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&d->perr_host), sizeof(int), hipHostMallocDefault));
+// Steps [s0, s1) of a B = 1 solve as ONE cooperative launch, enqueued on `st` with no host synchronisation:
+// a zeroed counter block, the kernel, and (outside a capture) HIP events around it plus an async copy of the
+// sticky failure word.  A failed launch NaN-poisons x and is reported by the next call / persist_info.
+static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, int s0, int s1, hipStream_t st) {
+  const bool cap = stream_capturing(st);
+  FL_REQUIRE(d->pmem && d->pfail_host, "persistent solve: scratch not allocated at load");
   pk::Params P{};
-  float* backup = nullptr;
-  persist_layout(d->pmem, &P, &backup);
+  persist_layout(d->pmem, &P);
+  d->pfail = P.fails;
   P.T = T; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
   P.dt = (float)(1.0 / (double)nfe);
   P.mods = mods; P.MS = d->MS; P.MS0 = d->MS0;
@@ -2235,27 +2293,24 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, i
   P.xt = xt;
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
   P.opt = tn().persist_opt;
-  const size_t xbytes = (size_t)T * pk::kC * 4;
-  FL_HIP(hipMemcpyAsync(backup, xt, xbytes, hipMemcpyDeviceToDevice, st));
+  P.inject_step = tn().persist_inject;
   FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pk::kCtrInts, st));
   if (P.opt & 512) FL_HIP(hipMemsetAsync(P.gnp, 0, (size_t)pk::kGroups * pk::kH * 16, st));  // granule tags
-  if (!d->pev[0]) FL_HIP(hipEventCreate(&d->pev[0]));
-  if (!d->pev[1]) FL_HIP(hipEventCreate(&d->pev[1]));
-  FL_HIP(hipEventRecord(d->pev[0], st));
+  hipEvent_t* ev = nullptr;
+  if (!cap) {
+    ev = d->pring[d->pring_n % Den::kPRing];
+    for (int k = 0; k < 2; ++k)
+      if (!ev[k]) FL_HIP(hipEventCreate(&ev[k]));
+    FL_HIP(hipEventRecord(ev[0], st));
+  }
   const int lrc = pk::persist_launch(P, st);
   if (lrc) return lrc;
-  FL_HIP(hipEventRecord(d->pev[1], st));
-  FL_HIP(hipMemcpyAsync(d->perr_host, P.ctr + pk::CT_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
-  FL_HIP(hipStreamSynchronize(st));
-  if (*d->perr_host != 0) {  // a wait timed out: every workgroup left; x is rolled back
-    FL_HIP(hipMemcpyAsync(xt, backup, xbytes, hipMemcpyDeviceToDevice, st));
-    d->pbroken = true;
-    fprintf(stderr, "flamed: persistent solve timed out (T=%d); this handle uses the launch path from now on\n", T);
-    return kOk;
+  if (!cap) {
+    FL_HIP(hipEventRecord(ev[1], st));
+    ++d->pring_n;
+    FL_HIP(hipMemcpyAsync(d->pfail_host, P.fails, sizeof(int), hipMemcpyDeviceToHost, st));
   }
-  *done = true;
   ++d->pruns;
-  FL_HIP(hipEventElapsedTime(&d->plast_ms, d->pev[0], d->pev[1]));
   return kOk;
 }
 
@@ -2309,10 +2364,53 @@ FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, f
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && runs && broken && last_ms, "flamed_den_persist_info: bad args");
   std::lock_guard<std::recursive_mutex> lk(d->mu);
+  DeviceGuard dg(d->device);
+  *last_ms = 0.f;
+  if (d->pring_n > 0) {  // waits for the last uncaptured launch (a diagnostic query, not the call path)
+    hipEvent_t* ev = d->pring[(d->pring_n - 1) % Den::kPRing];
+    FL_HIP(hipEventSynchronize(ev[1]));
+    FL_HIP(hipEventElapsedTime(last_ms, ev[0], ev[1]));
+  }
+  persist_poll_fails(d);
   *runs = d->pruns;
   *broken = d->pbroken ? 1 : 0;
-  *last_ms = d->plast_ms;
   return kOk;
+}
+
+FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && fails, "flamed_den_persist_fails: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  DeviceGuard dg(d->device);
+  *fails = 0;
+  if (!d->pmem) return kOk;
+  pk::Params P{};
+  persist_layout(d->pmem, &P);
+  FL_HIP(hipDeviceSynchronize());  // captured launches leave no event: wait for everything (diagnostic)
+  FL_HIP(hipMemcpy(fails, P.fails, sizeof(int), hipMemcpyDeviceToHost));
+  if (d->pfail_host) __atomic_store_n(d->pfail_host, *fails, __ATOMIC_RELAXED);
+  persist_poll_fails(d);
+  return kOk;
+}
+
+FLAMED_API int flamed_den_persist_times(flamed_den_t h, float* ms, int n) {
+  Den* d = reinterpret_cast<Den*>(h);
+  if (!d || !ms || n < 0) {
+    set_error("flamed_den_persist_times: bad args");
+    return -1;
+  }
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  DeviceGuard dg(d->device);
+  int k = n < d->pring_n ? n : d->pring_n;
+  if (k > Den::kPRing) k = Den::kPRing;
+  for (int i = 0; i < k; ++i) {
+    hipEvent_t* ev = d->pring[(d->pring_n - k + i) % Den::kPRing];
+    if (hipEventSynchronize(ev[1]) != hipSuccess || hipEventElapsedTime(ms + i, ev[0], ev[1]) != hipSuccess) {
+      set_error("flamed_den_persist_times: event query failed");
+      return -1;
+    }
+  }
+  return k;
 }
 
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
@@ -2345,14 +2443,24 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   const int G = graph_chunk(nfe);
   FL_REQUIRE(s0 % G == 0 && (s1 % G == 0 || s1 == nfe), "flamed_den_solve_part: range [%d, %d) not on %d-step graph chunks",
              s0, s1, G);
-  // the parts of one solve must run one step structure: a knob change between parts is rejected
-  if (s0 == 0) d->part_epoch = d->tune_ver;
+  // the parts of one solve must run one step structure: a knob change between parts is rejected, and the
+  // path (one persistent launch per part, or the graph of launches) is decided once, by the step-0 part
+  if (s0 == 0) {
+    d->part_epoch = d->tune_ver;
+    d->ppath = persist_eligible(d, B, T) ? 1 : 0;
+    d->ppath_key[0] = B; d->ppath_key[1] = T; d->ppath_key[2] = nfe;
+  }
   FL_REQUIRE(d->part_epoch == d->tune_ver, "flamed_den_solve_part: knobs changed since step 0 of this solve (part [%d, %d))",
              s0, s1);
-  if (persist_eligible(d, B, T, st)) {  // one persistent launch for the whole range (B = 1)
-    bool done = false;
-    const int prc = persist_solve(d, xt, mods, nfe, T, s0, s1, st, &done);
-    if (prc != kOk || done) return prc;
+  FL_REQUIRE(d->ppath >= 0 && d->ppath_key[0] == B && d->ppath_key[1] == T && d->ppath_key[2] == nfe,
+             "flamed_den_solve_part: part [%d, %d) of a solve whose step-0 part did not run on this handle", s0, s1);
+  if (d->ppath == 1) {  // one persistent launch for the whole range (B = 1)
+    const int prc = persist_solve(d, xt, mods, nfe, T, s0, s1, st);
+    if (prc == kOk || s0 != 0 || prc != kBadArg) return prc;
+    // the runtime refused the cooperative grid (not all 256 workgroups co-resident): this device never
+    // runs the persistent solve; this solve (still at step 0) takes the graph of launches
+    d->pdev_ok = 0;
+    d->ppath = 0;
   }
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
@@ -2392,6 +2500,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
     }
   }
   for (int r = s0 / G; r < s1 / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
+  note_graph_use(d->gexec, st);
   if (fused && s1 == nfe) {  // the last step's combine + Euler update: x_nfe = XP + dt * v (nfe even: XP holds x_{nfe-1})
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, nullptr, B * T, T,
                        d->C, dt, nullptr, w.XP);

@@ -586,16 +586,17 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   }
   FL_HIP(hipMemsetAsync(gp.ctr, 0, 2 * sizeof(int), st));
   for (int r = 0; r < nfe / G; ++r) FL_HIP(hipGraphLaunch(gp.exec, st));
+  note_graph_use(gp.exec, st);
   return kOk;
 }
 
-FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int B, int L) {
+FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int B, int L, hipStream_t st) {
   DurNet* nd = reinterpret_cast<DurNet*>(dur);
   DurNet* ns = reinterpret_cast<DurNet*>(sil);
   FL_REQUIRE(nd && ns && nd->dev && ns->dev && B > 0 && L > 0, "flamed_pva_persist_ready: bad args");
   std::lock_guard<std::mutex> lk(nd->mu);
   FL_ON_DEVICE(nd->device);
-  return pva_persist_eligible(nd, ns, B * L, nullptr) ? 1 : 0;
+  return pva_persist_eligible(nd, ns, B * L, st) ? 1 : 0;
 }
 
 FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms) {

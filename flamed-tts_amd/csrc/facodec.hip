@@ -530,6 +530,7 @@ FLAMED_API int flamed_fac_decode(flamed_fac_t h, const float* latents, const flo
     f->gkey = key;
   }
   FL_HIP(hipGraphLaunch(f->gexec, st));
+  note_graph_use(f->gexec, st);
   return kOk;
 }
 
@@ -906,6 +907,7 @@ FLAMED_API int flamed_enc_encode(flamed_enc_t h, const float* wav, int B, int n,
     e->gkey = key;
   }
   FL_HIP(hipGraphLaunch(e->gexec, st));
+  note_graph_use(e->gexec, st);
   return kOk;
 }
 

@@ -76,10 +76,18 @@ __device__ __forceinline__ void signal(int* ctr) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Abandon the solve: the first workgroup to set the error word also counts the failed launch in the sticky
+// word the host reads later (the per-launch counter block is zeroed before every launch, `fails` is not).
+__device__ __forceinline__ void raise_err(int* err, int* fails, int code) {
+  int expected = 0;
+  if (__hip_atomic_compare_exchange_strong(err, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    __hip_atomic_fetch_add(fails, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Wave 0 polls n counters (base + k * stride, k < n) with sc1 loads until all reach `target` (s_sleep
 // between polls); bounded by P.tmo, and an error word set by any workgroup ends every wait.  The
 // other waves meet it at a barrier.  Returns false when the solve is being abandoned.
-__device__ __forceinline__ bool wait_ge(int* err, long long tmo, int* base, int stride, int n, int target, int* flag) {
+__device__ __forceinline__ bool wait_ge(int* err, int* fails, long long tmo, int* base, int stride, int n, int target, int* flag) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -91,7 +99,7 @@ __device__ __forceinline__ bool wait_ge(int* err, long long tmo, int* base, int 
       if ((it & 31) == 31) {  // the error word and the clock only every 32 polls: one round trip per poll
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
         if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
-          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) raise_err(err, fails, 1);
           ok = false;
           break;
         }
@@ -364,7 +372,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const int slot = __hip_atomic_fetch_add(P.ctr + CT_SLOT + 16 * xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       tk[0] = (int)xcc;
       tk[1] = slot;
-      if (slot >= kSlots) __hip_atomic_store(P.ctr + CT_ERR, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (slot >= kSlots) raise_err(P.ctr + CT_ERR, P.fails, 2);
     }
     __syncthreads();
     g = tk[0];
@@ -399,6 +407,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   int* mygrp = grp + 16 * g;
   int* gnc = P.ctr + CT_GN + 16 * s;
   int* errw = P.ctr + CT_ERR;
+  int* fails = P.fails;
   const long long tmo = P.tmo;
   int L = 0;    // group signals so far (the same sequence in every workgroup)
   int ndg = 0;  // GroupNorm hand-offs so far
@@ -408,7 +417,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   int pst_k = 0;
 #endif
   // after a GEMM phase: the next GEMM's panel goes into the buffer the finished one did not use
-  int cur_step = P.s0;  // (FL_STAMPS builds: the step a helper lambda stamps)
+  [[maybe_unused]] int cur_step = P.s0;  // (FL_STAMPS builds: the step a helper lambda stamps)
   const bool fastdma = !(P.opt & 256);  // persist_opt 256: the generic issue loop (A/B)
   const bool w4 = (P.opt & 1) != 0;
   auto next_w = [&](const bf16* W) {
@@ -453,6 +462,14 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     xs0 = P.xt[(size_t)(r0 + xr_row) * kC + xch];
     xs1 = P.xt[(size_t)(r0 + xr_row) * kC + xch + 1];
   }
+  // An abandoned solve leaves NaN in this workgroup's part of x (every workgroup leaves through here or
+  // finishes normally), so a failure can never pass for a result.
+  auto fail_exit = [&]() {
+    if (xr_row < nr) {
+      P.xt[(size_t)(r0 + xr_row) * kC + xch] = __builtin_nanf("");
+      P.xt[(size_t)(r0 + xr_row) * kC + xch + 1] = __builtin_nanf("");
+    }
+  };
   // weights of the first GEMM (proj_in) while the state is published
   dma_panel<kC>(smem, [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane, P.opt);
   // bf16 rows of x (proj_in's operand): 16 B per tile row, staged in LDS
@@ -488,13 +505,18 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   for (int step = P.s0; step < P.s1; ++step) {
     const float* md = P.mods + (size_t)step * P.MS;
     cur_step = step;
+    if (step == P.inject_step) {  // diagnostic failure injection: every workgroup abandons here
+      if (tid == 0) raise_err(errw, fails, 3);
+      fail_exit();
+      return;
+    }
 #ifdef FL_STAMPS
     pst_k = 0;
 #endif
     // ------------------------------ proj_in (:361) ------------------------------
     const float binv[2] = {P.bin[col0 + c], P.bin[col0 + 16 + c]};
     PST(step);
-    if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
     PST(step);
     gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     PST(step);
@@ -525,7 +547,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
       // -------- LN + modulate + depthwise k31 + GroupNorm(H, H) over T (prob_generator.py:81-89, 153-156)
       PST(step);
-      if (!wait_ge(errw, tmo, grp, 16, kGroups, 32 * L, flag)) return;  // every group: the halo rows of the neighbours
+      if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
       const int wa = max(r0 - kHalo, 0), wz = min(r0 + nr + kHalo, T);
       const int cc = tid & 31, rg = tid >> 5;
@@ -668,7 +690,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
             if ((it & 31) == 31) {
               if (__hip_atomic_load(errw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
               if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
-                if (tid == 0) __hip_atomic_store(errw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tid == 0) raise_err(errw, fails, 1);
                 ok = false;
                 break;
               }
@@ -691,10 +713,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         __syncthreads();
         const bool okw = *flag != 0;
         __syncthreads();
-        if (!okw) return;
+        if (!okw) { fail_exit(); return; }
         PST(step);
       } else {
-      if (!wait_ge(errw, tmo, gnc, 0, 1, kGroups * ndg, flag)) return;
+      if (!wait_ge(errw, fails, tmo, gnc, 0, 1, kGroups * ndg, flag)) { fail_exit(); return; }
       PST(step);
       if (tid < kCols) {  // the 8 groups' partials of this channel, Chan-combined in group order
         const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
@@ -725,7 +747,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       // -------- conv_2 (1x1) + GELU (:90-91)
       const float b2v[2] = {bw.b2[col0 + c], bw.b2[col0 + 16 + c]};  // epilogue vectors before the wait
       PST(step);
-      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
       PST(step);
       gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
@@ -757,7 +779,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         alv[nt] = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
       }
       PST(step);
-      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
       PST(step);
       gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
@@ -790,7 +812,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const float* fo0 = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
       const float fa0[2] = {fo0[col0 + c], fo0[col0 + 16 + c]}, fb0[2] = {fo0[H + col0 + c], fo0[H + col0 + 16 + c]};
       PST(step);
-      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
       PST(step);
       row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
       gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);  // (its barrier orders the statistics)
@@ -818,7 +840,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       // -------- mlp.2 + gated residual (:159-160)
       const float g2v[2] = {mb[5 * H + col0 + c], mb[5 * H + col0 + 16 + c]}, bm2[2] = {bw.mb2[col0 + c], bw.mb2[col0 + 16 + c]};
       PST(step);
-      if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
       PST(step);
       gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
@@ -852,7 +874,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
     }
     PST(step);
-    if (!wait_ge(errw, tmo, mygrp, 0, 1, 32 * L, flag)) return;
+    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
     PST(step);
     row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
     gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
@@ -884,7 +906,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
     // -------- Euler update x += dt * v, v[t] = b + Y1[t] + Y0[t-1] + Y2[t+1] (:445; conv3_combine order)
     PST(step);
-    if (!wait_ge(errw, tmo, grp, 16, kGroups, 32 * L, flag)) return;
+    if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag)) { fail_exit(); return; }
     PST(step);
     if (xr_row < nr) {
       const int t = r0 + xr_row;
@@ -951,8 +973,17 @@ int persist_launch(const Params& Pin, hipStream_t st) {
   P.pst = g_pst_buf;
   P.pst_step = g_pst_step;
 #endif
-  hipLaunchKernelGGL(den_persist_kernel, dim3(kWGs), dim3(kThreads), kLds, st, P);
-  FL_LAUNCH_CHECK();
+  // Cooperative: the runtime checks the grid against the kernel's occupancy and rejects it up front
+  // (hipErrorCooperativeLaunchTooLarge) instead of queueing workgroups behind resident ones that wait for
+  // them.  Capturable: a captured cooperative launch replays cooperatively (MI355X_MICROARCH.md, Residency).
+  void* args[] = {&P};
+  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(den_persist_kernel), dim3(kWGs), dim3(kThreads),
+                                                  args, kLds, st);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("persistent solve: hipLaunchCooperativeKernel -> %s", hipGetErrorString(e));
+    return e == hipErrorCooperativeLaunchTooLarge ? kBadArg : kHip;
+  }
   return kOk;
 }
 

@@ -26,8 +26,11 @@
 // GroupNorm, conv_2, conv_3, conv_out), Euler update.  Numerics follow the bf16 launch path (bf16
 // operands, fp32 accumulation / residual / statistics / state, the LayerNorm fold of mlp.0 and
 // conv_out); GroupNorm statistics are exact per group (two passes) and Chan-combined across the 8
-// groups in a fixed order (deterministic).  Every spin is bounded (timeout -> error word -> every
-// workgroup exits); the host then restores x and runs the launch path.
+// groups in a fixed order (deterministic).  The grid is launched cooperatively (hipLaunchCooperativeKernel:
+// all 256 workgroups co-resident, or the launch fails up front), so no wait depends on a workgroup that
+// is not running.  Every spin is still bounded: a timeout sets the error word, every workgroup leaves and
+// writes NaN into its part of x (a failed solve is loud, never silently wrong), and the first to set the
+// word adds one to a sticky failure count the host reads after the fact (no host sync on the call path).
 #pragma once
 #include "common.hpp"
 
@@ -81,6 +84,8 @@ struct Params {
   float4* gnp;             // GroupNorm partials (n, mean, M2) per (group, channel): 8 x H
   float* yb;               // conv_out boundary rows per workgroup: Y0 of its last row, Y2 of its first
   int* ctr;
+  int* fails;              // failed launches so far (sticky across launches: the host reads it after the fact)
+  int inject_step = -1;    // diagnostic (flamed_tune persist_inject): every workgroup fails at this step
   long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
   int opt = 0;                        // experiment bits (flamed_tune persist_opt)
   unsigned long long* pst = nullptr;  // FL_STAMPS builds: timeline of step pst_step (persist_timeline.py)

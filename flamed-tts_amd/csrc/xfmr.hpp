@@ -517,6 +517,7 @@ static int with_graph(CapGraph& g, const std::vector<const void*>& key_in, bool 
     g.key = key;
   }
   FL_HIP(hipGraphLaunch(g.exec, st));
+  note_graph_use(g.exec, st);
   return kOk;
 }
 

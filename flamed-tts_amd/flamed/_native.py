@@ -37,6 +37,8 @@ SIGNATURES = {
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_den_solve_chunk": (c_int, [P, c_int]),
     "flamed_den_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_float)]),
+    "flamed_den_persist_fails": (c_int, [P, ctypes.POINTER(c_int)]),
+    "flamed_den_persist_times": (c_int, [P, ctypes.POINTER(c_float), c_int]),
     "flamed_den_solve_part": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, c_int, c_int, P]),
     "flamed_den_time_kernels_graph": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),
@@ -53,7 +55,7 @@ SIGNATURES = {
     "flamed_pva_workspace_size": (c_size_t, [P, c_int, c_int, c_int]),
     "flamed_pva_flow": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_pva_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_float)]),
-    "flamed_pva_persist_ready": (c_int, [P, P, c_int, c_int]),
+    "flamed_pva_persist_ready": (c_int, [P, P, c_int, c_int, P]),
     "flamed_lr_lengths": (c_int, [P, P, P, c_int, c_int, c_int, P, P, P]),
     "flamed_lr_expand": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "flamed_fac_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), c_int, ctypes.POINTER(P)]),

@@ -464,14 +464,29 @@ class DenoiserHIP:
         return v.to(x.dtype)
 
     def persist_info(self, with_ms: bool = False):
-        """(completed persistent launches, broken[, device ms of the last launch]) of this handle: whether
-        B = 1 solves ran as one persistent launch (flamed_den_persist_info)."""
+        """(persistent launches enqueued, broken[, device ms of the last uncaptured launch]) of this handle:
+        whether B = 1 solves ran as one persistent launch (flamed_den_persist_info; waits for that launch)."""
         runs, broken, ms = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_float(0.0)
         nat.check(nat.lib().flamed_den_persist_info(self.handle, ctypes.byref(runs), ctypes.byref(broken), ctypes.byref(ms)),
                   "flamed_den_persist_info")
         if with_ms:
             return runs.value, bool(broken.value), float(ms.value)
         return runs.value, bool(broken.value)
+
+    def persist_fails(self) -> int:
+        """Failed (NaN-poisoned) persistent launches so far on this handle (diagnostic: waits for the device)."""
+        f = ctypes.c_int(0)
+        nat.check(nat.lib().flamed_den_persist_fails(self.handle, ctypes.byref(f)), "flamed_den_persist_fails")
+        return f.value
+
+    def persist_times(self, n: int) -> List[float]:
+        """Device ms of the up to n most recent uncaptured persistent launches, oldest first (HIP events
+        around each kernel on its launch stream; flamed_den_persist_times)."""
+        buf = (ctypes.c_float * max(n, 1))()
+        k = nat.lib().flamed_den_persist_times(self.handle, buf, n)
+        if k < 0:
+            nat.check(-1, "flamed_den_persist_times")
+        return [float(buf[i]) for i in range(k)]
 
     def solve(self, xt: torch.Tensor, ts: torch.Tensor, spk: torch.Tensor, nfe: int) -> torch.Tensor:
         """Full Euler solve; returns a new (B,T,C) fp32 tensor."""

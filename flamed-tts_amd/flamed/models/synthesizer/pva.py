@@ -290,7 +290,8 @@ class PvaHIP:
         self._ensure(dev)
         B, L, D = x.shape
         Lb = nat.lib()
-        if self.pva.hip_graph and Lb.flamed_pva_persist_ready(self.handles[0], self.handles[1], B, L) == 1:
+        if self.pva.hip_graph and Lb.flamed_pva_persist_ready(self.handles[0], self.handles[1], B, L,
+                                                              nat.stream_ptr(dev)) == 1:
             # one persistent launch, no captured graph keyed on buffer addresses: the caller's tensors go in
             # directly (the bool mask's bytes are the uint8 the kernel reads) and the states are flowed in
             # place in fresh copies (the op returns new tensors)
@@ -298,7 +299,10 @@ class PvaHIP:
             mask = src_mask.contiguous()
             if mask.dtype not in (torch.bool, torch.uint8):
                 mask = mask.to(torch.uint8)
-            d, s = dur_t.float().clone(), sil_t.float().clone()
+            # contiguous copies: the kernel indexes the states flat (r = b L + l); clone() would keep the
+            # strides of a dense non-contiguous input (preserve_format)
+            d = dur_t.float().clone(memory_format=torch.contiguous_format)
+            s = sil_t.float().clone(memory_format=torch.contiguous_format)
             tsc = ts.float().contiguous()
             ws = self.ws.get(Lb.flamed_pva_workspace_size(self.handles[0], B, L, nfe), dev)
             nat.check(Lb.flamed_pva_flow(self.handles[0], self.handles[1], nat.ptr(enc), nat.ptr(mask), nat.ptr(d),

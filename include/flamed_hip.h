@@ -7,7 +7,8 @@
  *
  * Conventions: every tensor argument is a DEVICE pointer owned by the caller, row-major, fp32
  * unless stated; work is enqueued on `stream` and is stream-ordered (no host synchronisation
- * inside, so every call is hipGraph-capturable except the *_load / *_create calls).  Scratch memory
+ * inside, so every call is hipGraph-capturable except the *_load / *_create calls and the documented
+ * diagnostic queries; flamed_pva_flow's persistent launch waits for its error word).  Scratch memory
  * comes from a caller-provided workspace sized by the matching *_workspace_size query.
  * Handles: *_load copies or packs every weight and vector into the handle's own device arena (the
  * caller's tensors may be freed afterwards) on the device those tensors live on; each call on a
@@ -108,11 +109,20 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
                                      size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t stream);
 /* The persistent B = 1 solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken
  * by flamed_den_solve / _solve_part with use_graph != 0 for one utterance of 16..512 frames on a bf16
- * handle): *runs = launches completed on this handle, *broken = 1 once a launch timed out (the handle
- * then stays on the graph-of-launches path), *last_ms = device time of the last persistent launch (HIP
- * events around the kernel on the launch stream).  The solve checks its error word before returning (a
- * stream sync), so it is never taken inside a stream capture. */
+ * handle; decided once per solve by its step-0 part, and later parts follow it).  The launch is
+ * cooperative (all workgroups co-resident or refused up front, then this device uses the graph of launches)
+ * and is only ENQUEUED: no host synchronisation, so it may be captured into a hipGraph (the captured node
+ * replays cooperatively).  A launch whose in-kernel wait times out leaves NaN in xt and adds one to a sticky
+ * device failure count that later calls read asynchronously; after 3 failures the handle uses the graph of
+ * launches.  flamed_den_persist_info: *runs = persistent launches enqueued on this handle, *broken = 1 once
+ * it has given up the persistent path, *last_ms = device time of the last uncaptured launch (HIP events
+ * around the kernel on the launch stream; waits for it). */
 FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, float* last_ms);
+/* (diagnostic) failed persistent launches so far on this handle (waits for the device to be idle). */
+FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails);
+/* Device times (ms, oldest first) of the up to n most recent uncaptured persistent launches (a ring of 64
+ * HIP event pairs; waits for them); returns how many were written, -1 on error. */
+FLAMED_API int flamed_den_persist_times(flamed_den_t h, float* ms, int n);
 
 /* Kernel classes of an Euler step (flamed_den_time_kernels_graph): 0 proj_in GEMM, 1 LN/mod +
  * depthwise conv (+ GroupNorm partials, + finalize by the last-arriving T-chunk), 2 standalone GroupNorm
@@ -165,6 +175,10 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "fuse_euler"    — 1 (default): small-M solve graphs compute the conv_out tap combine + Euler
  *                     update inside the next step's proj_in A loader (25 launches per step, state
  *                     ping-ponged through the workspace); 0: separate combine kernel (26);
+ *   "persist"       — 1 (default): B = 1 bf16 solves run as one persistent cooperative launch;
+ *   "persist_opt"   — persistent kernel variant bits (diagnostic A/B; default 585);
+ *   "persist_inject"— diagnostic: every persistent launch fails at this step (-1 default = never), to
+ *                     exercise the NaN poisoning / failure count / retry budget;
  *   "pva_split"     — 1: the PVA nets' small-M exact-fp32 GEMMs split K over workgroups
  *                     (per-handle slabs, fixed slice order: deterministic); 0 (default: measured
  *                     no faster): one K chain;
@@ -228,9 +242,10 @@ FLAMED_API size_t flamed_pva_workspace_size(flamed_dur_t h, int B, int L, int nf
 FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* enc, const uint8_t* mask, float* dur_t,
                                float* sil_t, const float* ts, int nfe, int B, int L, void* ws, size_t ws_bytes,
                                int use_graph, hipStream_t stream);
-/* 1 when a flamed_pva_flow(use_graph != 0) of B x L rows on this pair would run as the persistent launch
- * (the caller may then pass its own buffers: no graph keyed on their addresses), 0 otherwise. */
-FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int B, int L);
+/* 1 when a flamed_pva_flow(use_graph != 0) of B x L rows on this pair, on `stream` (its capture state
+ * counts), would run as the persistent launch (the caller may then pass its own buffers: no graph keyed on
+ * their addresses), 0 otherwise. */
+FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int B, int L, hipStream_t stream);
 /* (diagnostic) persistent PVA flows completed on the duration handle, whether one timed out (the pair
  * then stays on the graph path), device ms of the last one. */
 FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms);
@@ -332,8 +347,11 @@ FLAMED_API int flamed_prior_decode(flamed_prior_t h, const float* x, const uint8
                                    int B, int T, int P, const float* pos, float* embs, float* logits, void* ws,
                                    size_t ws_bytes, int use_graph, hipStream_t stream);
 /* Operand type of the decoder-side GEMMs (bridge, shared decoder, per-quantizer decoders, head):
- * FLAMED_F32 (default: exact fp32 MFMA) or FLAMED_BF16 (bf16 operands, fp32 accumulation; the weights
- * are converted once on the first bf16 decode).  The encoder always runs fp32 (it feeds the durations). */
+ * FLAMED_F32 (the C default: exact fp32 MFMA) or FLAMED_BF16 (bf16 operands, fp32 accumulation; the weights
+ * are converted once on the first bf16 decode).  The encoder always runs fp32 (it feeds the durations).
+ * The Python package (flamed/models/synthesizer/prior_generator.py, PriorGenerator.hip_dec_dtype) calls this
+ * with FLAMED_BF16 by default; its end-to-end output is checked against the reference Flamed.sample_batch
+ * fixture (tests/test_flamed_gpu.py, bf16: prior embeddings and latents rel-L2 <= 2e-2, tgt_mask exact). */
 FLAMED_API int flamed_prior_set_dtype(flamed_prior_t h, int dtype);
 
 /* ============== prompt-side quantizers + timbre encoder (once per prompt) ==============

@@ -40,3 +40,27 @@ def test_world_mismatch_rejected():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--plumbing"], capture_output=True,
                        text=True, timeout=300, env=env, cwd=REPO)
     assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+def test_launcher_world2_configs3_labels():
+    """a multi-rank run is labelled as the configs[3] layout with its global batch, every
+    rank's own frames/s and the efficiency against rank 0 running the same per-GPU workload alone."""
+    line = _run(["--gpus", "2", "--plumbing", "--config", "3", "--batch", "4", "--frames", "12", "--nfe", "2",
+                 "--steps", "1", "--warmup", "1"])
+    cfg = line["config"]
+    assert "configs[3]" in cfg["workload"] and "utterance-sharded over 2 GPU" in cfg["workload"], cfg["workload"]
+    assert cfg["global_batch"] == 8 and cfg["batch_per_gpu"] == 4
+    per = line["per_rank_frames_per_s"]
+    assert len(per) == 2 and all(v > 0 for v in per)
+    eff = line["scaling_detail"]
+    assert eff["solo_rank0_frames_per_s"] > 0 and 0.0 < eff["efficiency_vs_n1"] < 4.0
+    assert abs(line["value"] - 2 * 4 * 12 / (line["ms_per_step"] / 1e3)) / line["value"] < 1e-2
+
+
+def test_single_rank_labels():
+    """One rank: B = 1 is labelled configs[1]; --config 2 at a reduced size names configs[2] and says so."""
+    one = _run(["--plumbing", "--steps", "1", "--warmup", "1", "--frames", "8", "--nfe", "2"])
+    assert "configs[1]" in one["config"]["workload"] and one["scaling_detail"] is None
+    two = _run(["--plumbing", "--config", "2", "--batch", "2", "--frames", "8", "--nfe", "2", "--steps", "1", "--warmup", "1"])
+    assert "configs[2]" in two["config"]["workload"] and "non-reference size" in two["config"]["workload"]
+    assert two["config"]["global_batch"] == 2

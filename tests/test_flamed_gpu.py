@@ -59,3 +59,33 @@ def test_sample_raw_prompt_gpu():
                    codec_decoder=dec, temp_durgen=0.3, temp_denoiser=0.3, nsteps_durgen=4, nsteps_denoiser=4)
     assert res["wav"].shape == g["wav"].shape
     assert rel_l2(res["wav"], g["wav"]) < 2e-3
+
+
+def test_end_to_end_duration_flips_vs_oracle():
+    """the integer durations of an end-to-end run at the bench's 5 s utterance size
+    (L = 285 phonemes, --nsteps-durgen 64) from the HIP prior encoder's output: the HIP PVA flow against
+    the oracle's restatement of PVA.sample's Euler loop (pva.py:97-109) on the same encoder output and the
+    same CPU-RNG noise.  Zero frame flips away from .5 rounding boundaries (pva.py:111-112); log-durations
+    rel-L2 <= 1e-5."""
+    from _common import orc
+    m, _ = build_flamed(DEV, "bf16")
+    pr = m.prior_generator
+    L, nfe = 285, 64
+    phon = torch.randint(1, 300, (1, L), generator=torch.Generator().manual_seed(1234)).to(DEV)
+    smask = torch.zeros(1, L, dtype=torch.bool, device=DEV)
+    with torch.inference_mode():
+        enc = pr.hip().encode(phon, smask)
+        torch.manual_seed(0)
+        d_g, s_g = pr.pva.flow(enc, smask, nfe, 0.3)
+    sd = {"prior_generator.pva." + k: v.detach().float().cpu() for k, v in pr.pva.state_dict().items()}
+    torch.manual_seed(0)
+    d_c, s_c = orc.pva_flow(sd, enc.float().cpu(), smask.cpu(), nfe, 0.3)
+    assert rel_l2(d_g.cpu(), d_c) < 1e-5 and rel_l2(s_g.cpu(), s_c) < 1e-5
+    near, flips = 0, 0
+    for got, ref in ((d_g.cpu(), d_c), (s_g.cpu(), s_c)):
+        e = torch.exp(ref) - 1
+        safe = (e - e.floor() - 0.5).abs() > 1e-4
+        near += int((~safe).sum())
+        flips += int((orc.log_to_frames(got)[safe] != orc.log_to_frames(ref)[safe]).sum())
+    print(f"end-to-end L=285 nfe=64: duration flips {flips} of {2 * L}, near a .5 boundary {near}")
+    assert flips == 0

@@ -56,7 +56,7 @@ def _solve(pg, x0, spk, nfe):
 
 def _runs(pg):
     runs, broken = pg.denoiser.hip().persist_info()
-    assert not broken, "a persistent solve timed out and was rolled back"
+    assert not broken, "the handle gave up the persistent path (failed launches)"
     return runs
 
 
@@ -150,3 +150,127 @@ def test_persist_variants_bitwise(pgb, T, opt):
         b = _solve(pg, x0, spk, 8)
     assert _runs(pg) == r0 + 2
     assert torch.equal(a, b)
+
+
+def test_persist_enqueue_is_async(pgb):
+    """The C-ABI contract (include/flamed_hip.h conventions; SURVEY.md §8(b) threading row): the persistent solve
+    is only enqueued.  Two back-to-back configs[1] solves return to the host while the device is still busy
+    (no hipStreamSynchronize on the call path), and both give the same (deterministic) result."""
+    pg, _ = pgb
+    hip = pg.denoiser.hip()
+    x0, spk = _inputs(21, 1, 400)
+    ts = torch.linspace(0, 1, 129, device=DEV)
+    xd, sd_ = x0.to(DEV), spk.to(DEV)
+    import time
+    with torch.inference_mode():
+        hip.solve(xd, ts, sd_, 128)  # warm: buffers, workspace, modulation table
+        torch.cuda.synchronize()
+        r0 = _runs(pg)
+        t0 = time.perf_counter()
+        a = hip.solve(xd, ts, sd_, 128)
+        b = hip.solve(xd, ts, sd_, 128)
+        host_ms = (time.perf_counter() - t0) * 1e3
+        pending = not torch.cuda.current_stream().query()
+        torch.cuda.synchronize()
+    dev_ms = hip.persist_times(2)
+    print(f"two persistent solves: host {host_ms:.2f} ms to enqueue, device {dev_ms} ms, pending after enqueue: {pending}")
+    assert _runs(pg) == r0 + 2
+    assert len(dev_ms) == 2 and host_ms < dev_ms[0]
+    assert pending
+    assert torch.equal(a, b) and torch.isfinite(a).all()
+
+
+def test_persist_failure_poisons_and_retry_budget(pgb):
+    """A persistent launch that gives up (forced by the diagnostic knob persist_inject: every workgroup abandons
+    at that step) leaves NaN in x instead of a silently wrong result and is counted; the handle keeps the
+    persistent path for 3 failures, then uses the graph of launches, whose result equals the launch path's.
+    A fresh handle, so the module's shared handle stays on the persistent path."""
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
+    pg, _ = pgb
+    h = DenoiserHIP(pg.denoiser, "bf16")
+    x0, spk = _inputs(22, 1, 96)
+    ts = torch.linspace(0, 1, 9, device=DEV)
+    with torch.inference_mode():
+        with knob("persist_inject", 3, -1):
+            for k in range(1, 4):
+                out = h.solve(x0.to(DEV), ts, spk.to(DEV), 8)
+                assert torch.isnan(out).all(), "a failed persistent solve must be NaN-poisoned"
+                assert h.persist_fails() == k
+        runs, broken = h.persist_info()
+        assert runs == 3 and broken, (runs, broken)
+        ok = h.solve(x0.to(DEV), ts, spk.to(DEV), 8)
+        assert h.persist_info()[0] == 3, "after the retry budget the handle must not launch persistently"
+        with knob("persist", 0, 1):
+            ref = pg.denoiser.hip().solve(x0.to(DEV), ts, spk.to(DEV), 8)
+    assert torch.isfinite(ok).all() and torch.equal(ok, ref)
+
+
+def test_persist_single_failure_then_recovers(pgb):
+    """One failure is reported (fails = 1, not broken) and the next solve on the same handle is persistent and
+    correct (it equals a solve on a handle that never failed)."""
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
+    pg, _ = pgb
+    h = DenoiserHIP(pg.denoiser, "bf16")
+    x0, spk = _inputs(23, 1, 131)
+    ts = torch.linspace(0, 1, 9, device=DEV)
+    with torch.inference_mode():
+        with knob("persist_inject", 0, -1):
+            bad = h.solve(x0.to(DEV), ts, spk.to(DEV), 8)
+        assert torch.isnan(bad).all()
+        good = h.solve(x0.to(DEV), ts, spk.to(DEV), 8)
+        ref = pg.denoiser.hip().solve(x0.to(DEV), ts, spk.to(DEV), 8)
+    runs, broken = h.persist_info()
+    assert h.persist_fails() == 1 and not broken and runs == 2
+    assert torch.equal(good, ref)
+
+
+def test_persist_graph_capture(pgb):
+    """The persistent solve inside a torch.cuda.graph capture (a caller capturing ProbGenerator.sample's solve):
+    the cooperative launch is captured, the replay runs it, and the result equals the eager persistent solve
+    bitwise."""
+    pg, _ = pgb
+    hip = pg.denoiser.hip()
+    x0, spk = _inputs(24, 1, 257)
+    ts = torch.linspace(0, 1, 17, device=DEV)
+    xd, sd_ = x0.to(DEV), spk.to(DEV)
+    with torch.inference_mode():
+        eager = hip.solve(xd, ts, sd_, 16)
+        torch.cuda.synchronize()
+        r0 = _runs(pg)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            hip.solve(xd, ts, sd_, 16)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = hip.solve(xd, ts, sd_, 16)
+        assert _runs(pg) == r0 + 2, "the captured solve did not take the persistent path"
+        g.replay()
+        torch.cuda.synchronize()
+        first = out.clone()
+        g.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(first, eager) and torch.equal(out, eager)
+
+
+def test_solve_part_without_step0_rejected(pgb):
+    """a later part of a solve whose step-0 part never ran on the handle (or ran for another shape)
+    is rejected instead of reading a stale step counter / uninitialised state."""
+    from flamed import _native as nat
+    pg, _ = pgb
+    hip = pg.denoiser.hip()
+    L = nat.lib()
+    nfe, T = 32, 77
+    x0, spk = _inputs(25, 1, T)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        G = L.flamed_den_solve_chunk(hip.handle, nfe)
+        r = torch.arange(nfe, device=DEV)
+        mods = hip.adaln(ts[:nfe], spk.to(DEV), r.to(torch.int32), torch.zeros(nfe, dtype=torch.int32, device=DEV))
+        x = x0.to(DEV).contiguous()
+        ws = nat.Workspace().get(L.flamed_den_workspace_size(hip.handle, 1, T), DEV)
+        rc = L.flamed_den_solve_part(hip.handle, nat.ptr(x), nat.ptr(mods), nfe, 1, T, nat.ptr(ws), ws.numel(), 1, G, nfe,
+                                     nat.stream_ptr(DEV))
+    assert rc == 1001
