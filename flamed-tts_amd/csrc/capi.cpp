@@ -88,6 +88,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"persist", &Tune::persist, 0, 1, nullptr},
       {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
+      {"persist_capmode", &Tune::persist_capmode, 0, 1, nullptr},
       {"pva_persist", &Tune::pva_persist, 0, 1, nullptr},
       {"attn_mfma", &Tune::attn_mfma, 0, 1, nullptr},
       {"prior_split", &Tune::prior_split, 0, 1, nullptr},

@@ -174,6 +174,7 @@ struct Tune {
   int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in
   int persist = 1;         // B = 1 bf16 solves: one persistent launch for all steps (persist.hpp)
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
+  int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
   int persist_opt = 585;   // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
                            // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms)

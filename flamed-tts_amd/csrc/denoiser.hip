@@ -2184,15 +2184,15 @@ static bool den_fused_ok(const Den* d, int B, int T) {
 // nfe-step one).
 // ------------------------------ persistent B = 1 solve (persist.hpp) ------------------------------
 
-// Scratch of the persistent solve, sized for T <= pk::kMaxT: the counters first (the per-launch memset
-// block starts the allocation and is a multiple of 16 B), then the sticky failure word (never zeroed by a
-// launch) and the hand-off buffers.
+// Scratch of the persistent solve, sized for T <= pk::kMaxT: the counter block (reset by every launch's own
+// prologue), the sticky words (failure count and the prologue's monotonic arrival counters: zeroed once at
+// allocation, never again) and the hand-off buffers.
 static size_t persist_layout(char* base, pk::Params* P) {
   size_t off = 0;
   auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off = align256(off + bytes); return p; };
   const size_t T = pk::kMaxT, H = pk::kH, C = pk::kC;
   char* ctr = take(4 * (size_t)pk::kCtrInts);
-  char* fails = take(16);
+  char* sticky = take(4 * (size_t)pk::kStickyInts);
   char* xp0 = take(T * pk::kSlots * 8);
   char* xp1 = take(T * pk::kSlots * 8);
   char* ximg = take(T * H * 4);
@@ -2204,7 +2204,7 @@ static size_t persist_layout(char* base, pk::Params* P) {
   char* yb = take((size_t)pk::kWGs * 16 * 4);
   if (P) {
     P->ctr = reinterpret_cast<int*>(ctr);
-    P->fails = reinterpret_cast<int*>(fails);
+    P->sticky = reinterpret_cast<int*>(sticky);
     P->xpart[0] = reinterpret_cast<float2*>(xp0);
     P->xpart[1] = reinterpret_cast<float2*>(xp1);
     P->ximg = reinterpret_cast<float*>(ximg);
@@ -2266,14 +2266,14 @@ static bool persist_eligible(Den* d, int B, int T) {
 }
 
 // Steps [s0, s1) of a B = 1 solve as ONE cooperative launch, enqueued on `st` with no host synchronisation:
-// a zeroed counter block, the kernel, and (outside a capture) HIP events around it plus an async copy of the
-// sticky failure word.  A failed launch NaN-poisons x and is reported by the next call / persist_info.
+// the kernel (it resets its own counter block) and, outside a capture, HIP events around it plus an async
+// copy of the sticky failure word.  A failed launch NaN-poisons x and is reported by the next call / persist_info.
 static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, int s0, int s1, hipStream_t st) {
   const bool cap = stream_capturing(st);
   FL_REQUIRE(d->pmem && d->pfail_host, "persistent solve: scratch not allocated at load");
   pk::Params P{};
   persist_layout(d->pmem, &P);
-  d->pfail = P.fails;
+  d->pfail = P.sticky + pk::SY_FAILS;
   P.T = T; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
   P.dt = (float)(1.0 / (double)nfe);
   P.mods = mods; P.MS = d->MS; P.MS0 = d->MS0;
@@ -2294,8 +2294,6 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, i
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
   P.opt = tn().persist_opt;
   P.inject_step = tn().persist_inject;
-  FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pk::kCtrInts, st));
-  if (P.opt & 512) FL_HIP(hipMemsetAsync(P.gnp, 0, (size_t)pk::kGroups * pk::kH * 16, st));  // granule tags
   hipEvent_t* ev = nullptr;
   if (!cap) {
     ev = d->pring[d->pring_n % Den::kPRing];
@@ -2303,12 +2301,14 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, i
       if (!ev[k]) FL_HIP(hipEventCreate(&ev[k]));
     FL_HIP(hipEventRecord(ev[0], st));
   }
-  const int lrc = pk::persist_launch(P, st);
+  // inside a capture: a cooperative kernel node (persist_capmode 0) or a plain one (1; residency was checked
+  // by the uncaptured cooperative launches and persist_device_ok)
+  const int lrc = pk::persist_launch(P, st, !cap || tn().persist_capmode == 0);
   if (lrc) return lrc;
   if (!cap) {
     FL_HIP(hipEventRecord(ev[1], st));
     ++d->pring_n;
-    FL_HIP(hipMemcpyAsync(d->pfail_host, P.fails, sizeof(int), hipMemcpyDeviceToHost, st));
+    FL_HIP(hipMemcpyAsync(d->pfail_host, d->pfail, sizeof(int), hipMemcpyDeviceToHost, st));
   }
   ++d->pruns;
   return kOk;
@@ -2387,7 +2387,7 @@ FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails) {
   pk::Params P{};
   persist_layout(d->pmem, &P);
   FL_HIP(hipDeviceSynchronize());  // captured launches leave no event: wait for everything (diagnostic)
-  FL_HIP(hipMemcpy(fails, P.fails, sizeof(int), hipMemcpyDeviceToHost));
+  FL_HIP(hipMemcpy(fails, P.sticky + pk::SY_FAILS, sizeof(int), hipMemcpyDeviceToHost));
   if (d->pfail_host) __atomic_store_n(d->pfail_host, *fails, __ATOMIC_RELAXED);
   persist_poll_fails(d);
   return kOk;

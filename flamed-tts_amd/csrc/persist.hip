@@ -115,6 +115,29 @@ __device__ __forceinline__ bool wait_ge(int* err, int* fails, long long tmo, int
   return ok;
 }
 
+// The reset prologue's grid-wide arrival: wave 0 polls a monotonic counter until it reaches `target` (no
+// error word yet: the counter block is being reset); a timeout leaves the launch (x NaN-poisoned).
+__device__ __forceinline__ bool arrive_wait(int* ctr, int target, long long tmo, int* flag) {
+  if (threadIdx.x < 64) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (unsigned it = 0;; ++it) {
+      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if ((it & 31) == 31 && (long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (threadIdx.x == 0) *flag = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = *flag != 0;
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: later hand-off loads stay below
+  return ok;
+}
+
 // ---- weight panels: 32 rows (output columns) x K bf16, 16-B chunks XOR-swizzled by row & 15 (the 16
 // lanes of a ds_read_b128 group hit 16 distinct 16-B slots); the swizzle is applied to each lane's DMA
 // SOURCE chunk (an involution), since LDS-DMA writes a wave's 64 lanes linearly.
@@ -356,30 +379,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = P.T;
   const int H = kH;
-  // Group / slot.  opt & 4: group = this workgroup's XCD (hardware register), slot = its arrival ticket
-  // on that XCD, so a group's hand-offs stay in one L2: group-local payloads are stored plainly (the
-  // line stays in the XCD's L2) and read with sc1 loads (L1 bypass, L2 hit); cross-group payloads stay
-  // write-through.  More than 32 workgroups on one XCD (not all 256 resident) aborts the solve.
-  // Otherwise group = blockIdx % 8 (the round-robin dispatch puts it on one XCD: speed only).
-  const bool xcc_id = (P.opt & 4) != 0;
+  // Group / slot: group = blockIdx % 8 (the round-robin dispatch puts it on one XCD: speed only).
   int g = blockIdx.x % kGroups, s = blockIdx.x / kGroups;
-  if (xcc_id) {
-    int* tk = reinterpret_cast<int*>(smem + L_FLAG);
-    if (threadIdx.x == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      xcc &= kGroups - 1;
-      const int slot = __hip_atomic_fetch_add(P.ctr + CT_SLOT + 16 * xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tk[0] = (int)xcc;
-      tk[1] = slot;
-      if (slot >= kSlots) raise_err(P.ctr + CT_ERR, P.fails, 2);
-    }
-    __syncthreads();
-    g = tk[0];
-    s = tk[1];
-    __syncthreads();
-    if (s >= kSlots) return;
-  }
   // opt & 8: the XCDs as a 2 x 4 grid of (row half, column quarter): XCD x holds row groups
   // 4 (x / 4) .. + 3 and column slots 8 (x % 4) .. + 7, so per GEMM phase an XCD's L2 pulls 4 row
   // panels of A (each read by 8 of its CUs) and 8 weight panels (each read by 4) -- ~0.9 MB per XCD
@@ -390,7 +391,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     g = 4 * (x / 4) + (j % 4);
     s = 8 * (x % 4) + j / 4;
   }
-  const bool xloc = xcc_id && !(P.opt & 8);  // group-local payloads may stay in the XCD's L2
+  constexpr bool xloc = false;  // (plain stores kept for an XCD-local group layout; every hand-off is write-through)
   const bool frag = (P.opt & 64) != 0;        // fragment-major GEMM A images (a2, u, xa, xs)
   const bool gran = (P.opt & 512) != 0;       // GroupNorm partials as tagged granules (gnp zeroed per launch)
   int r0, nr;
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   int* mygrp = grp + 16 * g;
   int* gnc = P.ctr + CT_GN + 16 * s;
   int* errw = P.ctr + CT_ERR;
-  int* fails = P.fails;
+  int* fails = P.sticky + SY_FAILS;
   const long long tmo = P.tmo;
   int L = 0;    // group signals so far (the same sequence in every workgroup)
   int ndg = 0;  // GroupNorm hand-offs so far
@@ -497,6 +498,29 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     signal(mygrp);
     ++L;
   };
+  // ---- reset prologue: this launch zeroes its own counter block (and the GroupNorm granule tags), so no
+  // host memset node has to be ordered before the kernel (a memset node replayed in a captured graph did not
+  // reset the counters of later replays).  Two grid-wide arrivals on monotonic counters that are never
+  // reset: the first says every workgroup of this launch has started (so the previous launch, stream-
+  // ordered before it, is done with the block), the second that every share has been zeroed.
+  {
+    int* tk = reinterpret_cast<int*>(smem + L_FLAG);
+    if (tid == 0) tk[1] = __hip_atomic_fetch_add(P.sticky + SY_ARRIVE0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / kWGs;
+    __syncthreads();
+    const int launch = tk[1];
+    __syncthreads();
+    if (!arrive_wait(P.sticky + SY_ARRIVE0, (launch + 1) * kWGs, tmo, flag)) { fail_exit(); return; }
+    if (tid < 4 && kCtrInts > 4 * (int)blockIdx.x + tid)
+      __hip_atomic_store(P.ctr + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gran && tid < 32) {  // 512 B of the 128 KB granule block per workgroup
+      const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
+      st16(rq, (unsigned)((blockIdx.x * 32 + tid) * 16), u32x4{0u, 0u, 0u, 0u});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(P.sticky + SY_ARRIVE1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!arrive_wait(P.sticky + SY_ARRIVE1, (launch + 1) * kWGs, tmo, flag)) { fail_exit(); return; }
+  }
   publish_xs();
 
   float X[2][4];  // residual stream tile (this wave's 16 rows x 32 columns), MFMA layout
@@ -546,11 +570,28 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       };
 
       // -------- LN + modulate + depthwise k31 + GroupNorm(H, H) over T (prob_generator.py:81-89, 153-156)
+      // what this phase reads that no other workgroup writes goes out before the wait (its latency hides in
+      // the poll): the modulation vectors of the thread's columns, the depthwise taps and bias of channel cc,
+      // the GroupNorm affine of the GN-combining lanes
+      const int cc = tid & 31, rg = tid >> 5;
+      float hva[4], hvb[4], ova[2], ovb[2];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vab(col0 + 4 * (tid & 7) + e, hva[e], hvb[e]);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) vab(col0 + 16 * nt + c, ova[nt], ovb[nt]);
+      float w[kTaps];
+#pragma unroll
+      for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col0 + cc];
+      const float dbias = bw.dwb[col0 + cc];
+      float gwv = 0.f, gbv = 0.f;
+      if (tid < kCols) {
+        gwv = bw.gnw[col0 + tid];
+        gbv = bw.gnb[col0 + tid];
+      }
       PST(step);
       if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
       const int wa = max(r0 - kHalo, 0), wz = min(r0 + nr + kHalo, T);
-      const int cc = tid & 31, rg = tid >> 5;
       // Everything this phase reads that does not wait on another phase goes out first, so the loads'
       // latencies overlap: the thread's 3 window items (its 4 columns col0 + 4 (tid & 7) are the same in
       // every item), their modulation vectors, the depthwise taps of channel cc, the row statistics.
@@ -565,17 +606,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           hv[k] = halo ? as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * (tid & 7)) * 4))) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      float hva[4], hvb[4], ova[2], ovb[2];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) vab(col0 + 4 * (tid & 7) + e, hva[e], hvb[e]);
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) vab(col0 + 16 * nt + c, ova[nt], ovb[nt]);
-      float w[kTaps];
-#pragma unroll
-      for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col0 + cc];
-      const float dbias = bw.dwb[col0 + cc];
       row_stats(P.xpart[0], T, wa, wz, r0 - kHalo, st);
       __syncthreads();
+      PST(step);  // halo rows + row statistics in
       // window h[p] (frame r0 - 15 + p): own rows from X (registers), halo rows from ximg, 0 outside [0, T)
 #pragma unroll
       for (int k = 0; k < kItems; ++k) {
@@ -605,6 +638,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           }
       }
       __syncthreads();
+      PST(step);  // normalised window in LDS
       // depthwise conv (zero padding at the utterance edges): thread -> channel cc, tile rows 8 rg .. 8 rg + 7
       float d[8];
       {
@@ -619,6 +653,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           d[k] = a;
         }
       }
+      PST(step);  // depthwise conv done
       // GroupNorm partials of this group's frames: exact two passes (sum, squared deviations)
       const int nv = min(max(nr - 8 * rg, 0), 8);
       {
@@ -660,11 +695,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (!gran) signal(gnc);
       PST(step);
       ++ndg;
-      float gwv = 0.f, gbv = 0.f;
-      if (tid < kCols) {
-        gwv = bw.gnw[col0 + tid];
-        gbv = bw.gnb[col0 + tid];
-      }
       PST(step);
       if (gran) {
         // wave 0: lane cc < 32 re-reads the 8 groups' granules of channel col0 + cc until every tag is this
@@ -967,7 +997,7 @@ bool persist_device_ok(int device) {
   return nb >= 1;
 }
 
-int persist_launch(const Params& Pin, hipStream_t st) {
+int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
   Params P = Pin;
 #ifdef FL_STAMPS
   P.pst = g_pst_buf;
@@ -977,8 +1007,9 @@ int persist_launch(const Params& Pin, hipStream_t st) {
   // (hipErrorCooperativeLaunchTooLarge) instead of queueing workgroups behind resident ones that wait for
   // them.  Capturable: a captured cooperative launch replays cooperatively (MI355X_MICROARCH.md, Residency).
   void* args[] = {&P};
-  const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(den_persist_kernel), dim3(kWGs), dim3(kThreads),
-                                                  args, kLds, st);
+  const void* kern = reinterpret_cast<const void*>(den_persist_kernel);
+  const hipError_t e = cooperative ? hipLaunchCooperativeKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st)
+                                   : hipLaunchKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     set_error("persistent solve: hipLaunchCooperativeKernel -> %s", hipGetErrorString(e));

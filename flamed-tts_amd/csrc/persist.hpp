@@ -51,9 +51,11 @@ constexpr int L_GNV = L_RED + 8 * kCols * 4;
 constexpr int L_FLAG = L_GNV + kCols * 16;
 constexpr int kLds = (L_FLAG + 16 + 15) / 16 * 16;
 static_assert(kLds <= 160 * 1024, "persistent solve LDS");
-// counters (ints, one 64-B line each); zeroed before every launch
-constexpr int CT_GRP = 0, CT_GN = 16 * kGroups, CT_ERR = CT_GN + 16 * kSlots, CT_SLOT = CT_ERR + 16,
-              kCtrInts = CT_SLOT + 16 * kGroups;
+// counters (ints, one 64-B line each); zeroed by the launch itself (its reset prologue)
+constexpr int CT_GRP = 0, CT_GN = 16 * kGroups, CT_ERR = CT_GN + 16 * kSlots, kCtrInts = CT_ERR + 16;
+// sticky words (never reset; zeroed once at allocation): failed launches, and the two monotonic arrival
+// counters of the reset prologue, each on a 128-B line of its own
+constexpr int SY_FAILS = 0, SY_ARRIVE0 = 32, SY_ARRIVE1 = 64, kStickyInts = 96;
 
 struct BlockW {
   const bf16 *w2, *w3, *m0, *m2;
@@ -84,7 +86,8 @@ struct Params {
   float4* gnp;             // GroupNorm partials (n, mean, M2) per (group, channel): 8 x H
   float* yb;               // conv_out boundary rows per workgroup: Y0 of its last row, Y2 of its first
   int* ctr;
-  int* fails;              // failed launches so far (sticky across launches: the host reads it after the fact)
+  int* sticky;             // kStickyInts words never reset between launches: [SY_FAILS] failed launches so far
+                           // (the host reads it after the fact), [SY_ARRIVE0/1] the reset prologue's arrivals
   int inject_step = -1;    // diagnostic (flamed_tune persist_inject): every workgroup fails at this step
   long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
   int opt = 0;                        // experiment bits (flamed_tune persist_opt)
@@ -94,7 +97,7 @@ struct Params {
 
 // Host side (persist.hip): whether this device runs the 256-workgroup grid fully resident, and the launch.
 bool persist_device_ok(int device);
-int persist_launch(const Params& P, hipStream_t st);
+int persist_launch(const Params& P, hipStream_t st, bool cooperative = true);
 
 }  // namespace pk
 }  // namespace fl

@@ -133,23 +133,45 @@ def test_persist_knob_off_uses_launch_path(pgb):
     assert _runs(pg) == r0
 
 
+PERSIST_DEFAULT = 585  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
+
+
 @pytest.mark.parametrize("T", [400, 131, 16])
-@pytest.mark.parametrize("opt", [9, 73])
-def test_persist_variants_bitwise(pgb, T, opt):
-    """Hand-off variants change where and how data moves, never the arithmetic: the default (persist_opt 585:
-    fragment-major A images + tagged-granule GroupNorm exchange) equals the row-major, counter-based variant
-    (opt 9) and the counter-based GroupNorm exchange (opt 73) bitwise, for full, partial-tile and nearly-empty
+@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 2048])
+def test_persist_variants_bitwise(pgb, T, flip):
+    """Hand-off variants change where and how data moves, never the arithmetic: the default equals, bitwise,
+    the default with row-major instead of fragment-major A images (bit 64), counter-based instead of
+    tagged-granule GroupNorm exchange (bit 512), both plus the other weight-DMA wave split (bit 1), and
+    wave-0 publishing with the DMA on waves 1..3 toggled (bit 2048), for full, partial-tile and nearly-empty
     row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
     pg, _ = pgb
     x0, spk = _inputs(11, 1, T)
     from flamed import _native as nat
-    nat.check(nat.lib().flamed_tune(b"persist_opt", 585), "flamed_tune")
+    nat.check(nat.lib().flamed_tune(b"persist_opt", PERSIST_DEFAULT), "flamed_tune")
     r0 = _runs(pg)
     a = _solve(pg, x0, spk, 8)
-    with knob("persist_opt", opt, 585):
+    with knob("persist_opt", PERSIST_DEFAULT ^ flip, PERSIST_DEFAULT):
         b = _solve(pg, x0, spk, 8)
     assert _runs(pg) == r0 + 2
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("T", [400, 77])
+def test_persist_ksplit_vs_oracle(pgb, T):
+    """K split over the waves (persist_opt bit 1024: four K-quarter partials summed in fixed order) against
+    the whole-K wave loop and the oracle: same bf16 operands, fp32 reassociation only (rel-L2 <= 1e-3 between
+    the two; each within the bf16 solve bar of the oracle), and bitwise deterministic."""
+    pg, sd = pgb
+    x0, spk = _inputs(12, 1, T)
+    with knob("persist_opt", PERSIST_DEFAULT ^ 1024, PERSIST_DEFAULT):
+        a = _solve(pg, x0, spk, 8)
+        a2 = _solve(pg, x0, spk, 8)
+    b = _solve(pg, x0, spk, 8)
+    ref = orc.euler_solve(sd, x0, spk, 8)
+    print(f"T={T}: K-split toggled vs default rel-L2 {rel_l2(a, b):.3e}; vs oracle {rel_l2(a, ref):.3e} / {rel_l2(b, ref):.3e}")
+    assert torch.equal(a, a2)
+    assert rel_l2(a, b) < 1e-3
+    assert rel_l2(a, ref) < BF16_SOLVE and rel_l2(b, ref) < BF16_SOLVE
 
 
 def test_persist_enqueue_is_async(pgb):
