@@ -246,11 +246,23 @@ __device__ __forceinline__ float erf_fast(float x) {
 }
 __device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
-__device__ __forceinline__ float wave_sum16(float v) {  // sum over the 16 lanes sharing lane>>4
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
+// v + the value of another lane, picked by a DPP control (a VALU operand modifier: no LDS round trip, unlike
+// __shfl_xor's ds_bpermute): quad_perm [1,0,3,2] = lane ^ 1, [2,3,0,1] = lane ^ 2 (within a quad),
+// row_half_mirror (lane i <-> 7 - i of each 8), row_mirror (lane i <-> 15 - i of each 16).
+template <int kCtrl>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), kCtrl, 0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+// Sum over the 16 lanes sharing lane >> 4.  Bitwise the same as the xor-1/2/4/8 butterfly: after the two quad
+// steps every lane of a quad holds the quad sum, so the half-row and row mirrors add exactly the partner sums
+// the xor-4 and xor-8 steps add (fp32 addition is commutative).
+__device__ __forceinline__ float wave_sum16(float v) {
+  v = dpp_add<kDppXor1>(v);
+  v = dpp_add<kDppXor2>(v);
+  v = dpp_add<kDppHalfMirror>(v);
+  v = dpp_add<kDppMirror>(v);
   return v;
 }
 

@@ -296,7 +296,7 @@ __device__ __forceinline__ void row_stats(const float2* xpart, int T, int ra, in
     float sm = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) sm += mv[k];
-    sm += __shfl_xor(sm, 1);
+    sm = dpp_add<kDppXor1>(sm);
     const float mean = sm * (1.0f / kSlots);
     float m2 = 0.f;
 #pragma unroll
@@ -304,7 +304,7 @@ __device__ __forceinline__ void row_stats(const float2* xpart, int T, int ra, in
       const float d = mv[k] - mean;
       m2 += qv[k] + (float)kCols * d * d;
     }
-    m2 += __shfl_xor(m2, 1);
+    m2 = dpp_add<kDppXor1>(m2);
     if (act && half == 0) {
       st[2 * (row - rbase)] = mean;
       st[2 * (row - rbase) + 1] = 1.0f / sqrtf(m2 * (1.0f / kH) + 1e-6f);

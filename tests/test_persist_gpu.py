@@ -137,13 +137,12 @@ PERSIST_DEFAULT = 585  # flamed_tune persist_opt default (csrc/common.hpp Tune::
 
 
 @pytest.mark.parametrize("T", [400, 131, 16])
-@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 2048])
+@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1])
 def test_persist_variants_bitwise(pgb, T, flip):
     """Hand-off variants change where and how data moves, never the arithmetic: the default equals, bitwise,
     the default with row-major instead of fragment-major A images (bit 64), counter-based instead of
-    tagged-granule GroupNorm exchange (bit 512), both plus the other weight-DMA wave split (bit 1), and
-    wave-0 publishing with the DMA on waves 1..3 toggled (bit 2048), for full, partial-tile and nearly-empty
-    row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
+    tagged-granule GroupNorm exchange (bit 512), and both plus the other weight-DMA wave split (bit 1), for
+    full, partial-tile and nearly-empty row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
     pg, _ = pgb
     x0, spk = _inputs(11, 1, T)
     from flamed import _native as nat
@@ -154,24 +153,6 @@ def test_persist_variants_bitwise(pgb, T, flip):
         b = _solve(pg, x0, spk, 8)
     assert _runs(pg) == r0 + 2
     assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("T", [400, 77])
-def test_persist_ksplit_vs_oracle(pgb, T):
-    """K split over the waves (persist_opt bit 1024: four K-quarter partials summed in fixed order) against
-    the whole-K wave loop and the oracle: same bf16 operands, fp32 reassociation only (rel-L2 <= 1e-3 between
-    the two; each within the bf16 solve bar of the oracle), and bitwise deterministic."""
-    pg, sd = pgb
-    x0, spk = _inputs(12, 1, T)
-    with knob("persist_opt", PERSIST_DEFAULT ^ 1024, PERSIST_DEFAULT):
-        a = _solve(pg, x0, spk, 8)
-        a2 = _solve(pg, x0, spk, 8)
-    b = _solve(pg, x0, spk, 8)
-    ref = orc.euler_solve(sd, x0, spk, 8)
-    print(f"T={T}: K-split toggled vs default rel-L2 {rel_l2(a, b):.3e}; vs oracle {rel_l2(a, ref):.3e} / {rel_l2(b, ref):.3e}")
-    assert torch.equal(a, a2)
-    assert rel_l2(a, b) < 1e-3
-    assert rel_l2(a, ref) < BF16_SOLVE and rel_l2(b, ref) < BF16_SOLVE
 
 
 def test_persist_enqueue_is_async(pgb):
