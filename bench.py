@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--dma", type=int, default=None, help="flamed_tune dma (0: register-staged GEMM main loop)")
     ap.add_argument("--persist", type=int, default=None, help="flamed_tune persist (B = 1: one persistent launch per solve)")
     ap.add_argument("--persist-opt", type=int, default=None, help="flamed_tune persist_opt (persistent kernel experiment bits)")
+    ap.add_argument("--split-batch", type=int, default=None, help="flamed_tune split_batch (large-M sub-batch chains, 1 = off)")
+    ap.add_argument("--persist-capmode", type=int, default=None, help="flamed_tune persist_capmode")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU rehearsal of the launcher/timing harness over gloo (no GPU; tests/test_bench_cpu.py)")
@@ -663,7 +665,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler", "persist", "persist_opt"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler", "persist", "persist_opt", "split_batch", "persist_capmode"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")

@@ -86,6 +86,8 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"fuse_euler", &Tune::fuse_euler, 0, 1, nullptr},
       {"pva_split", &Tune::pva_split, 0, 1, nullptr},
       {"persist", &Tune::persist, 0, 1, nullptr},
+      {"split_batch", &Tune::split_batch, 1, 4, nullptr},
+      {"split_min_rows", &Tune::split_min_rows, 1024, 1 << 30, nullptr},
       {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
       {"persist_capmode", &Tune::persist_capmode, 0, 1, nullptr},

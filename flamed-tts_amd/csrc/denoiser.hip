@@ -1580,6 +1580,9 @@ struct Den {
   // graph cache
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
+  static constexpr int kMaxSplit = 4;          // sub-batch chains of a large-M solve (den_split)
+  hipStream_t cap_aux[kMaxSplit] = {};         // capture streams of chains 1..S-1
+  hipEvent_t cap_ev[kMaxSplit] = {};           // fork / join events of the chains' capture
   int g_B = -1, g_T = -1, g_nfe = -1, g_epoch = -1;
   const void *g_xt = nullptr, *g_mods = nullptr, *g_ws = nullptr;
   int* ctr = nullptr;  // device Euler step counter for graph replay
@@ -1717,6 +1720,29 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
 }
 static size_t den_ws_bytes(const Den* d, int B, int T) { return den_ws_layout(d, B, T, nullptr, nullptr); }
 
+// Large-M solves as concurrent sub-batches (tune split_batch, default 2): utterances are independent in the
+// denoiser (GroupNorm statistics and the depthwise halo never cross an utterance: prob_generator.py:81-89), so
+// the batch's Euler steps run as S chains of B / S utterances, captured as S parallel branches of one graph.
+// One chain's inter-kernel gaps and the partly filled last round of its GEMM tiles are then covered by the
+// other chain's kernels.  Every chain is the same step structure at B / S (so a split solve is bitwise the
+// split eager loop); fp8 handles keep one chain (their MX GEMMs need the large tiles of the whole batch).
+static int den_split(const Den* d, int B, int T) {
+  const Tune& tu = tn();
+  const int S = tu.split_batch;
+  if (S <= 1 || d->dt != FLAMED_BF16 || d->f8 || !tu.big || B % S != 0) return 1;
+  if ((size_t)(B / S) * T < (size_t)tu.split_min_rows) return 1;
+  return S;
+}
+// workspace of one of the S sub-batch chains (each chain has its own; chain k's starts at k * this)
+static size_t den_split_ws(const Den* d, int B, int T, int S) { return align256(den_ws_bytes(d, B / S, T)); }
+// workspace a solve of B x T needs (the whole-batch layout, or S chain workspaces when it splits)
+static size_t den_solve_ws(const Den* d, int B, int T) {
+  const size_t one = den_ws_bytes(d, B, T);
+  const int S = den_split(d, B, T);
+  const size_t split = S > 1 ? (size_t)S * den_split_ws(d, B, T, S) : 0;
+  return one > split ? one : split;
+}
+
 }  // namespace fl
 
 using namespace fl;
@@ -1751,6 +1777,10 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
     DeviceGuard dg(d->device);
     retire_graph(d->gexec);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
+    for (auto& a : d->cap_aux)
+      if (a) (void)hipStreamDestroy(a);
+    for (auto& e : d->cap_ev)
+      if (e) (void)hipEventDestroy(e);
     if (d->ctr) (void)hipFree(d->ctr);
     if (d->scnt) (void)hipFree(d->scnt);
     if (d->gcnt) (void)hipFree(d->gcnt);
@@ -1798,6 +1828,10 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     DeviceGuard og(d->device);
     retire_graph(d->gexec);
     if (d->cap_stream) { (void)hipStreamDestroy(d->cap_stream); d->cap_stream = nullptr; }
+    for (auto& a : d->cap_aux)
+      if (a) { (void)hipStreamDestroy(a); a = nullptr; }
+    for (auto& e : d->cap_ev)
+      if (e) { (void)hipEventDestroy(e); e = nullptr; }
     if (d->ctr) { (void)hipFree(d->ctr); d->ctr = nullptr; }
     if (d->scnt) { (void)hipFree(d->scnt); d->scnt = nullptr; }
     if (d->gcnt) { (void)hipFree(d->gcnt); d->gcnt = nullptr; }
@@ -1985,7 +2019,7 @@ FLAMED_API size_t flamed_den_workspace_size(flamed_den_t h, int B, int T) {
   if (!d) return 0;
   std::lock_guard<std::recursive_mutex> lk(d->mu);
   TuneScope ts(den_tune_sync(d));  // the layout depends on the handle's large-M threshold
-  return den_ws_bytes(d, B, T);
+  return den_solve_ws(d, B, T);
 }
 
 }  // extern "C"
@@ -1997,10 +2031,11 @@ namespace fl {
 // mods + (*ctr) * B * MS and the last kernel increments it (graph replay of captured steps).
 template <typename DT, typename XT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
-                         const DenWs& w, int* ctr, hipStream_t st, const float* xsrc) {
+                         const DenWs& w, int* ctr, hipStream_t st, const float* xsrc, int Bs) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const Tune& tu = tn();
-  const StepOff so{tu.noctr ? nullptr : ctr, (long long)B * MS};
+  // a step's modulation rows are Bs apart (Bs = B, or the whole batch when this is one of its sub-batches)
+  const StepOff so{tu.noctr ? nullptr : ctr, (long long)Bs * MS};
   SplitCtx sctx;
   sctx.slab = w.SL; sctx.slab_floats = w.SLn; sctx.cnt = d->scnt; sctx.cnt_n = Den::kSplitCounters;
   sctx.target = tu.split_target; sctx.max_split = tu.split_max;
@@ -2159,14 +2194,15 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
 }
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
-                    hipStream_t st, int* ctr = nullptr, const float* xsrc = nullptr) {
+                    hipStream_t st, int* ctr = nullptr, const float* xsrc = nullptr, int Bs = 0) {
+  if (Bs <= 0) Bs = B;
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   if (d->dt == FLAMED_BF16) {
-    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc);
-    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc);
+    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs);
+    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs);
   }
-  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc);
+  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs);
 }
 
 // The fused Euler step (LoadEulerIn) runs where proj_in takes the small-M register loop with one
@@ -2426,18 +2462,28 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   FL_REQUIRE(0 <= s0 && s0 < s1 && s1 <= nfe, "flamed_den_solve_part: bad step range [%d, %d) of %d", s0, s1, nfe);
   FL_DEN_CALL(d);
   FL_REQUIRE_ON(xt, d->device, "flamed_den_solve");
-  if (ws_bytes < den_ws_bytes(d, B, T)) {
+  if (ws_bytes < den_solve_ws(d, B, T)) {
     set_error("flamed_den_solve: workspace too small");
     return kNoWorkspace;
   }
   // delta_t = 1 / nfe as a python float, applied in fp32 (prob_generator.py:441,445)
   const float dt = (float)(1.0 / (double)nfe);
   const size_t step_stride = (size_t)B * d->MS;
+  const int S = den_split(d, B, T), Bk = B / S;
+  const size_t wsk = S > 1 ? den_split_ws(d, B, T, S) : 0;
+  auto sub = [&](int k, float*& xk, const float*& mk, void*& wk) {  // chain k's state, table rows, workspace
+    xk = xt + (size_t)k * Bk * T * d->C;
+    mk = mods + (size_t)k * Bk * d->MS;
+    wk = static_cast<char*>(ws) + k * wsk;
+  };
   if (!use_graph) {
-    for (int s = s0; s < s1; ++s) {
-      int rc = den_step(d, xt, mods + s * step_stride, T, B, T, dt, nullptr, ws, st);
-      if (rc) return rc;
-    }
+    for (int s = s0; s < s1; ++s)
+      for (int k = 0; k < S; ++k) {
+        float* xk; const float* mk; void* wk;
+        sub(k, xk, mk, wk);
+        int rc = den_step(d, xk, mk + s * step_stride, T, Bk, T, dt, nullptr, wk, st, nullptr, nullptr, B);
+        if (rc) return rc;
+      }
     return kOk;
   }
   const int G = graph_chunk(nfe);
@@ -2465,7 +2511,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   if (!d->ctr) FL_HIP(hipMalloc(&d->ctr, 256));
   // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
   // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even
-  const bool fused = den_fused_ok(d, B, T) && G % 2 == 0;
+  const bool fused = S == 1 && den_fused_ok(d, B, T) && G % 2 == 0;
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   // the graph bakes in dt = 1/nfe, so nfe is part of the key
@@ -2474,11 +2520,28 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   if (!hit) {
     retire_graph(d->gexec);
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
+    for (int k = 1; k < S; ++k)
+      if (!d->cap_aux[k]) FL_HIP(hipStreamCreateWithFlags(&d->cap_aux[k], hipStreamNonBlocking));
+    for (int k = 0; k < Den::kMaxSplit; ++k)
+      if (!d->cap_ev[k]) FL_HIP(hipEventCreateWithFlags(&d->cap_ev[k], hipEventDisableTiming));
     FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
     int rc = kOk;
-    for (int s = 0; s < G && rc == kOk; ++s) {
-      if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr, s % 2 ? xt : w.XP);
-      else rc = den_step(d, xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr);
+    if (S > 1) {  // fork: chains 1..S-1 on their own capture streams
+      FL_HIP(hipEventRecord(d->cap_ev[0], d->cap_stream));
+      for (int k = 1; k < S; ++k) FL_HIP(hipStreamWaitEvent(d->cap_aux[k], d->cap_ev[0], 0));
+    }
+    for (int k = 0; k < S && rc == kOk; ++k) {
+      float* xk; const float* mk; void* wk;
+      sub(k, xk, mk, wk);
+      hipStream_t cs = k == 0 ? d->cap_stream : d->cap_aux[k];
+      for (int s = 0; s < G && rc == kOk; ++s) {
+        if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, cs, d->ctr, s % 2 ? xt : w.XP);
+        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, nullptr, B);
+      }
+    }
+    for (int k = 1; k < S && rc == kOk; ++k) {  // join
+      FL_HIP(hipEventRecord(d->cap_ev[k], d->cap_aux[k]));
+      FL_HIP(hipStreamWaitEvent(d->cap_stream, d->cap_ev[k], 0));
     }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
@@ -2496,7 +2559,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
       FL_LAUNCH_CHECK();
       FL_HIP(hipMemsetAsync(d->ctr, 0xff, sizeof(int), st));
     } else {
-      FL_HIP(hipMemsetAsync(d->ctr, 0, sizeof(int), st));
+      FL_HIP(hipMemsetAsync(d->ctr, 0, 256, st));  // the step counters of every chain (16 ints apart)
     }
   }
   for (int r = s0 / G; r < s1 / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));

@@ -76,6 +76,17 @@ __device__ __forceinline__ void signal(int* ctr) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same signal issued AFTER the next phase's weight DMA (persist_opt 4096): vmcnt counts loads, stores and
+// LDS-DMA together in issue order, so waiting until only this wave's kDma youngest operations (its DMA pieces)
+// are outstanding drains exactly the older hand-off stores -- the drain's round trip overlaps the DMA issue
+// instead of preceding it, and the DMA stays in flight across the barrier.
+template <int kDma>
+__device__ __forceinline__ void signal_dma(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kDma) : "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Abandon the solve: the first workgroup to set the error word also counts the failed launch in the sticky
 // word the host reads later (the per-launch counter block is zeroed before every launch, `fails` is not).
 __device__ __forceinline__ void raise_err(int* err, int* fails, int code) {
@@ -421,6 +432,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   [[maybe_unused]] int cur_step = P.s0;  // (FL_STAMPS builds: the step a helper lambda stamps)
   const bool fastdma = !(P.opt & 256);  // persist_opt 256: the generic issue loop (A/B)
   const bool w4 = (P.opt & 1) != 0;
+  // drain behind the next panel's DMA (signal_dma): needs the four-wave fast issue, whose per-wave piece count
+  // is fixed (16 for a 32 x 1024 panel, 4 for proj_in's 32 x 256)
+  const bool dmafirst = (P.opt & 4096) != 0 && w4 && !(P.opt & 256);
   auto next_w = [&](const bf16* W) {
     wb ^= 1;
     if (fastdma)
@@ -553,10 +567,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     stage_tile<float>(stg, X, wave, lane);
     __syncthreads();
     flush_halo(stg, P.ximg, r0, nr, col0, T);
-    signal(mygrp);
+    if (dmafirst) {
+      next_w(P.blk[0].w2);
+      signal_dma<16>(mygrp);
+    } else {
+      signal(mygrp);
+      next_w(P.blk[0].w2);
+    }
     PST(step);
     ++L;
-    next_w(P.blk[0].w2);
 
     for (int blk = 0; blk <= P.NB; ++blk) {
       const bool fin = blk == P.NB;
@@ -793,10 +812,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
-      signal(mygrp);
+      if (dmafirst) {
+        next_w(bw.w3);
+        signal_dma<16>(mygrp);
+      } else {
+        signal(mygrp);
+        next_w(bw.w3);
+      }
       PST(step);
       ++L;
-      next_w(bw.w3);
 
       // -------- conv_3 (1x1) + ConvNeXt residual + gated residual (:92-93, 109, 156); x * alpha for the fold
       float g3[2], b3v[2], alv[2];  // (ova / ovb of the dwconv phase are this epilogue's LN vectors)
@@ -832,11 +856,18 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.xa, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T, xloc);
-      signal(mygrp);
+      if (dmafirst) {
+        if (fin) issue_out();  // conv_out's panel (into the other buffer; the flip follows the loop)
+        else next_w(bw.m0);
+        signal_dma<16>(mygrp);
+      } else {
+        signal(mygrp);
+        if (fin) issue_out();
+        else next_w(bw.m0);
+      }
       PST(step);
       ++L;
       if (fin) break;  // conv_out follows the FinalLayer's conv_3
-      next_w(bw.m0);
 
       // -------- mlp.0 + SiLU, the LayerNorm folded into the epilogue (:157-158)
       const float* fo0 = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
@@ -862,10 +893,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
-      signal(mygrp);
+      if (dmafirst) {
+        next_w(bw.m2);
+        signal_dma<16>(mygrp);
+      } else {
+        signal(mygrp);
+        next_w(bw.m2);
+      }
       PST(step);
       ++L;
-      next_w(bw.m2);
 
       // -------- mlp.2 + gated residual (:159-160)
       const float g2v[2] = {mb[5 * H + col0 + c], mb[5 * H + col0 + 16 + c]}, bm2[2] = {bw.mb2[col0 + c], bw.mb2[col0 + 16 + c]};
@@ -882,16 +918,20 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       stage_tile<float>(stg, X, wave, lane);
       __syncthreads();
       flush_halo(stg, P.ximg, r0, nr, col0, T);
-      signal(mygrp);
+      if (dmafirst) {
+        next_w(P.blk[blk + 1].w2);
+        signal_dma<16>(mygrp);
+      } else {
+        signal(mygrp);
+        next_w(P.blk[blk + 1].w2);
+      }
       PST(step);
       ++L;
-      next_w(P.blk[blk + 1].w2);
     }
 
     // -------- conv_out k3 (taps stacked; LayerNorm + modulate folded; :238-245, 264).  Panel row n < 24 is
     // tap n / 8 of latent channel 8 s + n % 8; rows 24..31 repeat rows 0..7 (ignored)
-    issue_out();
-    wb ^= 1;
+    wb ^= 1;  // conv_out's panel was issued behind the FinalLayer's conv_3
     float fac[2], fbc[2];  // fold vectors of the lane's stacked columns, before the wait
     {
       const float* fo = md + P.MS0 + (size_t)P.NB * 2 * H;  // [wa (3 C), wb (3 C)]
@@ -929,10 +969,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const float* src = half == 0 ? yl + (nr - 1) * 24 + 4 * k : yl + 16 + 4 * k;
       st16(ry, (unsigned)(((g + kGroups * s) * 16 + half * 8 + 4 * k) * 4), __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(src)));
     }
-    signal(mygrp);
+    if (dmafirst && step + 1 < P.s1) {
+      next_win();
+      signal_dma<4>(mygrp);
+    } else {
+      signal(mygrp);
+      if (step + 1 < P.s1) next_win();
+    }
     PST(step);
     ++L;
-    if (step + 1 < P.s1) next_win();
 
     // -------- Euler update x += dt * v, v[t] = b + Y1[t] + Y0[t-1] + Y2[t+1] (:445; conv3_combine order)
     PST(step);
