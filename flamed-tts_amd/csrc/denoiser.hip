@@ -2229,6 +2229,7 @@ static size_t persist_layout(char* base, pk::Params* P) {
   const size_t T = pk::kMaxT, H = pk::kH, C = pk::kC;
   char* ctr = take(4 * (size_t)pk::kCtrInts);
   char* sticky = take(4 * (size_t)pk::kStickyInts);
+  char* seal = take((size_t)pk::kWGs * 16);
   char* xp0 = take(T * pk::kSlots * 8);
   char* xp1 = take(T * pk::kSlots * 8);
   char* ximg = take(T * H * 4);
@@ -2241,6 +2242,7 @@ static size_t persist_layout(char* base, pk::Params* P) {
   if (P) {
     P->ctr = reinterpret_cast<int*>(ctr);
     P->sticky = reinterpret_cast<int*>(sticky);
+    P->seal = reinterpret_cast<int*>(seal);
     P->xpart[0] = reinterpret_cast<float2*>(xp0);
     P->xpart[1] = reinterpret_cast<float2*>(xp1);
     P->ximg = reinterpret_cast<float*>(ximg);

@@ -149,6 +149,38 @@ __device__ __forceinline__ bool arrive_wait(int* ctr, int target, long long tmo,
   return ok;
 }
 
+// Seal check (persist_opt 16384, a verification mode): every producer stores, write-through and ahead of the
+// drain that precedes its counter add, the number of the group hand-off it is completing into its seal; a
+// consumer that has seen a counter reach hand-off `target` then requires every seal it depends on to show
+// >= target.  A seal behind its counter would mean the ordering that the hand-off protocol relies on
+// (MI355X_MICROARCH.md, Valid forms row 1) did not hold: the consumer spins on it, and gives the launch up
+// (error 4, NaN-poisoned x) if it never arrives.  Wave 0 checks n seals from sp; the others meet it.
+__device__ __forceinline__ bool seals_ok(const int* sp, int n, int target, int* err, int* fails, long long tmo, int* flag) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (unsigned it = 0;; ++it) {
+      bool mine = true;
+      for (int i = lane; i < n; i += 64)
+        mine = mine && __hip_atomic_load(sp + 4 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      if (__all(mine)) break;
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
+        if (lane == 0) raise_err(err, fails, 4);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *flag = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = *flag != 0;
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return ok;
+}
+
 // ---- weight panels: 32 rows (output columns) x K bf16, 16-B chunks XOR-swizzled by row & 15 (the 16
 // lanes of a ds_read_b128 group hit 16 distinct 16-B slots); the swizzle is applied to each lane's DMA
 // SOURCE chunk (an involution), since LDS-DMA writes a wave's 64 lanes linearly.
@@ -262,6 +294,81 @@ __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* 
       }
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, x0), acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, x1), acc[1], 0, 0, 0);
+    }
+  }
+}
+
+// The same product with the work split 2 x 2 (persist_opt 1024): wave w = (pair p, half h) multiplies row tiles
+// 2p and 2p + 1 by K-steps [h KST/2, (h + 1) KST/2), so each B fragment read from LDS feeds two row tiles and
+// the panel is read twice per workgroup instead of four times; the two halves of tile w are then summed
+// through LDS (K-half 0 + K-half 1, the same order in every wave: deterministic) and wave w holds row tile w
+// exactly where gemm() leaves it.
+template <int K>
+__device__ __forceinline__ void gemm_kh(const bf16* A, int r0, int nr, char* wl, f32x4 (&acc)[2], int wave, int lane_in,
+                                        unsigned long long* stamp = nullptr, int g = 0, bool frag = false) {
+  constexpr int KST = K / 32, KH = KST / 2;
+  const int lane = opq(lane_in);
+  const int ntile = (nr + 15) >> 4;
+  const int c = lane & 15, q = lane >> 4;
+  const int tp = wave >> 1, kh = wave & 1, t0 = 2 * tp;
+  const int k0 = __builtin_amdgcn_readfirstlane(kh * KH);
+  u32x4 a[2][KH];
+  if (frag) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(reinterpret_cast<const char*>(A) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST));
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < KH; ++kk) a[t][kk] = ld16(rs, (unsigned)((((t0 + t) * KST + k0 + kk) * 64 + lane) * 16));
+  } else {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < KH; ++kk) a[t][kk] = ld16(rs, (unsigned)(((16 * (t0 + t) + c) * K + (k0 + kk) * 32 + q * 8) * 2));
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * KH) : "memory");  // this wave's (older) weight DMA landed
+  __syncthreads();  // every wave's DMA: the whole panel is in LDS
+  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // FL_STAMPS timeline only
+  f32x4 p[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) p[t][0] = p[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool use0 = t0 < ntile, use1 = t0 + 1 < ntile;
+  constexpr int kBP = 4;
+  u32x4 b0[kBP], b1[kBP];
+#pragma unroll
+  for (int pp = 0; pp < kBP; ++pp) {
+    b0[pp] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (k0 + pp) + q));
+    b1[pp] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (k0 + pp) + q));
+  }
+#pragma unroll
+  for (int kk = 0; kk < KH; ++kk) {
+    const u32x4 x0 = b0[kk % kBP], x1 = b1[kk % kBP];
+    if (kk + kBP < KH) {
+      b0[kk % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (k0 + kk + kBP) + q));
+      b1[kk % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (k0 + kk + kBP) + q));
+    }
+    if (use0) {
+      p[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[0][kk]), __builtin_bit_cast(bf16x8, x0), p[0][0], 0, 0, 0);
+      p[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[0][kk]), __builtin_bit_cast(bf16x8, x1), p[0][1], 0, 0, 0);
+    }
+    if (use1) {
+      p[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[1][kk]), __builtin_bit_cast(bf16x8, x0), p[1][0], 0, 0, 0);
+      p[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[1][kk]), __builtin_bit_cast(bf16x8, x1), p[1][1], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every wave has read the panel: its buffer now carries the partials
+  f32x4* red = reinterpret_cast<f32x4*>(wl);  // [tile][K-half][nt][lane]
+  const int other = t0 + (1 - kh);             // the tile whose other half this wave computed
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) red[((other * 2 + kh) * 2 + nt) * 64 + lane] = p[1 - kh][nt];
+  __syncthreads();
+  acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (wave < ntile) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const f32x4 mine = p[kh][nt], theirs = red[((wave * 2 + (1 - kh)) * 2 + nt) * 64 + lane];
+      acc[nt] = kh == 0 ? mine + theirs : theirs + mine;  // K-half 0 + K-half 1
     }
   }
 }
@@ -384,6 +491,9 @@ __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) 
     for (int i = 0; i < 4; ++i) v[nt][i] = acc[nt][i];
 }
 
+// KH: GEMM phases split 2 x 2 over the waves (gemm_kh, persist_opt 1024): a template parameter, so each variant
+// gets its own register allocation
+template <bool KH>
 __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -479,6 +589,16 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   }
   // An abandoned solve leaves NaN in this workgroup's part of x (every workgroup leaves through here or
   // finishes normally), so a failure can never pass for a result.
+  // seal mode: this workgroup's seal, written before each group signal; the check after each group wait
+  const bool seal = (P.opt & 16384) != 0;
+  auto seal_put = [&]() {
+    if (seal && tid == 0)
+      __hip_atomic_store(P.seal + 4 * (g * kSlots + s), L + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto seal_wait = [&](int g0, int ng) -> bool {
+    return !seal || seals_ok(P.seal + 4 * g0 * kSlots, ng * kSlots, L, P.ctr + CT_ERR, P.sticky + SY_FAILS, P.tmo,
+                             reinterpret_cast<int*>(smem + L_FLAG));
+  };
   auto fail_exit = [&]() {
     if (xr_row < nr) {
       P.xt[(size_t)(r0 + xr_row) * kC + xch] = __builtin_nanf("");
@@ -509,6 +629,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
       else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
     }
+    seal_put();
     signal(mygrp);
     ++L;
   };
@@ -526,6 +647,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (!arrive_wait(P.sticky + SY_ARRIVE0, (launch + 1) * kWGs, tmo, flag)) { fail_exit(); return; }
     if (tid < 4 && kCtrInts > 4 * (int)blockIdx.x + tid)
       __hip_atomic_store(P.ctr + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 4) __hip_atomic_store(P.seal + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (gran && tid < 32) {  // 512 B of the 128 KB granule block per workgroup
       const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
       st16(rq, (unsigned)((blockIdx.x * 32 + tid) * 16), u32x4{0u, 0u, 0u, 0u});
@@ -554,9 +676,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     // ------------------------------ proj_in (:361) ------------------------------
     const float binv[2] = {P.bin[col0 + c], P.bin[col0 + 16 + c]};
     PST(step);
-    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
+    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
-    gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    else gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     PST(step);
     acc_to(X, acc);
 #pragma unroll
@@ -567,6 +690,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     stage_tile<float>(stg, X, wave, lane);
     __syncthreads();
     flush_halo(stg, P.ximg, r0, nr, col0, T);
+    seal_put();
     if (dmafirst) {
       next_w(P.blk[0].w2);
       signal_dma<16>(mygrp);
@@ -608,7 +732,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         gbv = bw.gnb[col0 + tid];
       }
       PST(step);
-      if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
+      if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
       const int wa = max(r0 - kHalo, 0), wz = min(r0 + nr + kHalo, T);
       // Everything this phase reads that does not wait on another phase goes out first, so the loads'
@@ -789,6 +913,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.a2, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T, xloc);
+      seal_put();
       signal(mygrp);
       PST(step);
       ++L;
@@ -796,9 +921,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       // -------- conv_2 (1x1) + GELU (:90-91)
       const float b2v[2] = {bw.b2[col0 + c], bw.b2[col0 + 16 + c]};  // epilogue vectors before the wait
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+      if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    else gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
       {
         float v[2][4];
@@ -812,6 +938,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
+      seal_put();
       if (dmafirst) {
         next_w(bw.w3);
         signal_dma<16>(mygrp);
@@ -833,9 +960,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         alv[nt] = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
       }
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+      if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
       {
         float v[2][4];
@@ -856,6 +984,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.xa, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T, xloc);
+      seal_put();
       if (dmafirst) {
         if (fin) issue_out();  // conv_out's panel (into the other buffer; the flip follows the loop)
         else next_w(bw.m0);
@@ -873,10 +1002,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const float* fo0 = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
       const float fa0[2] = {fo0[col0 + c], fo0[col0 + 16 + c]}, fb0[2] = {fo0[H + col0 + c], fo0[H + col0 + 16 + c]};
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
       row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
-      gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);  // (its barrier orders the statistics)
+      if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);  // (its barrier orders the statistics)
       PST(step);
       {
         float v[2][4];
@@ -893,6 +1023,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       __syncthreads();
       if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
       else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
+      seal_put();
       if (dmafirst) {
         next_w(bw.m2);
         signal_dma<16>(mygrp);
@@ -906,9 +1037,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       // -------- mlp.2 + gated residual (:159-160)
       const float g2v[2] = {mb[5 * H + col0 + c], mb[5 * H + col0 + 16 + c]}, bm2[2] = {bw.mb2[col0 + c], bw.mb2[col0 + 16 + c]};
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+      if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
       PST(step);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
@@ -918,6 +1050,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       stage_tile<float>(stg, X, wave, lane);
       __syncthreads();
       flush_halo(stg, P.ximg, r0, nr, col0, T);
+      seal_put();
       if (dmafirst) {
         next_w(P.blk[blk + 1].w2);
         signal_dma<16>(mygrp);
@@ -944,10 +1077,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
     }
     PST(step);
-    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag)) { fail_exit(); return; }
+    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
     row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
-    gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     PST(step);
     float* yl = reinterpret_cast<float*>(stg);  // Y of the tile: [row][24] fp32 (tap-major x 8 channels)
 #pragma unroll
@@ -969,6 +1103,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const float* src = half == 0 ? yl + (nr - 1) * 24 + 4 * k : yl + 16 + 4 * k;
       st16(ry, (unsigned)(((g + kGroups * s) * 16 + half * 8 + 4 * k) * 4), __builtin_bit_cast(u32x4, *reinterpret_cast<const float4*>(src)));
     }
+    seal_put();
     if (dmafirst && step + 1 < P.s1) {
       next_win();
       signal_dma<4>(mygrp);
@@ -981,7 +1116,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
     // -------- Euler update x += dt * v, v[t] = b + Y1[t] + Y0[t-1] + Y2[t+1] (:445; conv3_combine order)
     PST(step);
-    if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag)) { fail_exit(); return; }
+    if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }
     PST(step);
     if (xr_row < nr) {
       const int t = r0 + xr_row;
@@ -1037,9 +1172,12 @@ int persist_stamps(void* buf, int step) {
 bool persist_device_ok(int device) {
   int cus = 0, nb = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus != kWGs) return false;
-  if (set_max_lds(reinterpret_cast<const void*>(den_persist_kernel)) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, den_persist_kernel, kThreads, kLds) != hipSuccess) return false;
-  return nb >= 1;
+  int nb2 = 0;
+  if (set_max_lds(reinterpret_cast<const void*>(den_persist_kernel<false>)) != hipSuccess) return false;
+  if (set_max_lds(reinterpret_cast<const void*>(den_persist_kernel<true>)) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, den_persist_kernel<false>, kThreads, kLds) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, den_persist_kernel<true>, kThreads, kLds) != hipSuccess) return false;
+  return nb >= 1 && nb2 >= 1;
 }
 
 int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
@@ -1052,7 +1190,8 @@ int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
   // (hipErrorCooperativeLaunchTooLarge) instead of queueing workgroups behind resident ones that wait for
   // them.  Capturable: a captured cooperative launch replays cooperatively (MI355X_MICROARCH.md, Residency).
   void* args[] = {&P};
-  const void* kern = reinterpret_cast<const void*>(den_persist_kernel);
+  const void* kern = (P.opt & 1024) ? reinterpret_cast<const void*>(den_persist_kernel<true>)
+                                    : reinterpret_cast<const void*>(den_persist_kernel<false>);
   const hipError_t e = cooperative ? hipLaunchCooperativeKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st)
                                    : hipLaunchKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st);
   if (e != hipSuccess) {

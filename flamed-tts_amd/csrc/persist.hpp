@@ -86,6 +86,7 @@ struct Params {
   float4* gnp;             // GroupNorm partials (n, mean, M2) per (group, channel): 8 x H
   float* yb;               // conv_out boundary rows per workgroup: Y0 of its last row, Y2 of its first
   int* ctr;
+  int* seal;               // persist_opt 16384: per (group, slot) the number of its last group hand-off (16 B each)
   int* sticky;             // kStickyInts words never reset between launches: [SY_FAILS] failed launches so far
                            // (the host reads it after the fact), [SY_ARRIVE0/1] the reset prologue's arrivals
   int inject_step = -1;    // diagnostic (flamed_tune persist_inject): every workgroup fails at this step

@@ -137,12 +137,14 @@ PERSIST_DEFAULT = 585  # flamed_tune persist_opt default (csrc/common.hpp Tune::
 
 
 @pytest.mark.parametrize("T", [400, 131, 16])
-@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1])
+@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 4096, 16384])
 def test_persist_variants_bitwise(pgb, T, flip):
     """Hand-off variants change where and how data moves, never the arithmetic: the default equals, bitwise,
     the default with row-major instead of fragment-major A images (bit 64), counter-based instead of
-    tagged-granule GroupNorm exchange (bit 512), and both plus the other weight-DMA wave split (bit 1), for
-    full, partial-tile and nearly-empty row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
+    tagged-granule GroupNorm exchange (bit 512), both plus the other weight-DMA wave split (bit 1), the
+    hand-off drain issued behind the next weight DMA (bit 4096), and the seal verification mode (bit 16384:
+    every group wait also checks the producers' hand-off seals), for full, partial-tile and nearly-empty
+    row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
     pg, _ = pgb
     x0, spk = _inputs(11, 1, T)
     from flamed import _native as nat
@@ -277,3 +279,20 @@ def test_solve_part_without_step0_rejected(pgb):
         rc = L.flamed_den_solve_part(hip.handle, nat.ptr(x), nat.ptr(mods), nfe, 1, T, nat.ptr(ws), ws.numel(), 1, G, nfe,
                                      nat.stream_ptr(DEV))
     assert rc == 1001
+
+
+def test_persist_seal_mode_cfg1(pgb):
+    """the configs[1] solve with every group hand-off sealed (persist_opt bit 16384: each
+    producer stores its hand-off number write-through ahead of the drain that precedes its counter add, and
+    every consumer checks the seals of all the producers it reads after its counter wait).  No seal may lag
+    its counter (a lag spins, then fails the launch with error 4 and NaN), and the result equals the unsealed
+    solve bitwise."""
+    pg, _ = pgb
+    hip = pg.denoiser.hip()
+    x0, spk = _inputs(26, 1, 400)
+    f0 = hip.persist_fails()
+    a = _solve(pg, x0, spk, 128)
+    with knob("persist_opt", PERSIST_DEFAULT ^ 16384, PERSIST_DEFAULT):
+        b = _solve(pg, x0, spk, 128)
+    assert hip.persist_fails() == f0
+    assert torch.isfinite(b).all() and torch.equal(a, b)
