@@ -90,6 +90,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"split_min_rows", &Tune::split_min_rows, 1024, 1 << 30, nullptr},
       {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
+      {"persist_multi", &Tune::persist_multi, 0, 1, nullptr},
       {"persist_capmode", &Tune::persist_capmode, 0, 1, nullptr},
       {"pva_persist", &Tune::pva_persist, 0, 1, nullptr},
       {"attn_mfma", &Tune::attn_mfma, 0, 1, nullptr},

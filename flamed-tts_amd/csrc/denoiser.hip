@@ -2297,8 +2297,16 @@ static bool persist_eligible(Den* d, int B, int T) {
   const Tune& tu = tn();
   persist_poll_fails(d);
   if (!tu.persist || d->pbroken || d->dt != FLAMED_BF16 || d->f8 || !d->fold || !tu.lnfold) return false;
-  if (B != 1 || T < 16 || T > pk::kMaxT || d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps)
-    return false;
+  if (d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps || T < 16) return false;
+  if (B == 1) {
+    if (T > pk::kMaxT) return false;
+  } else {
+    // several utterances (knob persist_multi): B in {2, 4, 8}, each utterance's frames split over its 8 / B
+    // row groups of at most kMaxRows frames
+    if (!tu.persist_multi || (B != 2 && B != 4 && B != 8)) return false;
+    const int gpu = pk::kGroups / B;
+    if ((T + gpu - 1) / gpu > pk::kMaxRows) return false;
+  }
   if (d->pdev_ok < 0) d->pdev_ok = pk::persist_device_ok(d->device) ? 1 : 0;
   return d->pdev_ok == 1;
 }
@@ -2306,13 +2314,13 @@ static bool persist_eligible(Den* d, int B, int T) {
 // Steps [s0, s1) of a B = 1 solve as ONE cooperative launch, enqueued on `st` with no host synchronisation:
 // the kernel (it resets its own counter block) and, outside a capture, HIP events around it plus an async
 // copy of the sticky failure word.  A failed launch NaN-poisons x and is reported by the next call / persist_info.
-static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int T, int s0, int s1, hipStream_t st) {
+static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, int T, int s0, int s1, hipStream_t st) {
   const bool cap = stream_capturing(st);
   FL_REQUIRE(d->pmem && d->pfail_host, "persistent solve: scratch not allocated at load");
   pk::Params P{};
   persist_layout(d->pmem, &P);
   d->pfail = P.sticky + pk::SY_FAILS;
-  P.T = T; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
+  P.T = T; P.B = B; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
   P.dt = (float)(1.0 / (double)nfe);
   P.mods = mods; P.MS = d->MS; P.MS0 = d->MS0;
   P.win = reinterpret_cast<const bf16*>(d->win); P.bin = d->bin;
@@ -2503,7 +2511,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   FL_REQUIRE(d->ppath >= 0 && d->ppath_key[0] == B && d->ppath_key[1] == T && d->ppath_key[2] == nfe,
              "flamed_den_solve_part: part [%d, %d) of a solve whose step-0 part did not run on this handle", s0, s1);
   if (d->ppath == 1) {  // one persistent launch for the whole range (B = 1)
-    const int prc = persist_solve(d, xt, mods, nfe, T, s0, s1, st);
+    const int prc = persist_solve(d, xt, mods, nfe, B, T, s0, s1, st);
     if (prc == kOk || s0 != 0 || prc != kBadArg) return prc;
     // the runtime refused the cooperative grid (not all 256 workgroups co-resident): this device never
     // runs the persistent solve; this solve (still at step 0) takes the graph of launches

@@ -55,17 +55,21 @@ __device__ __forceinline__ int opq(int v) {
 // shares, not whole 16-row tiles: every group's GEMM operand then moves the same bytes (T = 400: 50 rows
 // each, instead of one 64-row group pacing seven 48-row ones); rows past nr in a wave's last 16-row
 // fragment read as zero through the buffer range and are never stored.
-__device__ __forceinline__ void group_rows(int g, int T, int& r0, int& nr, int opt) {
-  if (opt & 2) {  // whole 16-row tiles [g MT / 8, (g + 1) MT / 8)
+// Several utterances (B = 2, 4 or 8, each of T frames; rows u T .. u T + T - 1): utterance u owns the 8 / B
+// groups u 8/B .. + 8/B - 1 and splits its frames among them the same way, so a group never spans two
+// utterances (its modulation row, GroupNorm statistics and zero padding are its utterance's).
+__device__ __forceinline__ void group_rows(int g, int T, int B, int& r0, int& nr, int opt) {
+  const int gpu = kGroups / B, u = g / gpu, gi = g - u * gpu;
+  if (opt & 2) {  // whole 16-row tiles [gi MT / gpu, (gi + 1) MT / gpu) of the utterance
     const int MT = (T + 15) >> 4;
-    const int tb = g * MT / kGroups, te = (g + 1) * MT / kGroups;
-    r0 = 16 * tb;
-    nr = max(min(16 * te, T) - r0, 0);
+    const int tb = gi * MT / gpu, te = (gi + 1) * MT / gpu;
+    r0 = u * T + 16 * tb;
+    nr = max(min(16 * te, T) - 16 * tb, 0);
     return;
   }
-  const int R = (T + kGroups - 1) / kGroups;
-  r0 = g * R;
-  nr = max(min(R, T - r0), 0);
+  const int R = (T + gpu - 1) / gpu;
+  r0 = u * T + gi * R;
+  nr = max(min(R, T - gi * R), 0);
 }
 
 // ---- hand-off primitives ----
@@ -498,7 +502,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int T = P.T;
+  const int T = P.T;            // frames per utterance
+  const int TT = P.B * P.T;     // rows of the batch (buffer ranges)
   const int H = kH;
   // Group / slot: group = blockIdx % 8 (the round-robin dispatch puts it on one XCD: speed only).
   int g = blockIdx.x % kGroups, s = blockIdx.x / kGroups;
@@ -516,7 +521,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   const bool frag = (P.opt & 64) != 0;        // fragment-major GEMM A images (a2, u, xa, xs)
   const bool gran = (P.opt & 512) != 0;       // GroupNorm partials as tagged granules (gnp zeroed per launch)
   int r0, nr;
-  group_rows(g, T, r0, nr, P.opt);
+  group_rows(g, T, P.B, r0, nr, P.opt);
+  const int gpu = kGroups / P.B, utt = g / gpu;  // this group's utterance and its frames [ub, ue)
+  const int ub = utt * T, ue = ub + T;
   const int c = lane & 15, q = lane >> 4;
   const int col0 = kCols * s;
   char* stg = smem + L_HS;  // epilogue staging (aliases the dwconv window)
@@ -624,7 +631,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         else st16(rs, off, v);
       }
     } else if (tid < nr) {
-      const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)T * kC * 2);
+      const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)TT * kC * 2);
       const unsigned off = (unsigned)(((size_t)(r0 + tid) * kC + kCh * s) * 2);
       if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
       else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
@@ -663,7 +670,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   f32x4 acc[2];
 
   for (int step = P.s0; step < P.s1; ++step) {
-    const float* md = P.mods + (size_t)step * P.MS;
+    const float* md = P.mods + (size_t)(step * P.B + utt) * P.MS;  // this utterance's modulation row
     cur_step = step;
     if (step == P.inject_step) {  // diagnostic failure injection: every workgroup abandons here
       if (tid == 0) raise_err(errw, fails, 3);
@@ -689,7 +696,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
     stage_tile<float>(stg, X, wave, lane);
     __syncthreads();
-    flush_halo(stg, P.ximg, r0, nr, col0, T);
+    flush_halo(stg, P.ximg, r0, nr, col0, TT);
     seal_put();
     if (dmafirst) {
       next_w(P.blk[0].w2);
@@ -734,22 +741,22 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
-      const int wa = max(r0 - kHalo, 0), wz = min(r0 + nr + kHalo, T);
+      const int wa = max(r0 - kHalo, ub), wz = min(r0 + nr + kHalo, ue);  // the utterance's frames only
       // Everything this phase reads that does not wait on another phase goes out first, so the loads'
       // latencies overlap: the thread's 3 window items (its 4 columns col0 + 4 (tid & 7) are the same in
       // every item), their modulation vectors, the depthwise taps of channel cc, the row statistics.
       constexpr int kItems = (kWin * 8 + kThreads - 1) / kThreads;
       float4 hv[kItems];
       {
-        const __amdgpu_buffer_rsrc_t rx = rsrc(P.ximg, (unsigned)T * H * 4);
+        const __amdgpu_buffer_rsrc_t rx = rsrc(P.ximg, (unsigned)TT * H * 4);
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
           const int idx = tid + k * kThreads, p = idx >> 3, r = r0 - kHalo + p;
-          const bool halo = idx < kWin * 8 && (p < kHalo || p >= kHalo + nr) && r >= 0 && r < T;
+          const bool halo = idx < kWin * 8 && (p < kHalo || p >= kHalo + nr) && r >= ub && r < ue;
           hv[k] = halo ? as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * (tid & 7)) * 4))) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      row_stats(P.xpart[0], T, wa, wz, r0 - kHalo, st);
+      row_stats(P.xpart[0], TT, wa, wz, r0 - kHalo, st);
       __syncthreads();
       PST(step);  // halo rows + row statistics in
       // window h[p] (frame r0 - 15 + p): own rows from X (registers), halo rows from ximg, 0 outside [0, T)
@@ -758,7 +765,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         const int idx = tid + k * kThreads, p = idx >> 3, r = r0 - kHalo + p;
         if (idx < kWin * 8 && (p < kHalo || p >= kHalo + nr)) {
           float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r >= 0 && r < T) {
+          if (r >= ub && r < ue) {
             const float mean = st[2 * p], rstd = st[2 * p + 1];
             o.x = ((hv[k].x - mean) * rstd) * hva[0] + hvb[0];
             o.y = ((hv[k].y - mean) * rstd) * hva[1] + hvb[1];
@@ -876,7 +883,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
             for (int k = 0; k < kGroups; ++k) {
               int ka, kn;
-              group_rows(k, T, ka, kn, P.opt);
+              group_rows(k, T, P.B, ka, kn, P.opt);
+              if (k / gpu != utt) kn = 0;  // another utterance's group: not part of these statistics
               chan_combine(n, mean, m2, (float)kn, kn > 0 ? mv[k] : 0.f, kn > 0 ? qv[k] : 0.f);
             }
             const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
@@ -897,7 +905,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
         for (int k = 0; k < kGroups; ++k) {
           const float4 v = as_f4(ld16(rq, (unsigned)((k * H + col0 + tid) * 16)));
-          chan_combine(n, mean, m2, v.x, v.y, v.z);
+          chan_combine(n, mean, m2, k / gpu == utt ? v.x : 0.f, v.y, v.z);  // this utterance's groups only
         }
         const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
         gnv[tid] = make_float4(mean, sc, gbv, 0.f);
@@ -912,7 +920,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
       __syncthreads();
       if (frag) flush_frag(stg, P.a2, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, T, xloc);
+      else flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       signal(mygrp);
       PST(step);
@@ -937,7 +945,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
       __syncthreads();
       if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
+      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       if (dmafirst) {
         next_w(bw.w3);
@@ -983,7 +991,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
       __syncthreads();
       if (frag) flush_frag(stg, P.xa, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, T, xloc);
+      else flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       if (dmafirst) {
         if (fin) issue_out();  // conv_out's panel (into the other buffer; the flip follows the loop)
@@ -1004,7 +1012,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
+      row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
       if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);  // (its barrier orders the statistics)
       PST(step);
@@ -1022,7 +1030,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
       __syncthreads();
       if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, T, xloc);
+      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       if (dmafirst) {
         next_w(bw.m2);
@@ -1049,7 +1057,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
       stage_tile<float>(stg, X, wave, lane);
       __syncthreads();
-      flush_halo(stg, P.ximg, r0, nr, col0, T);
+      flush_halo(stg, P.ximg, r0, nr, col0, TT);
       seal_put();
       if (dmafirst) {
         next_w(P.blk[blk + 1].w2);
@@ -1079,7 +1087,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     PST(step);
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
-    row_stats(P.xpart[1], T, r0, r0 + nr, r0 - kHalo, st);
+    row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
     if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
     PST(step);
@@ -1123,7 +1131,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       int gp = 0, gn_ = 0;  // the groups owning frames r0 - 1 and r0 + nr (nearest non-empty neighbours)
       for (int k = 0; k < kGroups; ++k) {
         int a, b;
-        group_rows(k, T, a, b, P.opt);
+        group_rows(k, T, P.B, a, b, P.opt);
         if (b > 0 && a + b == r0) gp = k;
         if (b > 0 && a == r0 + nr) gn_ = k;
       }
@@ -1133,13 +1141,13 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       for (int e = 0; e < 2; ++e) {
         const int chl = 2 * (tid & 3) + e, ch = kCh * s + chl;
         float v = P.bout[ch] + yl[xr_row * 24 + 8 + chl];
-        if (t > 0) {
+        if (t > ub) {  // zero padding at the utterance's edges (conv_out k3)
           const float y0 = xr_row > 0 ? yl[(xr_row - 1) * 24 + chl]
                                       : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                             ry, (unsigned)(((gp + kGroups * s) * 16 + chl) * 4), 0, 16));
           v += y0;
         }
-        if (t < T - 1) {
+        if (t < ue - 1) {
           const float y2 = xr_row < nr - 1 ? yl[(xr_row + 1) * 24 + 16 + chl]
                                            : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                  ry, (unsigned)(((gn_ + kGroups * s) * 16 + 8 + chl) * 4), 0, 16));

@@ -64,6 +64,7 @@ struct BlockW {
 
 struct Params {
   int T, NB, s0, s1;
+  int B = 1;               // utterances (1, 2, 4 or 8), each T frames: utterance u owns row groups u 8/B .. + 8/B - 1
   float dt;
   const float* mods;
   int MS, MS0;

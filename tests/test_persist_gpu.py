@@ -296,3 +296,25 @@ def test_persist_seal_mode_cfg1(pgb):
         b = _solve(pg, x0, spk, 128)
     assert hip.persist_fails() == f0
     assert torch.isfinite(b).all() and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,T", [(2, 200), (4, 100), (8, 64), (2, 37)])
+def test_persist_multi_utterance(pgb, B, T):
+    """the persistent solve for several equal-length utterances (knob persist_multi; each
+    utterance's frames split over its 8 / B row groups, so its modulation row, GroupNorm statistics over T and
+    zero padding stay its own).  Every utterance against a one-utterance oracle solve (equal lengths: no
+    padding coupling; prob_generator.py:439-447) at the bf16 solve bar, and the batch against the graph of
+    launches (same bf16 operands, other fp32 order) at 4e-3."""
+    pg, sd = pgb
+    x0, spk = _inputs(30 + B, B, T)
+    with knob("persist_multi", 1, 0):
+        r0 = _runs(pg)
+        out = _solve(pg, x0, spk, 8)
+        assert _runs(pg) == r0 + 1, "the multi-utterance solve did not take the persistent path"
+        with knob("persist", 0, 1):
+            launch = _solve(pg, x0, spk, 8)
+    assert torch.isfinite(out).all()
+    el = rel_l2(out, launch)
+    errs = [rel_l2(out[b:b + 1], orc.euler_solve(sd, x0[b:b + 1], spk[b:b + 1], 8)) for b in range(B)]
+    print(f"persistent B={B} T={T} 8 steps: vs oracle per utterance max {max(errs):.3e}; vs launch path {el:.3e}")
+    assert max(errs) < BF16_SOLVE and el < 4e-3
