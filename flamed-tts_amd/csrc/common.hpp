@@ -173,7 +173,7 @@ struct Tune {
   int dwgn_small = 1;      // small-M bf16 path: one-workgroup-per-8-channels depthwise conv + GroupNorm (T <= 576)
   int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in
   int persist = 1;         // B = 1 bf16 solves: one persistent launch for all steps (persist.hpp)
-  int split_batch = 2;     // large-M bf16 solves: sub-batch chains run as parallel graph branches (den_split)
+  int split_batch = 1;     // large-M bf16 solves: sub-batch chains as parallel graph branches (den_split; opt-in)
   int split_min_rows = 6144;  // ... when every chain still has this many rows
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_multi = 0;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)

@@ -1720,12 +1720,17 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
 }
 static size_t den_ws_bytes(const Den* d, int B, int T) { return den_ws_layout(d, B, T, nullptr, nullptr); }
 
-// Large-M solves as concurrent sub-batches (tune split_batch, default 2): utterances are independent in the
-// denoiser (GroupNorm statistics and the depthwise halo never cross an utterance: prob_generator.py:81-89), so
-// the batch's Euler steps run as S chains of B / S utterances, captured as S parallel branches of one graph.
+// Large-M solves as concurrent sub-batches (tune split_batch, opt-in, default 1): utterances are independent in
+// the denoiser (GroupNorm statistics and the depthwise halo never cross an utterance: prob_generator.py:81-89),
+// so the batch's Euler steps run as S chains of B / S utterances, captured as S parallel branches of one graph.
 // One chain's inter-kernel gaps and the partly filled last round of its GEMM tiles are then covered by the
-// other chain's kernels.  Every chain is the same step structure at B / S (so a split solve is bitwise the
-// split eager loop); fp8 handles keep one chain (their MX GEMMs need the large tiles of the whole batch).
+// other chain's kernels (B = 64: 336 -> 302 ms).  Opt-in because overlapped chains are NOT bitwise
+// reproducible: with the whole-utterance dwgn kernel on, a velocity evaluation run while another handle's (or
+// chain's) kernels run on a second stream differs from the same evaluation run alone (up to 5e-2 in v, whole
+// utterances; tools/conc_vel2.py), although the chains share no memory (own workspace, counters, step
+// counter) and in-kernel canaries saw neither dwgn's inputs change nor its LDS corrupted; with dwgn = 0 (or
+// the chains captured serially) every run is bitwise equal.  Cause not found.  fp8
+// handles keep one chain (their MX GEMMs need the large tiles of the whole batch).
 static int den_split(const Den* d, int B, int T) {
   const Tune& tu = tn();
   const int S = tu.split_batch;
@@ -2031,17 +2036,20 @@ namespace fl {
 // mods + (*ctr) * B * MS and the last kernel increments it (graph replay of captured steps).
 template <typename DT, typename XT>
 static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout,
-                         const DenWs& w, int* ctr, hipStream_t st, const float* xsrc, int Bs) {
+                         const DenWs& w, int* ctr, hipStream_t st, const float* xsrc, int Bs, int chain, int nchains) {
   const int M = B * T, H = d->H, C = d->C, MS = d->MS;
   const Tune& tu = tn();
   // a step's modulation rows are Bs apart (Bs = B, or the whole batch when this is one of its sub-batches)
   const StepOff so{tu.noctr ? nullptr : ctr, (long long)Bs * MS};
   SplitCtx sctx;
-  sctx.slab = w.SL; sctx.slab_floats = w.SLn; sctx.cnt = d->scnt; sctx.cnt_n = Den::kSplitCounters;
+  // sub-batch chains (den_split) each own 1/nchains of the split-K and GroupNorm counters
+  const int scn = Den::kSplitCounters / nchains, gcn = Den::kGnCounters / nchains;
+  sctx.slab = w.SL; sctx.slab_floats = w.SLn; sctx.cnt = d->scnt ? d->scnt + (size_t)chain * scn : nullptr;
+  sctx.cnt_n = scn;
   sctx.target = tu.split_target; sctx.max_split = tu.split_max;
   SplitScope split_scope(w.SLn ? &sctx : nullptr);
   // GroupNorm finalize fused into the depthwise-conv kernel when the counters cover B x H/64
-  int* gcnt = (d->gcnt && (size_t)B * (H / 16) <= (size_t)Den::kGnCounters) ? d->gcnt : nullptr;  // >= 16-channel groups
+  int* gcnt = (d->gcnt && (size_t)B * (H / 16) <= (size_t)gcn) ? d->gcnt + (size_t)chain * gcn : nullptr;  // >= 16-channel groups
   const GemmCfg cfg = (tu.bn32 && M < kTinyRows) ? kCfgTiny
                       : (std::is_same<DT, bf16>::value && tu.big && M >= tu.big_min_rows) ? kCfgLarge : pick_cfg(M);
   const bool big = std::is_same<DT, bf16>::value && cfg == kCfgLarge && tu.big;
@@ -2194,15 +2202,16 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
 }
 
 static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, int T, float dt, float* vout, void* ws,
-                    hipStream_t st, int* ctr = nullptr, const float* xsrc = nullptr, int Bs = 0) {
+                    hipStream_t st, int* ctr = nullptr, const float* xsrc = nullptr, int Bs = 0, int chain = 0,
+                    int nchains = 1) {
   if (Bs <= 0) Bs = B;
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   if (d->dt == FLAMED_BF16) {
-    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs);
-    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs);
+    if (den_x16(d, B, T)) return den_step_impl<bf16, bf16>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs, chain, nchains);
+    return den_step_impl<bf16, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs, chain, nchains);
   }
-  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs);
+  return den_step_impl<float, float>(d, xt, mods, mod_div, B, T, dt, vout, w, ctr, st, xsrc, Bs, chain, nchains);
 }
 
 // The fused Euler step (LoadEulerIn) runs where proj_in takes the small-M register loop with one
@@ -2491,7 +2500,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
       for (int k = 0; k < S; ++k) {
         float* xk; const float* mk; void* wk;
         sub(k, xk, mk, wk);
-        int rc = den_step(d, xk, mk + s * step_stride, T, Bk, T, dt, nullptr, wk, st, nullptr, nullptr, B);
+        int rc = den_step(d, xk, mk + s * step_stride, T, Bk, T, dt, nullptr, wk, st, nullptr, nullptr, B, k, S);
         if (rc) return rc;
       }
     return kOk;
@@ -2546,7 +2555,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
       hipStream_t cs = k == 0 ? d->cap_stream : d->cap_aux[k];
       for (int s = 0; s < G && rc == kOk; ++s) {
         if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, cs, d->ctr, s % 2 ? xt : w.XP);
-        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, nullptr, B);
+        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, nullptr, B, k, S);
       }
     }
     for (int k = 1; k < S && rc == kOk; ++k) {  // join
