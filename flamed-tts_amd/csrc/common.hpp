@@ -176,7 +176,7 @@ struct Tune {
   int split_batch = 1;     // large-M bf16 solves: sub-batch chains as parallel graph branches (den_split; opt-in)
   int split_min_rows = 6144;  // ... when every chain still has this many rows
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
-  int persist_multi = 0;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
+  int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
   int persist_opt = 585;   // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange

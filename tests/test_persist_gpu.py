@@ -128,8 +128,12 @@ def test_persist_knob_off_uses_launch_path(pgb):
     with knob("persist", 0, 1):
         _solve(pg, x0, spk, 4)
     assert _runs(pg) == r0
-    x2, spk2 = _inputs(8, 2, 64)  # B = 2: never persistent
-    _solve(pg, x2, spk2, 4)
+    x2, spk2 = _inputs(8, 2, 64)  # B = 2 with persist_multi off: the graph of launches
+    with knob("persist_multi", 0, 1):
+        _solve(pg, x2, spk2, 4)
+    assert _runs(pg) == r0
+    x3, spk3 = _inputs(9, 3, 64)  # B = 3 (not 2 / 4 / 8): never persistent
+    _solve(pg, x3, spk3, 4)
     assert _runs(pg) == r0
 
 
@@ -307,7 +311,7 @@ def test_persist_multi_utterance(pgb, B, T):
     launches (same bf16 operands, other fp32 order) at 4e-3."""
     pg, sd = pgb
     x0, spk = _inputs(30 + B, B, T)
-    with knob("persist_multi", 1, 0):
+    with knob("persist_multi", 1, 1):  # the default since round 4 (1.55-1.6x the graph of launches)
         r0 = _runs(pg)
         out = _solve(pg, x0, spk, 8)
         assert _runs(pg) == r0 + 1, "the multi-utterance solve did not take the persistent path"
