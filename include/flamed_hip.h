@@ -179,6 +179,12 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "persist_opt"   — persistent kernel variant bits (diagnostic A/B; default 585);
  *   "persist_inject"— diagnostic: every persistent launch fails at this step (-1 default = never), to
  *                     exercise the NaN poisoning / failure count / retry budget;
+ *   "persist_multi" — 1 (default): B = 2 / 4 / 8 equal-length utterances with at most 64 frames per row
+ *                     group (T <= 512 / B) also run as one persistent launch; 0: B = 1 only;
+ *   "persist_capmode" — persistent launch inside a stream capture: 0 (default) cooperative node, 1 plain;
+ *   "split_batch"   — large-M bf16 solves as this many concurrent sub-batch chains (parallel graph
+ *                     branches; 1 = default, off: overlapped chains are not bitwise reproducible);
+ *   "split_min_rows"— ... only when every chain keeps at least this many rows (default 6144);
  *   "pva_split"     — 1: the PVA nets' small-M exact-fp32 GEMMs split K over workgroups
  *                     (per-handle slabs, fixed slice order: deterministic); 0 (default: measured
  *                     no faster): one K chain;
