@@ -28,11 +28,11 @@ def main():
     spk = [torch.randn(B, 256, generator=g).to(dev) for _ in range(2)]
     ts = torch.linspace(0, 1, nfe + 1, device=dev)
     hips = [pg.denoiser.hip(), pg2.denoiser.hip()]
-    sets = [[("dwgn_diag", v)] for v in (0, 16, 24)] if os.environ.get("DIAG") else [[], [("dwgn", 0)], [("x16", 1)]]
+    sets = [[], [("dwgn", 0)], [("x16", 1)]]
     for knobs in sets:
         for k_, v_ in knobs:
             nat.check(L.flamed_tune(k_.encode(), v_), "tune")
-        for graph in ((False,) if os.environ.get("DIAG") else (False, True)):
+        for graph in (False, True):
             pg.denoiser.hip_graph = pg2.denoiser.hip_graph = graph
             with torch.inference_mode():
                 ser = [hips[i].solve(xs[i], ts, spk[i], nfe).clone() for i in range(2)]
@@ -51,7 +51,7 @@ def main():
                 d = [float((o[i] - ser[i]).abs().max()) for i in range(2)]
                 print(f"knobs {knobs} graph {graph} rep {rep}: concurrent vs serial max|d| {d[0]:.3e} {d[1]:.3e}", flush=True)
         for k_, v_ in knobs:
-            L.flamed_tune(k_.encode(), {"dwgn": 1, "x16": 0, "dwgn_diag": 0}[k_])
+            L.flamed_tune(k_.encode(), {"dwgn": 1, "x16": 0}[k_])
 
 
 if __name__ == "__main__":

@@ -33,10 +33,9 @@ def main():
     hip = pg.denoiser.hip()
     res = {}
     with torch.inference_mode():
-        for S, serial in ((1, 0), (2, 0), (2, 1)):
+        for S, serial in ((1, 0), (2, 0)):
             nat.check(L.flamed_tune(b"split_batch", S), "tune")
-            nat.check(L.flamed_tune(b"split_serial", serial), "tune")
-            for graph in ((True, True, False) if not serial else (True, True)):
+            for graph in (True, True, False):
                 pg.denoiser.hip_graph = graph
                 out = hip.solve(x0, ts, spk, nfe)
                 torch.cuda.synchronize()
@@ -44,25 +43,6 @@ def main():
                 key = key + "2" if key in res else key
                 res[key] = out.clone()
         pg.denoiser.hip_graph = True
-        if os.environ.get("SPLIT_BISECT"):
-            for knobs in ([], [("dwgn", 0)], [("lnfold", 0)], [("x16", 1)], [("dwgn", 0), ("lnfold", 0)]):
-                for k_, v_ in knobs:
-                    nat.check(L.flamed_tune(k_.encode(), v_), "tune")
-                outs = []
-                for serial in (1, 0, 0):
-                    nat.check(L.flamed_tune(b"split_batch", 2), "tune")
-                    nat.check(L.flamed_tune(b"split_serial", serial), "tune")
-                    pg.denoiser.hip_graph = True
-                    outs.append(hip.solve(x0, ts, spk, nfe).clone())
-                    torch.cuda.synchronize()
-                d1 = (outs[1] - outs[0]).abs().amax(dim=(1, 2))
-                d2 = (outs[2] - outs[0]).abs().amax(dim=(1, 2))
-                bad1 = [int(i) for i in torch.nonzero(d1 > 0).flatten()]
-                bad2 = [int(i) for i in torch.nonzero(d2 > 0).flatten()]
-                print(f"knobs {knobs}: concurrent vs serial max {float(d1.max()):.3e} utts {bad1}; run2 {float(d2.max()):.3e} utts {bad2}",
-                      flush=True)
-                for k_, v_ in knobs:
-                    L.flamed_tune(k_.encode(), {"dwgn": 1, "lnfold": 1, "x16": 0}[k_])
     ks = list(res)
     for i in range(len(ks)):
         for j in range(i + 1, len(ks)):
