@@ -5,6 +5,7 @@ a call fails — there is no silent fallback to PyTorch ops.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -105,6 +106,47 @@ DIAG_SIGNATURES = {
 FLAMED_F32, FLAMED_BF16, FLAMED_FP8 = 0, 1, 2
 DTYPES = {"f32": FLAMED_F32, "fp32": FLAMED_F32, "float32": FLAMED_F32, "bf16": FLAMED_BF16, "bfloat16": FLAMED_BF16,
           "fp8": FLAMED_FP8}  # fp8: denoiser handles only (MX-fp8 pointwise GEMMs at large M, bf16 elsewhere)
+
+
+_live = {}  # address of every handle this process created and has not destroyed -> its destroy function
+
+
+def track(h, destroy_fn: str):
+    """Record a created handle, so that an interpreter exit releases it while the HIP runtime (and any
+    profiler attached to it) is still up, instead of leaving its streams / events / graphs / pinned words to
+    the runtime's own teardown."""
+    with _lock:
+        _live[int(h.value)] = destroy_fn
+    return h
+
+
+def destroy(h, destroy_fn: str) -> None:
+    """Destroy a tracked handle once (later calls, e.g. a __del__ after the exit hook, are no-ops)."""
+    if h is None or not h.value:
+        return
+    with _lock:
+        owned = _live.pop(int(h.value), None)
+    if owned is not None:
+        getattr(lib(), destroy_fn)(h)
+
+
+@atexit.register
+def _release_all() -> None:
+    with _lock:
+        items = list(_live.items())
+        _live.clear()
+    if not items:
+        return
+    try:
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+    for addr, fn in items:
+        try:
+            getattr(lib(), fn)(ctypes.c_void_p(addr))
+        except Exception:
+            pass
 
 
 def lib():

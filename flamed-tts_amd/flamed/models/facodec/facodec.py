@@ -388,7 +388,7 @@ class FacDecoderHIP:
     def __del__(self):
         try:
             if self.handle is not None:
-                nat.lib().flamed_fac_destroy(self.handle)
+                nat.destroy(self.handle, "flamed_fac_destroy")
         except Exception:
             pass
 
@@ -405,6 +405,7 @@ class FacDecoderHIP:
                                           len(self.dec.up_ratios), ups, nat.dtype_code(self.dtype_name),
                                           ctypes.byref(h)), "flamed_fac_create")
             self.handle = h
+            nat.track(h, "flamed_fac_destroy")
         keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
         arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
         nat.check(L.flamed_fac_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_fac_load")
@@ -471,7 +472,7 @@ class EncoderHIP:
     def __del__(self):
         try:
             if self.handle is not None:
-                nat.lib().flamed_enc_destroy(self.handle)
+                nat.destroy(self.handle, "flamed_enc_destroy")
         except Exception:
             pass
 
@@ -482,6 +483,7 @@ class EncoderHIP:
             nat.check(nat.lib().flamed_enc_create(self.enc.ngf, len(self.enc.up_ratios), ups, self.enc.out_channels,
                                                   nat.dtype_code(self.dtype_name), ctypes.byref(h)), "flamed_enc_create")
             self.handle = h
+            nat.track(h, "flamed_enc_destroy")
 
     def _ensure(self, dev):
         params = enc_weight_list(self.enc)
@@ -557,7 +559,7 @@ class VqHIP:
     def __del__(self):
         try:
             if self.handle is not None:
-                nat.lib().flamed_vq_destroy(self.handle)
+                nat.destroy(self.handle, "flamed_vq_destroy")
         except Exception:
             pass
 
@@ -584,6 +586,7 @@ class VqHIP:
             d = self.dims()
             nat.check(L.flamed_vq_create((ctypes.c_int * len(d))(*d), len(d), ctypes.byref(h)), "flamed_vq_create")
             self.handle = h
+            nat.track(h, "flamed_vq_destroy")
         keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
         arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
         nat.check(L.flamed_vq_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_vq_load")

@@ -165,7 +165,7 @@ class PriorHIP:
     def __del__(self):
         try:
             if self.handle is not None:
-                nat.lib().flamed_prior_destroy(self.handle)
+                nat.destroy(self.handle, "flamed_prior_destroy")
         except Exception:
             pass
 
@@ -194,6 +194,7 @@ class PriorHIP:
             d = self.dims()
             nat.check(L.flamed_prior_create((ctypes.c_int * len(d))(*d), len(d), ctypes.byref(h)), "flamed_prior_create")
             self.handle = h
+            nat.track(h, "flamed_prior_destroy")
         keep = [p.detach().to(device=dev, dtype=torch.float32).contiguous() for p in params]
         arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
         nat.check(L.flamed_prior_load(self.handle, arr, len(keep), nat.stream_ptr(dev)), "flamed_prior_load")

@@ -379,7 +379,7 @@ class DenoiserHIP:
     def __del__(self):
         try:
             if self.handle is not None:
-                nat.lib().flamed_den_destroy(self.handle)
+                nat.destroy(self.handle, "flamed_den_destroy")
         except Exception:
             pass
 
@@ -395,6 +395,7 @@ class DenoiserHIP:
             nat.check(L.flamed_den_create(d.in_channels, d.model_channels, d.num_res_blocks, d.kernel_size,
                                           d.spk_dim, self.code, ctypes.byref(h)), "flamed_den_create")
             self.handle = h
+            nat.track(h, "flamed_den_destroy")
         keep = [p.detach().to(device=device, dtype=torch.float32).contiguous() for p in params]
         arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
         nat.check(L.flamed_den_load(self.handle, arr, len(keep), nat.stream_ptr(device)), "flamed_den_load")
@@ -539,7 +540,7 @@ class CondFoldHIP:
     def __del__(self):
         try:
             if self.handle is not None:
-                nat.lib().flamed_cond_destroy(self.handle)
+                nat.destroy(self.handle, "flamed_cond_destroy")
         except Exception:
             pass
 
@@ -555,6 +556,7 @@ class CondFoldHIP:
             nat.check(L.flamed_cond_create(q, d, self.pg.target_dim, self.pg.n_stages, self.code, ctypes.byref(h)),
                       "flamed_cond_create")
             self.handle = h
+            nat.track(h, "flamed_cond_destroy")
         keep = [p.detach().to(device=device, dtype=torch.float32).contiguous() for p in params]
         arr = (ctypes.c_void_p * len(keep))(*[t.data_ptr() for t in keep])
         nat.check(L.flamed_cond_load(self.handle, arr, len(keep), nat.stream_ptr(device)), "flamed_cond_load")

@@ -260,7 +260,7 @@ class PvaHIP:
         try:
             for h in self.handles:
                 if h is not None:
-                    nat.lib().flamed_dur_destroy(h)
+                    nat.destroy(h, "flamed_dur_destroy")
         except Exception:
             pass
 
@@ -277,6 +277,7 @@ class PvaHIP:
                 h = ctypes.c_void_p()
                 nat.check(L.flamed_dur_create(g.input_size, g.filter_size, g.kernel, ctypes.byref(h)), "flamed_dur_create")
                 self.handles[i] = h
+                nat.track(h, "flamed_dur_destroy")
             ws = [w.detach().to(device=dev, dtype=torch.float32).contiguous() for w in g.hip_weights()]
             arr = (ctypes.c_void_p * len(ws))(*[t.data_ptr() for t in ws])
             nat.check(L.flamed_dur_load(self.handles[i], arr, len(ws), nat.stream_ptr(dev)), "flamed_dur_load")
