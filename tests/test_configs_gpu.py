@@ -146,6 +146,30 @@ def test_cfg2_solve_128(pg_bf16, cfg2):
         assert e_ref < BF16_SOLVE and e_one < BF16_SOLVE
 
 
+def test_cfg2_split_batch_within_bf16_bar(pg_bf16, cfg2):
+    """Opt-in split_batch 2 (two sub-batch chains as parallel graph branches, denoiser.hip den_split): the
+    chains overlap on the device and are not bitwise reproducible, so the opt-in path is
+    held to the bf16 bars instead: against the single-chain solve (same bf16 operands) at the persistent-vs-
+    launch bar, and utterances 0 / 63 (one per chain) against the oracle at the solve bar."""
+    from flamed import _native as nat
+    pg, sd = pg_bf16
+    x0, spk = cfg2
+    base = _solve(pg, x0, spk, 128)
+    L = nat.lib()
+    nat.check(L.flamed_tune(b"split_batch", 2), "flamed_tune")
+    try:
+        sp = _solve(pg, x0, spk, 128)
+    finally:
+        nat.check(L.flamed_tune(b"split_batch", 1), "flamed_tune")
+    assert torch.isfinite(sp).all()
+    e = rel_l2(sp, base)
+    print(f"configs[2] split_batch 2 vs 1 rel-L2 {e:.3e}")
+    assert e < 4e-3
+    for i in (0, 63):
+        ref = orc.euler_solve(sd, x0[i:i + 1], spk[i:i + 1], 128)
+        assert rel_l2(sp[i:i + 1], ref) < BF16_SOLVE
+
+
 @pytest.fixture(scope="module")
 def cfg4(pg_bf16):
     return _inputs(4, 1, 2400)
