@@ -107,9 +107,10 @@ FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe);
  * stream-ordered and use the same arguments apart from s0 / s1. */
 FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                      size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t stream);
-/* The persistent B = 1 solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken
- * by flamed_den_solve / _solve_part with use_graph != 0 for one utterance of 16..512 frames on a bf16
- * handle; decided once per solve by its step-0 part, and later parts follow it).  The launch is
+/* The persistent solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken by
+ * flamed_den_solve / _solve_part with use_graph != 0 on a bf16 handle for one utterance of 16..512 frames,
+ * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances of at most 512 / B frames;
+ * decided once per solve by its step-0 part, and later parts follow it).  The launch is
  * cooperative (all workgroups co-resident or refused up front, then this device uses the graph of launches)
  * and is only ENQUEUED: no host synchronisation, so it may be captured into a hipGraph (the captured node
  * replays cooperatively).  A launch whose in-kernel wait times out leaves NaN in xt and adds one to a sticky
