@@ -133,3 +133,27 @@ def test_tune_is_thread_safe(lib):
         t.join()
     assert not errs
     assert lib.flamed_tune(b"graph_steps", 16) == 0
+
+
+def test_tracked_handles_released_once(lib):
+    """flamed/_native.py track / destroy / the atexit hook: a tracked handle is destroyed exactly once (a later
+    __del__ after the exit hook is a no-op), and the exit hook releases what is still alive."""
+    from flamed import _native
+    h = ctypes.c_void_p()
+    assert lib.flamed_den_create(256, 1024, 4, 31, 256, 1, ctypes.byref(h)) == 0
+    _native.track(h, "flamed_den_destroy")
+    assert int(h.value) in _native._live
+    _native.destroy(h, "flamed_den_destroy")
+    assert int(h.value) not in _native._live
+    _native.destroy(h, "flamed_den_destroy")  # second call: no-op (no double free)
+    h2 = ctypes.c_void_p()
+    assert lib.flamed_dur_create(192, 384, 3, ctypes.byref(h2)) == 0
+    saved = dict(_native._live)  # other tests' live handles stay out of this hook run
+    _native._live.clear()
+    try:
+        _native.track(h2, "flamed_dur_destroy")
+        _native._release_all()
+        assert not _native._live
+        _native.destroy(h2, "flamed_dur_destroy")  # after the hook: no-op
+    finally:
+        _native._live.update(saved)
