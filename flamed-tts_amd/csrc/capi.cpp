@@ -95,6 +95,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"pva_persist", &Tune::pva_persist, 0, 1, nullptr},
       {"attn_mfma", &Tune::attn_mfma, 0, 1, nullptr},
       {"prior_split", &Tune::prior_split, 0, 1, nullptr},
+      {"stop_after", &Tune::stop_after, -1, 1 << 20, nullptr},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(k.name, key) != 0) continue;

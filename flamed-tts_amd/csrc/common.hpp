@@ -186,6 +186,7 @@ struct Tune {
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)
   int attn_mfma = 1;       // transformer attention (prior stack, timbre encoder) on fp32 MFMA (xfmr.hpp)
   int prior_split = 1;     // bf16 prior decoders: split-K of the GEMMs with small tile grids
+  int stop_after = -1;     // diagnostic: a denoiser evaluation returns after this many kernel-class launches (-1 = never)
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)
 Tune tune_snapshot(int* epoch);                       // process defaults + their epoch
@@ -276,7 +277,9 @@ __device__ __forceinline__ float wave_sum64(float v) {
 }
 
 // Chan et al. parallel combine of (count, mean, M2) partials.
+// An empty partial (nb <= 0) contributes nothing, whatever its mean / M2 words hold.
 __device__ __forceinline__ void chan_combine(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  if (nb <= 0.f) return;
   float nn = n + nb;
   if (nn <= 0.f) return;
   float d = meanb - mean;

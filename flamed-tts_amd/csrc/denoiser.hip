@@ -11,6 +11,7 @@
 //                 gather prologue and the Euler update xt += dt*v fused in the epilogue.
 // AdaLN (depends only on t and the speaker) is precomputed for every (step, utterance) at once.
 #include "flamed_hip.h"
+#include "flamed_diag.h"
 #include "gemm.hpp"
 #include "gemm_dma.hpp"
 #include "gemm_8p.hpp"
@@ -2027,6 +2028,21 @@ FLAMED_API size_t flamed_den_workspace_size(flamed_den_t h, int B, int T) {
   return den_solve_ws(d, B, T);
 }
 
+// Diagnostic (include/flamed_diag.h): byte offsets of the one-chain step workspace's buffers
+// X, S0, S1, D, U, GP, GNS, Y, SL, A16, XA, XP (den_ws_layout; SIZE_MAX for an absent buffer).
+FLAMED_API int flamed_den_ws_offsets(flamed_den_t h, int B, int T, size_t* off) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && off && B > 0 && T > 0, "flamed_den_ws_offsets: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  TuneScope ts(den_tune_sync(d));
+  char* const base = reinterpret_cast<char*>(4096);  // any non-null base: offsets are relative to it
+  DenWs w;
+  den_ws_layout(d, B, T, base, &w);
+  const void* p[12] = {w.X, w.S0, w.S1, w.D, w.U, w.GP, w.GNS, w.Y, w.SL, w.A16, w.XA, w.XP};
+  for (int i = 0; i < 12; ++i) off[i] = p[i] ? (size_t)((const char*)p[i] - base) : SIZE_MAX;
+  return kOk;
+}
+
 }  // extern "C"
 
 namespace fl {
@@ -2085,7 +2101,15 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   bf16* const As = reinterpret_cast<bf16*>(w.D);
   int rc;
 #define TRY(x) do { if ((rc = (x)) != kOk) return rc; } while (0)
-#define K_(cls, x) do { if (tu.stamp_class >= 0) stamp_select(cls, st); TRY(x); if (tu.dup_class == (cls)) TRY(x); } while (0)
+  int n_launched = 0;  // kernel-class launches so far (diagnostic stop_after)
+#define K_(cls, x)                                                  \
+  do {                                                              \
+    if (tu.stop_after >= 0 && n_launched >= tu.stop_after) return kOk; \
+    ++n_launched;                                                   \
+    if (tu.stamp_class >= 0) stamp_select(cls, st);                 \
+    TRY(x);                                                         \
+    if (tu.dup_class == (cls)) TRY(x);                              \
+  } while (0)
   // fused solve step (xsrc != null; small M only, den_fused_ok): the previous step's combine + Euler
   // update is proj_in's A loader, and there is no combine launch at the end of the step
   FL_REQUIRE(!xsrc || (!big && !vout), "den_step: fused Euler step needs the small-M path");
@@ -2432,6 +2456,16 @@ FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, f
   return kOk;
 }
 
+FLAMED_API int flamed_den_persist_status(flamed_den_t h, int* runs, int* fails) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && runs && fails, "flamed_den_persist_status: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  *runs = d->pruns;
+  *fails = d->pfail_host ? __atomic_load_n(d->pfail_host, __ATOMIC_RELAXED) : 0;
+  persist_poll_fails(d);
+  return kOk;
+}
+
 FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails) {
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && fails, "flamed_den_persist_fails: bad args");
@@ -2495,7 +2529,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
     mk = mods + (size_t)k * Bk * d->MS;
     wk = static_cast<char*>(ws) + k * wsk;
   };
-  if (!use_graph) {
+  if (!(use_graph & 1)) {
     for (int s = s0; s < s1; ++s)
       for (int k = 0; k < S; ++k) {
         float* xk; const float* mk; void* wk;
@@ -2512,7 +2546,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   // path (one persistent launch per part, or the graph of launches) is decided once, by the step-0 part
   if (s0 == 0) {
     d->part_epoch = d->tune_ver;
-    d->ppath = persist_eligible(d, B, T) ? 1 : 0;
+    d->ppath = !(use_graph & 2) && persist_eligible(d, B, T) ? 1 : 0;  // bit 2: the caller's retry, no persistent launch
     d->ppath_key[0] = B; d->ppath_key[1] = T; d->ppath_key[2] = nfe;
   }
   FL_REQUIRE(d->part_epoch == d->tune_ver, "flamed_den_solve_part: knobs changed since step 0 of this solve (part [%d, %d))",

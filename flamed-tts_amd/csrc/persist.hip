@@ -3,6 +3,7 @@
 #include <cstdlib>
 
 #include "flamed_hip.h"
+#include "flamed_diag.h"
 #include "persist.hpp"
 #include "gemm_dma.hpp"
 
@@ -130,14 +131,14 @@ __device__ __forceinline__ bool wait_ge(int* err, int* fails, long long tmo, int
   return ok;
 }
 
-// The reset prologue's grid-wide arrival: wave 0 polls a monotonic counter until it reaches `target` (no
-// error word yet: the counter block is being reset); a timeout leaves the launch (x NaN-poisoned).
-__device__ __forceinline__ bool arrive_wait(int* ctr, int target, long long tmo, int* flag) {
+// The reset prologue's grid-wide arrival: wave 0 polls a monotonic (wrapping) ticket counter until it has
+// reached `target` (no error word yet: the counter block is being reset); a timeout leaves the launch.
+__device__ __forceinline__ bool arrive_wait(unsigned* ctr, unsigned target, long long tmo, int* flag) {
   if (threadIdx.x < 64) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
     for (unsigned it = 0;; ++it) {
-      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      if (arrive_reached(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), target)) break;
       if ((it & 31) == 31 && (long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
         ok = false;
         break;
@@ -646,23 +647,40 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   // reset: the first says every workgroup of this launch has started (so the previous launch, stream-
   // ordered before it, is done with the block), the second that every share has been zeroed.
   {
-    int* tk = reinterpret_cast<int*>(smem + L_FLAG);
-    if (tid == 0) tk[1] = __hip_atomic_fetch_add(P.sticky + SY_ARRIVE0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / kWGs;
+    unsigned* const a0 = reinterpret_cast<unsigned*>(P.sticky + SY_ARRIVE0);
+    unsigned* const a1 = reinterpret_cast<unsigned*>(P.sticky + SY_ARRIVE1);
+    unsigned* tk = reinterpret_cast<unsigned*>(smem + L_FLAG);
+    if (tid == 0) tk[1] = __hip_atomic_fetch_add(a0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    const int launch = tk[1];
+    const unsigned target = arrive_target(tk[1]);
     __syncthreads();
-    if (!arrive_wait(P.sticky + SY_ARRIVE0, (launch + 1) * kWGs, tmo, flag)) { fail_exit(); return; }
-    if (tid < 4 && kCtrInts > 4 * (int)blockIdx.x + tid)
-      __hip_atomic_store(P.ctr + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid < 4) __hip_atomic_store(P.seal + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (gran && tid < 32) {  // 512 B of the 128 KB granule block per workgroup
-      const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
-      st16(rq, (unsigned)((blockIdx.x * 32 + tid) * 16), u32x4{0u, 0u, 0u, 0u});
+    const bool ok0 = arrive_wait(a0, target, tmo, flag);
+    if (ok0) {
+      if (tid < 4 && kCtrInts > 4 * (int)blockIdx.x + tid)
+        __hip_atomic_store(P.ctr + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid < 4) __hip_atomic_store(P.seal + 4 * blockIdx.x + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (gran && tid < 32) {  // 512 B of the 128 KB granule block per workgroup
+        const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
+        st16(rq, (unsigned)((blockIdx.x * 32 + tid) * 16), u32x4{0u, 0u, 0u, 0u});
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(P.sticky + SY_ARRIVE1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!arrive_wait(P.sticky + SY_ARRIVE1, (launch + 1) * kWGs, tmo, flag)) { fail_exit(); return; }
+    // every workgroup adds to the second counter exactly once, also after a failed first wait, so both counters
+    // stay kWGs per launch and in phase for every later launch
+    if (tid == 0) __hip_atomic_fetch_add(a1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool ok1 = arrive_wait(a1, target, tmo, flag);
+    if (!ok0 || !ok1) {
+      // counted once per launch in the sticky failure word (the error word sits in the block being reset):
+      // the first workgroup to record this launch's target in SY_PFAIL adds the failure
+      if (tid == 0) {
+        unsigned* pf = reinterpret_cast<unsigned*>(P.sticky + SY_PFAIL);
+        if (__hip_atomic_exchange(pf, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != target)
+          __hip_atomic_fetch_add(fails, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      fail_exit();
+      return;
+    }
   }
   publish_xs();
 
@@ -905,7 +923,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
         for (int k = 0; k < kGroups; ++k) {
           const float4 v = as_f4(ld16(rq, (unsigned)((k * H + col0 + tid) * 16)));
-          chan_combine(n, mean, m2, k / gpu == utt ? v.x : 0.f, v.y, v.z);  // this utterance's groups only
+          // this utterance's groups only: another utterance's (count, mean, M2) all masked (a zero count
+          // alone would still add its M2 in chan_combine)
+          const bool mine = k / gpu == utt;
+          chan_combine(n, mean, m2, mine ? v.x : 0.f, mine ? v.y : 0.f, mine ? v.z : 0.f);
         }
         const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
         gnv[tid] = make_float4(mean, sc, gbv, 0.f);
@@ -1216,3 +1237,11 @@ int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
 #ifdef FL_STAMPS
 extern "C" FLAMED_API int flamed_persist_stamps(void* buf, int step) { return fl::pk::persist_stamps(buf, step); }
 #endif
+
+// Host-side check of the reset prologue's ticket arithmetic (include/flamed_diag.h; CPU unit test).
+extern "C" FLAMED_API int flamed_persist_ticket(unsigned ticket, unsigned cur, unsigned* target, int* reached) {
+  if (!target || !reached) return fl::kBadArg;
+  *target = fl::pk::arrive_target(ticket);
+  *reached = fl::pk::arrive_reached(cur, *target) ? 1 : 0;
+  return fl::kOk;
+}

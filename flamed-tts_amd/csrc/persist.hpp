@@ -55,7 +55,16 @@ static_assert(kLds <= 160 * 1024, "persistent solve LDS");
 constexpr int CT_GRP = 0, CT_GN = 16 * kGroups, CT_ERR = CT_GN + 16 * kSlots, kCtrInts = CT_ERR + 16;
 // sticky words (never reset; zeroed once at allocation): failed launches, and the two monotonic arrival
 // counters of the reset prologue, each on a 128-B line of its own
-constexpr int SY_FAILS = 0, SY_ARRIVE0 = 32, SY_ARRIVE1 = 64, kStickyInts = 96;
+constexpr int SY_FAILS = 0, SY_ARRIVE0 = 32, SY_ARRIVE1 = 64, SY_PFAIL = 96, kStickyInts = 128;
+
+// Reset-prologue arrival tickets, wrap-safe: every launch adds exactly kWGs to each arrival counter (unsigned),
+// and 2^32 is a multiple of kWGs, so the launch a ticket belongs to starts at ticket - ticket % kWGs on either
+// side of the 32-bit wrap; its arrivals are complete once the counter has moved kWGs past that base, compared
+// by signed difference.  (Host-callable for the CPU unit test: flamed_persist_ticket.)
+__host__ __device__ inline unsigned arrive_target(unsigned ticket) {
+  return ticket - ticket % (unsigned)kWGs + (unsigned)kWGs;
+}
+__host__ __device__ inline bool arrive_reached(unsigned cur, unsigned target) { return (int)(cur - target) >= 0; }
 
 struct BlockW {
   const bf16 *w2, *w3, *m0, *m2;
@@ -90,6 +99,7 @@ struct Params {
   int* seal;               // persist_opt 16384: per (group, slot) the number of its last group hand-off (16 B each)
   int* sticky;             // kStickyInts words never reset between launches: [SY_FAILS] failed launches so far
                            // (the host reads it after the fact), [SY_ARRIVE0/1] the reset prologue's arrivals
+                           // (unsigned tickets), [SY_PFAIL] the last launch whose prologue failed (counted once)
   int inject_step = -1;    // diagnostic (flamed_tune persist_inject): every workgroup fails at this step
   long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
   int opt = 0;                        // experiment bits (flamed_tune persist_opt)

@@ -38,8 +38,8 @@ SIGNATURES = {
     "flamed_den_solve": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_den_solve_chunk": (c_int, [P, c_int]),
     "flamed_den_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_float)]),
-    "flamed_den_persist_fails": (c_int, [P, ctypes.POINTER(c_int)]),
     "flamed_den_persist_times": (c_int, [P, ctypes.POINTER(c_float), c_int]),
+    "flamed_den_persist_status": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "flamed_den_solve_part": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, c_int, c_int, P]),
     "flamed_den_time_kernels_graph": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),
@@ -102,6 +102,13 @@ DIAG_SIGNATURES = {
     "flamed_persist_stamps": (c_int, [P, c_int]),
     "flamed_pva_stamps": (c_int, [P, c_int]),
 }
+# include/flamed_diag.h, "libflamed_hip.so diagnostics" section: exported by the product library, used by
+# tools and tests only
+HIP_DIAG_SIGNATURES = {
+    "flamed_den_persist_fails": (c_int, [P, ctypes.POINTER(c_int)]),
+    "flamed_den_ws_offsets": (c_int, [P, c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "flamed_persist_ticket": (c_int, [ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(c_int)]),
+}
 
 FLAMED_F32, FLAMED_BF16, FLAMED_FP8 = 0, 1, 2
 DTYPES = {"f32": FLAMED_F32, "fp32": FLAMED_F32, "float32": FLAMED_F32, "bf16": FLAMED_BF16, "bfloat16": FLAMED_BF16,
@@ -160,7 +167,7 @@ def lib():
                 raise RuntimeError(
                     f"Flamed HIP extension not found at {LIB_PATH}. Build it with "
                     "`make -C flamed-tts_amd/csrc` (or `python -c 'import __graft_entry__ as g; g.build()'`).")
-            _lib = _bind(ctypes.CDLL(LIB_PATH), {**DIAG_SIGNATURES, **SIGNATURES})
+            _lib = _bind(ctypes.CDLL(LIB_PATH), {**DIAG_SIGNATURES, **HIP_DIAG_SIGNATURES, **SIGNATURES})
     return _lib
 
 

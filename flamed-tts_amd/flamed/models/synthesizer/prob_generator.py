@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import warnings
 from typing import List, Optional
 
 import torch
@@ -374,6 +375,12 @@ class DenoiserHIP:
         self.ws = nat.Workspace()
         self.ada_ws = nat.Workspace()
         self._solve_bufs = {}
+        # after a solve that ran as a persistent launch (B = 1 .. 8, bf16), wait for it and re-run it on the
+        # graph of launches if the kernel reported a failure (NaN-poisoned x), so a failed launch never
+        # reaches the caller as a result; skipped inside a stream capture (the caller then owns the check:
+        # persist_status)
+        self.check_persist = True
+        self._fails_seen = 0
         self.oid = ops.register(self)  # torch.ops.flamed_hip.den_* carry this id
 
     def __del__(self):
@@ -510,10 +517,33 @@ class DenoiserHIP:
         # chunk runs was measured slower: 34.8 -> 36.6 ms at B = 1, 352 -> 358 ms at B = 64)
         self.adaln(ts[:nfe], spk, bufs["tidx"], bufs["sidx"], out=bufs["mods"])
         bufs["x"].copy_(xt)
+        use_graph = int(bool(self.den.hip_graph))
+        runs0, _ = self.persist_status()
         nat.check(L.flamed_den_solve(self.handle, nat.ptr(bufs["x"]), nat.ptr(bufs["mods"]), nfe, B, T, nat.ptr(ws),
-                                     ws.numel(), int(bool(self.den.hip_graph)), nat.stream_ptr(dev)),
+                                     ws.numel(), use_graph, nat.stream_ptr(dev)),
                   "flamed_den_solve")
+        if self.check_persist and not torch.cuda.is_current_stream_capturing():
+            runs1, _ = self.persist_status()
+            if runs1 > runs0:  # this solve ran as a persistent launch: make sure it did not fail
+                torch.cuda.current_stream(dev).synchronize()  # also completes the failure count's copy
+                _, fails = self.persist_status()
+                if fails > self._fails_seen:
+                    self._fails_seen = fails
+                    warnings.warn(f"flamed: persistent solve failed ({fails} so far on this handle); "
+                                  "re-running it on the graph of launches")
+                    bufs["x"].copy_(xt)
+                    nat.check(L.flamed_den_solve(self.handle, nat.ptr(bufs["x"]), nat.ptr(bufs["mods"]), nfe, B, T,
+                                                 nat.ptr(ws), ws.numel(), use_graph | 2, nat.stream_ptr(dev)),
+                              "flamed_den_solve (re-run)")
         return bufs["x"].clone()
+
+    def persist_status(self):
+        """(persistent launches enqueued, failed launches as of the last completed copy) of this handle; never
+        waits (flamed_den_persist_status)."""
+        runs, fails = ctypes.c_int(0), ctypes.c_int(0)
+        nat.check(nat.lib().flamed_den_persist_status(self.handle, ctypes.byref(runs), ctypes.byref(fails)),
+                  "flamed_den_persist_status")
+        return runs.value, fails.value
 
 
 def cond_weight_list(pg: "ProbGenerator") -> List[torch.Tensor]:

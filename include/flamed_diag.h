@@ -2,7 +2,7 @@
  *
  * flamed_probe_* live in libflamed_diag.so (csrc/probe.hip, `make -C flamed-tts_amd/csrc diag`);
  * flamed_stamp_buffer lives only in libflamed_hip_stamps.so (`make stamps`: the product sources built
- * with -DFL_STAMPS).  Nothing on the product path loads either library (tools/*.py only).
+ * with -DFL_STAMPS).  Nothing on the product path loads either library (scripts under tools/ only).
  */
 #ifndef FLAMED_DIAG_H
 #define FLAMED_DIAG_H
@@ -52,6 +52,19 @@ FLAMED_API int flamed_persist_stamps(void* buf, int step);
 /* Persistent PVA flow timeline (libflamed_hip_stamps.so only): thread 0 of every workgroup writes
  * s_memrealtime at fixed points of Euler step `step` into buf[wg * 16 + k]; tools/pva_timeline.py. */
 FLAMED_API int flamed_pva_stamps(void* buf, int step);
+
+/* ---- libflamed_hip.so diagnostics ----
+ * Exported by the product library for tools and tests; not part of the product contract (flamed_hip.h), and
+ * nothing on the product call path uses them. */
+/* Failed persistent launches so far on this handle (waits for the whole device to be idle). */
+FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails);
+/* Byte offsets inside the flamed_den_velocity / flamed_den_step workspace of its buffers X, S0, S1, D, U, GP, GNS,
+ * Y, SL, A16, XA, XP (off[12]; SIZE_MAX = absent at this B, T) under the handle's current knobs. */
+FLAMED_API int flamed_den_ws_offsets(flamed_den_t h, int B, int T, size_t* off);
+/* The persistent solve's reset-prologue ticket arithmetic, host-side (no GPU): the arrival count `*target` that
+ * completes the launch of `ticket` (a fetch_add result), and whether counter value `cur` has reached it
+ * (wrap-safe across 2^32). */
+FLAMED_API int flamed_persist_ticket(unsigned ticket, unsigned cur, unsigned* target, int* reached);
 
 #ifdef __cplusplus
 }

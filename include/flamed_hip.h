@@ -95,8 +95,9 @@ FLAMED_API int flamed_den_step(flamed_den_t h, float* xt, const float* mods, int
 
 /* The whole nfe-step Euler solve in place on xt ((B*T) x latent_dim).  mods holds nfe*B rows in
  * step-major order (row s*B + b = step s, utterance b; produced by flamed_den_adaln).
- * use_graph != 0 captures the nfe steps once into a hipGraph (cached per shape/pointers) and
- * replays it. */
+ * use_graph bit 1 captures the nfe steps once into a hipGraph (cached per shape/pointers) and
+ * replays it (0: plain launches); bit 2 never takes the persistent solve below (a caller's re-run of a
+ * solve whose persistent launch reported a failure). */
 FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                 size_t ws_bytes, int use_graph, hipStream_t stream);
 /* Steps per captured solve graph for nfe steps (the granularity of flamed_den_solve_part); -1 on error. */
@@ -119,8 +120,11 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
  * it has given up the persistent path, *last_ms = device time of the last uncaptured launch (HIP events
  * around the kernel on the launch stream; waits for it). */
 FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, float* last_ms);
-/* (diagnostic) failed persistent launches so far on this handle (waits for the device to be idle). */
-FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails);
+/* Never waits: *runs = persistent launches enqueued on this handle, *fails = its failed launches as of the
+ * last completed asynchronous copy of the device's failure count (exact once the stream of the last launch has
+ * been synchronised: the copy is ordered behind the launch).  The Python wrapper checks it after each
+ * persistent solve and re-runs a failed one with use_graph bit 2. */
+FLAMED_API int flamed_den_persist_status(flamed_den_t h, int* runs, int* fails);
 /* Device times (ms, oldest first) of the up to n most recent uncaptured persistent launches (a ring of 64
  * HIP event pairs; waits for them); returns how many were written, -1 on error. */
 FLAMED_API int flamed_den_persist_times(flamed_den_t h, float* ms, int n);

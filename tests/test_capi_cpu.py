@@ -87,13 +87,21 @@ DIAG_HDR = os.path.join(os.path.dirname(PKG), "include", "flamed_diag.h")
 
 
 def test_diag_header_bound_and_separate(lib):
-    """Diagnostic probes live in libflamed_diag.so (include/flamed_diag.h), not in the product library."""
+    """Diagnostic probes live in libflamed_diag.so (include/flamed_diag.h, first section), not in the product
+    library; the header's "libflamed_hip.so diagnostics" section is exported by the product library, bound in
+    HIP_DIAG_SIGNATURES, and kept out of the product contract (flamed_hip.h)."""
     from flamed import _native
-    names = re.findall(r"FLAMED_API\s+[\w\s\*]+?\b(flamed_\w+)\s*\(", open(DIAG_HDR).read())
+    src = open(DIAG_HDR).read()
+    probe_src, hip_src = src.split("---- libflamed_hip.so diagnostics ----")
+    pat = r"FLAMED_API\s+[\w\s\*]+?\b(flamed_\w+)\s*\("
+    names, hip_names = re.findall(pat, probe_src), re.findall(pat, hip_src)
     assert set(names) | {"flamed_last_error"} == set(_native.DIAG_SIGNATURES)
-    assert not set(names) & set(declared())
+    assert set(hip_names) == set(_native.HIP_DIAG_SIGNATURES)
+    assert not (set(names) | set(hip_names)) & set(declared())
     for n in names:
         assert not hasattr(lib, n), f"{n} must not be exported by the product library"
+    for n in hip_names:
+        assert hasattr(lib, n), f"{n} must be exported by the product library"
     dl = _native.diag_lib()
     for n in names:
         if n not in ("flamed_stamp_buffer", "flamed_persist_stamps", "flamed_pva_stamps"):  # FL_STAMPS build only
@@ -157,3 +165,24 @@ def test_tracked_handles_released_once(lib):
         _native.destroy(h2, "flamed_dur_destroy")  # after the hook: no-op
     finally:
         _native._live.update(saved)
+
+
+def test_persist_ticket_arithmetic_wraps(lib):
+    """The persistent solve's reset-prologue tickets (persist.hpp arrive_target / arrive_reached): every launch
+    adds 256 to each arrival counter, and the launch base and the reached test stay right across INT_MAX and
+    the 32-bit wrap (a signed ticket divided by 256 broke after ~8.4M launches)."""
+    tgt, ok = ctypes.c_uint(), ctypes.c_int()
+
+    def q(ticket, cur):
+        assert lib.flamed_persist_ticket(ticket % 2**32, cur % 2**32, ctypes.byref(tgt), ctypes.byref(ok)) == 0
+        return tgt.value, bool(ok.value)
+
+    for base in (0, 256 * 1000, 2**31 - 256, 2**31, 2**32 - 512, 2**32 - 256):
+        for k in (0, 1, 128, 255):  # every workgroup of one launch computes the same target
+            t, _ = q(base + k, 0)
+            assert t == (base + 256) % 2**32
+        assert q(base + 7, base + 255)[1] is False   # 255 of 256 arrived
+        assert q(base + 7, base + 256)[1] is True    # all arrived (also when base + 256 wraps to 0)
+        assert q(base + 7, base + 300)[1] is True    # the next launch has begun arriving
+    # INT_MAX crossing: a launch whose tickets straddle 2^31 still agrees on one target
+    assert q(2**31 - 1, 0)[0] == 2**31 and q(2**31 - 256, 0)[0] == 2**31
