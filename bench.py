@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--dtype", default=None, choices=["bf16", "f32", "fp8"], help="denoiser handle dtype (fp8: MX-fp8 pointwise GEMMs at large M)")
     ap.add_argument("--no-configs3", action="store_true",
                     help="N > 1: skip the extra configs[3] leg (64 utterances per GPU on every rank)")
+    ap.add_argument("--dist-single", action="store_true",
+                    help="one rank: still run the multi-rank branch (an NCCL/RCCL process group of one, device-tensor "
+                         "max-over-ranks timing, efficiency fields, the configs[3] leg); implied by --config 3")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -558,8 +561,9 @@ def launch_ranks(args) -> int:
 def scaling_stats(dist, world, rank, frames_per_rank, sec, solo_sec, dev=None):
     """Max-over-ranks step time (the contract's clock), every rank's own frames/s, and the efficiency of the
     whole job against N x the same per-GPU workload timed on rank 0 alone in the same process tree (the
-    other ranks idle at a barrier meanwhile).  One rank: (sec, [frames/s], None)."""
-    if world == 1:
+    other ranks idle at a barrier meanwhile).  No process group: (sec, [frames/s], None); a group of one rank
+    (--dist-single) takes the collective path below with world = 1."""
+    if dist is None:
         return sec, [round(frames_per_rank / sec, 3)], None
     import torch.distributed  # noqa: F401
     tt = torch.tensor([sec], dtype=torch.float64, device=dev)
@@ -655,10 +659,21 @@ def main():
     if args.plumbing:
         return plumbing(args, rank, world)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist_single or args.config == 3:
+        # one process per GPU over RCCL ("nccl" on ROCm); with one rank (--dist-single / --config 3) the same
+        # branch runs as a group of one, so its device-tensor collectives have run before a multi-GPU job needs them
         import torch.distributed as dist  # noqa: F811
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if world == 1:
+            import socket
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            dist.init_process_group("nccl", rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 

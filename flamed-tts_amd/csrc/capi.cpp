@@ -91,11 +91,14 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
       {"persist_multi", &Tune::persist_multi, 0, 1, nullptr},
+      {"persist_ntw", &Tune::persist_ntw, 1, 5, nullptr},
       {"persist_capmode", &Tune::persist_capmode, 0, 1, nullptr},
       {"pva_persist", &Tune::pva_persist, 0, 1, nullptr},
       {"attn_mfma", &Tune::attn_mfma, 0, 1, nullptr},
       {"prior_split", &Tune::prior_split, 0, 1, nullptr},
       {"stop_after", &Tune::stop_after, -1, 1 << 20, nullptr},
+      {"dwgn_var", &Tune::dwgn_var, 0, 2, nullptr},
+      {"pva_inject", &Tune::pva_inject, -1, 1 << 20, nullptr},
   };
   for (const Knob& k : knobs) {
     if (std::strcmp(k.name, key) != 0) continue;

@@ -177,6 +177,7 @@ struct Tune {
   int split_min_rows = 6144;  // ... when every chain still has this many rows
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
+  int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
   int persist_opt = 585;   // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
@@ -186,6 +187,8 @@ struct Tune {
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)
   int attn_mfma = 1;       // transformer attention (prior stack, timbre encoder) on fp32 MFMA (xfmr.hpp)
   int prior_split = 1;     // bf16 prior decoders: split-K of the GEMMs with small tile grids
+  int pva_inject = -1;     // diagnostic: every persistent PVA flow fails at this step (-1 = never)
+  int dwgn_var = 0;        // diagnostic: dwgn kernel variant (1 scalar fp32 math, 2 scalar LDS accesses; T in (384, 448])
   int stop_after = -1;     // diagnostic: a denoiser evaluation returns after this many kernel-class launches (-1 = never)
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)

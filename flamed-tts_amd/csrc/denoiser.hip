@@ -740,7 +740,31 @@ static int launch_dwconv_stats(const XT* X, int H, const float* S, int NT, int t
 // chunks are in flight while the current one is convolved.
 constexpr int kDgMaxT = 512;  // frames covered by the register-resident path (NCH <= 8)
 typedef float dg_f2 __attribute__((ext_vector_type(2)));
-template <bool AFF, int NCH, typename XT>
+// Diagnostic variants (tune dwgn_var, T in (384, 448] only): VAR 1 computes the staging and the conv with scalar
+// fp32 FMAs (no v_pk_*), VAR 2 moves the staged window through LDS with scalar (volatile) accesses.
+template <int VAR>
+__device__ __forceinline__ dg_f2 dg_fma(dg_f2 a, dg_f2 b, dg_f2 c) {
+  if constexpr (VAR == 1) {
+    float x = __builtin_fmaf(a.x, b.x, c.x), y = __builtin_fmaf(a.y, b.y, c.y);
+    asm volatile("" : "+v"(x), "+v"(y));  // keep them scalar (no re-pairing into v_pk_fma_f32)
+    return dg_f2{x, y};
+  } else {
+    return __builtin_elementwise_fma(a, b, c);
+  }
+}
+template <int VAR>
+__device__ __forceinline__ dg_f2 dg_lnmod(dg_f2 x, dg_f2 mean, dg_f2 rstd, dg_f2 a, dg_f2 b) {
+  if constexpr (VAR == 1) {
+    float u = (x.x - mean.x) * rstd.x, v = (x.y - mean.y) * rstd.y;
+    asm volatile("" : "+v"(u), "+v"(v));
+    float o0 = u * a.x + b.x, o1 = v * a.y + b.y;
+    asm volatile("" : "+v"(o0), "+v"(o1));
+    return dg_f2{o0, o1};
+  } else {
+    return ((x - mean) * rstd) * a + b;
+  }
+}
+template <bool AFF, int NCH, typename XT, int VAR = 0>
 __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int H, const float* __restrict__ S, int NT, int tw,
                                                    float eps_ln, ModRef mod, const float* __restrict__ lnw,
                                                    const float* __restrict__ lnb, const float* __restrict__ dww,
@@ -817,10 +841,15 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
         if (t >= 0 && t < T) {
           const dg_f2 mean = rs[2 * t], rstd = rs[2 * t + 1];
           const float4 a4 = *reinterpret_cast<const float4*>(va + 4 * c4), b4 = *reinterpret_cast<const float4*>(vb + 4 * c4);
-          lo = ((dg_f2{xcj.x, xcj.y} - mean) * rstd) * dg_f2{a4.x, a4.y} + dg_f2{b4.x, b4.y};
-          hi = ((dg_f2{xcj.z, xcj.w} - mean) * rstd) * dg_f2{a4.z, a4.w} + dg_f2{b4.z, b4.w};
+          lo = dg_lnmod<VAR>(dg_f2{xcj.x, xcj.y}, mean, rstd, dg_f2{a4.x, a4.y}, dg_f2{b4.x, b4.y});
+          hi = dg_lnmod<VAR>(dg_f2{xcj.z, xcj.w}, mean, rstd, dg_f2{a4.z, a4.w}, dg_f2{b4.z, b4.w});
         }
-        *reinterpret_cast<float4*>(h + r * LDH + 4 * c4) = make_float4(lo.x, lo.y, hi.x, hi.y);
+        if constexpr (VAR == 2) {
+          volatile float* hv = h + r * LDH + 4 * c4;
+          hv[0] = lo.x; hv[1] = lo.y; hv[2] = hi.x; hv[3] = hi.y;
+        } else {
+          *reinterpret_cast<float4*>(h + r * LDH + 4 * c4) = make_float4(lo.x, lo.y, hi.x, hi.y);
+        }
       }
     }
     // two chunks ahead, in flight during the next two convs; issued unconditionally (past the end: the
@@ -834,10 +863,16 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
     for (int q = 0; q < RPT; ++q) acc[q] = bias;
 #pragma unroll
     for (int r = 0; r < WIN; ++r) {
-      const dg_f2 row = *reinterpret_cast<const dg_f2*>(h + (rg * RPT + r) * LDH + 2 * pp);
+      dg_f2 row;
+      if constexpr (VAR == 2) {
+        volatile const float* hv = h + (rg * RPT + r) * LDH + 2 * pp;
+        row = dg_f2{hv[0], hv[1]};
+      } else {
+        row = *reinterpret_cast<const dg_f2*>(h + (rg * RPT + r) * LDH + 2 * pp);
+      }
 #pragma unroll
       for (int q = 0; q < RPT; ++q)
-        if (r - q >= 0 && r - q < KS) acc[q] = __builtin_elementwise_fma(w[r - q], row, acc[q]);
+        if (r - q >= 0 && r - q < KS) acc[q] = dg_fma<VAR>(w[r - q], row, acc[q]);
     }
     const int nv = T - (t0 + rg * RPT);  // valid frames of this thread in the chunk (may be <= 0)
 #pragma unroll
@@ -901,12 +936,16 @@ static int launch_dwgn(const XT* X, int H, const float* S, int NT, int tw, ModRe
   const int nch = (T + 63) / 64;
   const dim3 g(H / 32, B), blk(256);
 #define FL_DWGN(N) hipLaunchKernelGGL((dwgn_kernel<AFF, N, XT>), g, blk, 0, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, A, T)
-  if (nch <= 2) FL_DWGN(2);
+#define FL_DWGN_V(N, V) hipLaunchKernelGGL((dwgn_kernel<AFF, N, XT, V>), g, blk, 0, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, A, T)
+  if (tn().dwgn_var == 1 && nch == 7) FL_DWGN_V(7, 1);
+  else if (tn().dwgn_var == 2 && nch == 7) FL_DWGN_V(7, 2);
+  else if (nch <= 2) FL_DWGN(2);
   else if (nch <= 4) FL_DWGN(4);
   else if (nch <= 6) FL_DWGN(6);
   else if (nch == 7) FL_DWGN(7);
   else FL_DWGN(8);
 #undef FL_DWGN
+#undef FL_DWGN_V
   FL_LAUNCH_CHECK();
   return kOk;
 }
@@ -1265,13 +1304,14 @@ struct LoadEulerIn {
   }
 };
 
-// Fused solve start: src image x_0 and a conv_out output whose combine is exactly 0 (see LoadEulerIn).
+// Fused solve start: src image x_0 (xs; null on the large-M path, whose update is in place) and a conv_out
+// output whose combine is exactly 0 (see LoadEulerIn).
 __global__ void euler_init_kernel(const float* __restrict__ xt, const float* __restrict__ bias, float* __restrict__ xs,
                                   float* __restrict__ Y, int M, int C) {
   size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (size_t)M * C) return;
   int m = idx / C, n = idx - (size_t)m * C;
-  xs[idx] = xt[idx];
+  if (xs) xs[idx] = xt[idx];
   float* y = Y + (size_t)m * 3 * C;
   y[n] = 0.f;
   y[C + n] = -bias[n];
@@ -1332,6 +1372,44 @@ __global__ void stack_taps_kernel(const float* __restrict__ src, DT* __restrict_
 // 80.1/91.2/116.0 ms per solve; B=3 even); tn().big_ns: LDS ring depth of the 128 x 128 tiles (2: two
 // workgroups per CU, 635 TF plain at M = 25600; 3: one, 418 TF).
 thread_local bf16* g_a16 = nullptr;  // the calling thread's step workspace (set per step, A16Scope)
+
+// Large-M fused Euler step (tune fuse_euler): the previous step's conv_out tap combine + Euler update, in place
+// (each thread reads and writes only its own 8 state values), and the bf16 cast of the new state that proj_in
+// reads (A16) -- conv3_combine_kernel's arithmetic in its order, then cast_bf16x8_kernel's, so the solve is
+// bitwise the unfused one -- in ONE streaming pass instead of a combine launch at the end of the step and a
+// cast launch at its start.  Thread 0 advances the step counter (nothing here or in proj_in reads it).
+__global__ void euler_cast_kernel(float* xt, const float* __restrict__ Y, const float* __restrict__ bias,
+                                  bf16* __restrict__ a16, int M, int T, int C, float dt, int* step_ctr) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (step_ctr && i == 0) *step_ctr += 1;
+  const int C8 = C / 8;
+  if (i >= (size_t)M * C8) return;
+  const int m = i / C8, k = (int)(i - (size_t)m * C8) * 8, t = m % T;
+  const size_t ld = 3 * (size_t)C;
+  float x[8], o[8];
+  {
+    const float4 a = ld4(xt + (size_t)m * C + k), b = ld4(xt + (size_t)m * C + k + 4);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  }
+#pragma unroll
+  for (int h = 0; h < 8; h += 4) {
+    const float4 bb = ld4(bias + k + h), y1 = ld4(Y + (size_t)m * ld + C + k + h);
+    const float4 y0 = t > 0 ? ld4(Y + (size_t)(m - 1) * ld + k + h) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 y2 = t < T - 1 ? ld4(Y + (size_t)(m + 1) * ld + 2 * C + k + h) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, v1[4] = {y1.x, y1.y, y1.z, y1.w};
+    const float v0[4] = {y0.x, y0.y, y0.z, y0.w}, v2[4] = {y2.x, y2.y, y2.z, y2.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = bv[e] + v1[e];
+      if (t > 0) v += v0[e];
+      if (t < T - 1) v += v2[e];
+      o[h + e] = __fadd_rn(x[h + e], __fmul_rn(dt, v));
+    }
+  }
+  *reinterpret_cast<float4*>(xt + (size_t)m * C + k) = make_float4(o[0], o[1], o[2], o[3]);
+  *reinterpret_cast<float4*>(xt + (size_t)m * C + k + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  *reinterpret_cast<u32x4*>(a16 + (size_t)m * C + k) = pack_chunk<bf16>(o);
+}
 
 __global__ void cast_bf16x8_kernel(const float* __restrict__ src, int ld, bf16* __restrict__ dst, int M, int K) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2047,6 +2125,20 @@ FLAMED_API int flamed_den_ws_offsets(flamed_den_t h, int B, int T, size_t* off) 
 
 namespace fl {
 
+// Large-M fused Euler step: euler_cast_kernel (x_{s-1} -> x_s in place, bf16 x_s into A16) + proj_in on A16.
+template <typename XT>
+static int big_euler_proj_in(Den* d, float* xt, const DenWs& w, XT* X, int* ctr, float dt, int M, int T, hipStream_t st) {
+  const int H = d->H, C = d->C;
+  FL_REQUIRE(w.A16 && C % 8 == 0, "den_step: large-M fused Euler step needs the A16 buffer");
+  const size_t n = (size_t)M * (C / 8);
+  hipLaunchKernelGGL(euler_cast_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, w.Y, d->bout, w.A16, M, T, C, dt, ctr);
+  FL_LAUNCH_CHECK();
+  const GemmCfg cfg = kCfgLarge;
+  const int NT = H / 128;
+  return den_gemm<bf16>(cfg, false, LoadPlain<bf16>{w.A16, C}, (const bf16*)d->win, C,
+                        EpiBiasStatsT<false, XT>{d->bin, X, H, w.S0, NT}, M, H, C, st);
+}
+
 // One velocity evaluation (+ Euler update when vout == nullptr).
 // `ctr` (optional): device step counter; when set the modulation rows are read at
 // mods + (*ctr) * B * MS and the last kernel increments it (graph replay of captured steps).
@@ -2112,8 +2204,11 @@ static int den_step_impl(Den* d, float* xt, const float* mods, int mod_div, int 
   } while (0)
   // fused solve step (xsrc != null; small M only, den_fused_ok): the previous step's combine + Euler
   // update is proj_in's A loader, and there is no combine launch at the end of the step
-  FL_REQUIRE(!xsrc || (!big && !vout), "den_step: fused Euler step needs the small-M path");
-  if (xsrc) {
+  FL_REQUIRE(!xsrc || !vout, "den_step: a fused Euler step has no velocity output");
+  FL_REQUIRE(!xsrc || !big || xsrc == xt, "den_step: the large-M fused Euler step updates the state in place");
+  if (xsrc && big) {  // large M: the previous step's combine + Euler update and proj_in's bf16 cast in one pass
+    if constexpr (std::is_same<DT, bf16>::value) K_(0, big_euler_proj_in<XT>(d, xt, w, X, ctr, dt, M, T, st));
+  } else if (xsrc) {
     const LoadEulerIn<DT> le{xsrc, xt, w.Y, d->bout, ctr, dt, T, C};
     const EpiBiasStatsT<false, XT> ep{d->bin, X, H, w.S0, NT};
     if (cfg == kCfgTiny) K_(0, (launch_gemm_cfg<32, 32, 3, DT>(le, (const DT*)d->win, C, ep, M, H, C, st)));
@@ -2240,12 +2335,19 @@ static int den_step(Den* d, float* xt, const float* mods, int mod_div, int B, in
 
 // The fused Euler step (LoadEulerIn) runs where proj_in takes the small-M register loop with one
 // workgroup column per tile column (no XCD strip remap) and no split-K of its fp32-A GEMM; the large-M
-// path keeps the combine kernel.
+// path fuses differently (den_fused_big).
 static bool den_fused_ok(const Den* d, int B, int T) {
   const Tune& tu = tn();
   const int M = B * T;
   const bool big = d->dt == FLAMED_BF16 && tu.big && M >= tu.big_min_rows;
   return tu.fuse_euler && !big && tu.xcd_strips == 0 && !d->f8;
+}
+// Large-M solves fuse the combine + Euler update into the next step's proj_in cast (euler_cast_kernel, in place:
+// no ping-pong); per sub-batch chain when the solve splits.  `B` is the rows' batch of one chain.
+static bool den_fused_big(const Den* d, int B, int T) {
+  const Tune& tu = tn();
+  return tu.fuse_euler && d->dt == FLAMED_BF16 && tu.big && (size_t)B * T >= (size_t)tu.big_min_rows &&
+         !(tu.bn32 && (size_t)B * T < (size_t)kTinyRows);
 }
 
 // Steps per captured graph: the largest divisor of nfe that is <= tn().graph_steps (default 16; the
@@ -2331,15 +2433,11 @@ static bool persist_eligible(Den* d, int B, int T) {
   persist_poll_fails(d);
   if (!tu.persist || d->pbroken || d->dt != FLAMED_BF16 || d->f8 || !d->fold || !tu.lnfold) return false;
   if (d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps || T < 16) return false;
-  if (B == 1) {
-    if (T > pk::kMaxT) return false;
-  } else {
-    // several utterances (knob persist_multi): B in {2, 4, 8}, each utterance's frames split over its 8 / B
-    // row groups of at most kMaxRows frames
-    if (!tu.persist_multi || (B != 2 && B != 4 && B != 8)) return false;
-    const int gpu = pk::kGroups / B;
-    if ((T + gpu - 1) / gpu > pk::kMaxRows) return false;
-  }
+  // one utterance, or (knob persist_multi) B in {2, 4, 8}, each utterance's frames split over its 8 / B row groups;
+  // a group holds up to kMaxNTW chunks of 64 frames (kernel variant by chunk count; knob persist_ntw caps it)
+  if (B != 1 && (!tu.persist_multi || (B != 2 && B != 4 && B != 8))) return false;
+  const int ntw = pk::persist_ntw(B, T, tu.persist_opt);
+  if (ntw > pk::kMaxNTW || ntw > tu.persist_ntw || ((tu.persist_opt & 1024) && ntw != 1)) return false;
   if (d->pdev_ok < 0) d->pdev_ok = pk::persist_device_ok(d->device) ? 1 : 0;
   return d->pdev_ok == 1;
 }
@@ -2372,6 +2470,7 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, i
   P.xt = xt;
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
   P.opt = tn().persist_opt;
+  P.ntw = pk::persist_ntw(B, T, P.opt);
   P.inject_step = tn().persist_inject;
   hipEvent_t* ev = nullptr;
   if (!cap) {
@@ -2565,6 +2664,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   // fused Euler steps: 25 launches per step instead of 26 (the combine rides in the next proj_in); the
   // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even
   const bool fused = S == 1 && den_fused_ok(d, B, T) && G % 2 == 0;
+  const bool fbig = !fused && den_fused_big(d, Bk, T);  // large M: in-place fused steps, per chain
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   // the graph bakes in dt = 1/nfe, so nfe is part of the key
@@ -2589,7 +2689,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
       hipStream_t cs = k == 0 ? d->cap_stream : d->cap_aux[k];
       for (int s = 0; s < G && rc == kOk; ++s) {
         if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, cs, d->ctr, s % 2 ? xt : w.XP);
-        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, nullptr, B, k, S);
+        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, fbig ? xk : nullptr, B, k, S);
       }
     }
     for (int k = 1; k < S && rc == kOk; ++k) {  // join
@@ -2611,6 +2711,17 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
       hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, w.XP, w.Y, B * T, d->C);
       FL_LAUNCH_CHECK();
       FL_HIP(hipMemsetAsync(d->ctr, 0xff, sizeof(int), st));
+    } else if (fbig) {  // every chain: Y whose combine is exactly 0, counter -1 (its euler_cast advances it)
+      for (int k = 0; k < S; ++k) {
+        float* xk; const float* mk; void* wk;
+        sub(k, xk, mk, wk);
+        DenWs wc;
+        den_ws_layout(d, Bk, T, wk, &wc);
+        const size_t nk = (size_t)Bk * T * d->C;
+        hipLaunchKernelGGL(euler_init_kernel, dim3((nk + 255) / 256), dim3(256), 0, st, xk, d->bout, (float*)nullptr, wc.Y, Bk * T, d->C);
+        FL_LAUNCH_CHECK();
+        FL_HIP(hipMemsetAsync(d->ctr + 16 * k, 0xff, sizeof(int), st));
+      }
     } else {
       FL_HIP(hipMemsetAsync(d->ctr, 0, 256, st));  // the step counters of every chain (16 ints apart)
     }
@@ -2621,6 +2732,18 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, nullptr, B * T, T,
                        d->C, dt, nullptr, w.XP);
     FL_LAUNCH_CHECK();
+  }
+  if (fbig && s1 == nfe) {  // every chain's last combine + Euler update, in place
+    for (int k = 0; k < S; ++k) {
+      float* xk; const float* mk; void* wk;
+      sub(k, xk, mk, wk);
+      DenWs wc;
+      den_ws_layout(d, Bk, T, wk, &wc);
+      const size_t nk = (size_t)Bk * T * d->C;
+      hipLaunchKernelGGL(conv3_combine_kernel, dim3((nk + 255) / 256), dim3(256), 0, st, wc.Y, d->bout, xk, nullptr, Bk * T, T,
+                         d->C, dt, nullptr, nullptr);
+      FL_LAUNCH_CHECK();
+    }
   }
   return kOk;
 }
@@ -2669,11 +2792,13 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
   const int saved_dup = guard.dup;  // the handle's active snapshot (this call's TuneScope)
   // the step structure the solve graph uses: fused Euler steps (no combine launches) where it fuses
   const bool fused = den_fused_ok(d, B, T);
+  const bool fbig = !fused && den_fused_big(d, B, T);
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
-  if (fused) {
+  if (fused || fbig) {
     const size_t n = (size_t)B * T * d->C;
-    hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, w.XP, w.Y, B * T, d->C);
+    hipLaunchKernelGGL(euler_init_kernel, dim3((n + 255) / 256), dim3(256), 0, st, xt, d->bout, fused ? w.XP : (float*)nullptr,
+                       w.Y, B * T, d->C);
     FL_LAUNCH_CHECK();
   }
   auto timed = [&](int dup, float* ms) -> int {
@@ -2682,7 +2807,7 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
     int rc = kOk;
     for (int i = 0; i < kSteps && rc == kOk; ++i) {
       if (fused) rc = den_step(d, i % 2 ? w.XP : xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream, nullptr, i % 2 ? xt : w.XP);
-      else rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream);
+      else rc = den_step(d, xt, mods, T, B, T, 0.f, nullptr, ws, d->cap_stream, nullptr, fbig ? xt : nullptr);
     }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(d->cap_stream, &g);

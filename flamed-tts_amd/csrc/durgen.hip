@@ -159,21 +159,28 @@ struct DurNet {
   char* split_mem = nullptr;
   static constexpr int kSplitTarget = 256, kSplitCounters = 1024;
   // persistent flow of the (duration, silence) pair (pvaflow.hpp), kept on the duration net's handle:
-  // scratch (counters first, hand-off buffers of both nets, a backup of the two states), pinned error word
+  // scratch (self-resetting counters, the sticky failure count, hand-off buffers of both nets; zeroed once at
+  // allocation), a pinned copy of the failure count (refreshed asynchronously behind every uncaptured launch),
+  // HIP events around the last uncaptured launch
+  static constexpr int kPersistRetry = 3;  // failed launches before the pair stays on the graph path
   char* pmem = nullptr;
-  int* perr_host = nullptr;
+  int* pfail_host = nullptr;
+  int pfails_seen = 0;
   hipEvent_t pev[2] = {nullptr, nullptr};
+  bool pev_set = false;
   int pdev_ok[pv::kMaxRG + 1] = {-1, -1, -1, -1, -1, -1};  // per row-group count: the grid is all resident
   bool pbroken = false;
   int pruns = 0;
-  float plast_ms = 0.f;
   void release_persist() {
+    if (pev_set) (void)hipEventSynchronize(pev[1]);  // the last uncaptured launch still owns pmem
     if (pmem) (void)hipFree(pmem);
-    if (perr_host) (void)hipHostFree(perr_host);
+    if (pfail_host) (void)hipHostFree(pfail_host);
     for (hipEvent_t& e : pev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     pmem = nullptr;
-    perr_host = nullptr;
+    pfail_host = nullptr;
+    pfails_seen = 0;
+    pev_set = false;
   }
 };
 
@@ -232,27 +239,27 @@ static int net_step(DurNet* n, const float* P, const float* temb, float* xt, con
 }
 
 // -------- persistent flow (pvaflow.hpp) --------
-static size_t pva_persist_layout(char* base, int F, pv::Params* P, float** backup) {
+static size_t pva_persist_layout(char* base, int F, pv::Params* P) {
   size_t off = 0;
   auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off = a256(off + bytes); return p; };
   const size_t M = pv::kMaxM, CS = (size_t)F / pv::kCols;
   char* ctr = take(4 * (size_t)pv::kCtrInts);
+  char* sticky = take(256);
   char* buf[2][3];
   for (int n = 0; n < 2; ++n) {
     buf[n][0] = take(M * F * 4);
     buf[n][1] = take(M * CS * 8);
     buf[n][2] = take(M * CS * 16);
   }
-  char* bk = take(2 * M * 4);
   if (P) {
     P->ctr = reinterpret_cast<int*>(ctr);
+    P->sticky = reinterpret_cast<int*>(sticky);
     for (int n = 0; n < 2; ++n) {
       P->net[n].R1 = reinterpret_cast<float*>(buf[n][0]);
       P->net[n].S1 = reinterpret_cast<float2*>(buf[n][1]);
       P->net[n].S2 = reinterpret_cast<float4*>(buf[n][2]);
     }
   }
-  if (backup) *backup = reinterpret_cast<float*>(bk);
   return off;
 }
 
@@ -264,27 +271,62 @@ static int pva_persist_groups(int M, int F) {
   return (RG > 0 && MT <= RG * pv::kMaxTiles) ? RG : 0;
 }
 
-static bool pva_persist_eligible(DurNet* nd, DurNet* ns, int M, hipStream_t st) {
+// Failed launches the kernel has counted since the pair's last look (the pinned copy lags at most one launch;
+// exact once the stream of the last launch has been synchronised).  Never waits.
+static void pva_poll_fails(DurNet* nd) {
+  if (!nd->pfail_host) return;
+  const int f = __atomic_load_n(nd->pfail_host, __ATOMIC_RELAXED);
+  if (f <= nd->pfails_seen) return;
+  nd->pfails_seen = f;
+  if (f >= DurNet::kPersistRetry && !nd->pbroken) {
+    nd->pbroken = true;
+    fprintf(stderr, "flamed: %d persistent PVA flows failed (states NaN-poisoned); this pair uses the graph path from now on\n", f);
+  } else {
+    fprintf(stderr, "flamed: a persistent PVA flow failed (%d of %d allowed); its states were NaN-poisoned\n", f,
+            DurNet::kPersistRetry);
+  }
+}
+
+// Whether a use_graph flow of M rows runs as the persistent launch.  Allowed inside a stream capture (nothing
+// on that path waits on the device).
+static bool pva_persist_eligible(DurNet* nd, DurNet* ns, int M) {
+  pva_poll_fails(nd);
   if (!tn().pva_persist || nd->pbroken || nd->D != 192 || nd->F != 384 || ns->D != 192 || ns->F != 384) return false;
   const int RG = pva_persist_groups(M, nd->F);
   if (RG == 0) return false;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
   if (nd->pdev_ok[RG] < 0) nd->pdev_ok[RG] = pv::pva_persist_device_ok(nd->device, 2 * (nd->F / pv::kCols) * RG) ? 1 : 0;
   return nd->pdev_ok[RG] == 1;
 }
 
-// Every step of both flows in one launch.  *done = false: not run (timed out and rolled back; the pair
-// then stays on the graph path) -- the caller runs the graph path.
+static bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
+
+// Every step of both flows as ONE cooperative launch, only enqueued (no host synchronisation): the kernel
+// resets its own counters; outside a capture HIP events around it and an async copy of the failure count follow
+// it.  A failed launch leaves NaN in both states and is reported by the next call / flamed_pva_persist_status.
+// *done = false: the runtime refused the cooperative grid (this row-group count never runs persistently on this
+// device); the caller runs the graph path.
 static int pva_persist_run(DurNet* nd, DurNet* ns, const PvaWs& w, const uint8_t* mask, float* dur_t, float* sil_t, int nfe,
                            int B, int L, float dt, hipStream_t st, bool* done) {
   *done = false;
-  const int M = B * L, D = nd->D;
-  if (!nd->pmem) FL_HIP(hipMalloc(&nd->pmem, pva_persist_layout(nullptr, nd->F, nullptr, nullptr)));
-  if (!nd->perr_host) FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&nd->perr_host), sizeof(int), hipHostMallocDefault));
+  const int M = B * L;
+  const bool cap = stream_capturing(st);
+  if (!nd->pmem) {
+    FL_REQUIRE(!cap, "persistent PVA flow: first use inside a stream capture (run it once uncaptured first)");
+    const size_t bytes = pva_persist_layout(nullptr, nd->F, nullptr);
+    FL_HIP(hipMalloc(&nd->pmem, bytes));
+    FL_HIP(hipMemsetAsync(nd->pmem, 0, bytes, st));
+  }
+  if (!nd->pfail_host) {
+    FL_REQUIRE(!cap, "persistent PVA flow: first use inside a stream capture (run it once uncaptured first)");
+    FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&nd->pfail_host), 16, hipHostMallocDefault));
+    *nd->pfail_host = 0;
+    nd->pfails_seen = 0;
+  }
   pv::Params P{};
-  float* backup = nullptr;
-  pva_persist_layout(nd->pmem, nd->F, &P, &backup);
+  pva_persist_layout(nd->pmem, nd->F, &P);
   P.M = M; P.L = L; P.MT = (M + 15) / 16; P.RG = pva_persist_groups(M, nd->F); P.nfe = nfe; P.dt = dt;
   P.mask = mask;
   const DurNet* nets[2] = {nd, ns};
@@ -297,29 +339,26 @@ static int pva_persist_run(DurNet* nd, DurNet* ns, const PvaWs& w, const uint8_t
     o.P = Pn[i]; o.w0 = n->w0; o.temb = Tn[i]; o.c1w = n->c1w; o.c1b = n->c1b; o.g1 = n->g1; o.b1 = n->b1;
     o.c2w = n->c2w; o.c2b = n->c2b; o.g2 = n->g2; o.b2 = n->b2; o.lw = n->lw; o.lb = n->lb; o.xt = xn[i];
   }
-  (void)D;
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
-  FL_HIP(hipMemcpyAsync(backup, dur_t, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
-  FL_HIP(hipMemcpyAsync(backup + pv::kMaxM, sil_t, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
-  FL_HIP(hipMemsetAsync(P.ctr, 0, 4 * (size_t)pv::kCtrInts, st));
-  if (!nd->pev[0]) FL_HIP(hipEventCreate(&nd->pev[0]));
-  if (!nd->pev[1]) FL_HIP(hipEventCreate(&nd->pev[1]));
-  FL_HIP(hipEventRecord(nd->pev[0], st));
+  P.inject_step = tn().pva_inject;
+  if (!cap) {
+    if (!nd->pev[0]) FL_HIP(hipEventCreate(&nd->pev[0]));
+    if (!nd->pev[1]) FL_HIP(hipEventCreate(&nd->pev[1]));
+    FL_HIP(hipEventRecord(nd->pev[0], st));
+  }
   const int lrc = pv::pva_persist_launch(P, st);
-  if (lrc) return lrc;
-  FL_HIP(hipEventRecord(nd->pev[1], st));
-  FL_HIP(hipMemcpyAsync(nd->perr_host, P.ctr + pv::CT_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
-  FL_HIP(hipStreamSynchronize(st));
-  if (*nd->perr_host != 0) {  // a wait timed out: every workgroup left; both states are rolled back
-    FL_HIP(hipMemcpyAsync(dur_t, backup, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
-    FL_HIP(hipMemcpyAsync(sil_t, backup + pv::kMaxM, 4 * (size_t)M, hipMemcpyDeviceToDevice, st));
-    nd->pbroken = true;
-    fprintf(stderr, "flamed: persistent PVA flow timed out (B*L=%d); this pair uses the graph path from now on\n", M);
+  if (lrc == kBadArg) {  // cooperative grid refused: never again on this device for this row-group count
+    nd->pdev_ok[P.RG] = 0;
     return kOk;
+  }
+  if (lrc) return lrc;
+  if (!cap) {
+    FL_HIP(hipEventRecord(nd->pev[1], st));
+    nd->pev_set = true;
+    FL_HIP(hipMemcpyAsync(nd->pfail_host, P.sticky, sizeof(int), hipMemcpyDeviceToHost, st));
   }
   *done = true;
   ++nd->pruns;
-  FL_HIP(hipEventElapsedTime(&nd->plast_ms, nd->pev[0], nd->pev[1]));
   return kOk;
 }
 
@@ -530,12 +569,12 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
   int rc;
   if ((rc = net_prepare(nd, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBd, w.Pd, st))) return rc;
   if ((rc = net_prepare(ns, enc, M, ts, nfe, w.Fd, w.TH, w.TEMBs, w.Ps, st))) return rc;
-  if (use_graph && pva_persist_eligible(nd, ns, M, st)) {
+  if ((use_graph & 1) && !(use_graph & 2) && pva_persist_eligible(nd, ns, M)) {
     bool done = false;
     if ((rc = pva_persist_run(nd, ns, w, mask, dur_t, sil_t, nfe, B, L, dt, st, &done))) return rc;
     if (done) return kOk;
   }
-  if (!use_graph) {
+  if (!(use_graph & 1)) {
     for (int i = 0; i < nfe; ++i) {  // dur then sil on every step (pva.py:104-109)
       if ((rc = net_step(nd, w.Pd, w.TEMBd + (size_t)i * D, dur_t, mask, B, L, dt, bd, st))) return rc;
       if ((rc = net_step(ns, w.Ps, w.TEMBs + (size_t)i * D, sil_t, mask, B, L, dt, bs, st))) return rc;
@@ -596,16 +635,33 @@ FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int 
   FL_REQUIRE(nd && ns && nd->dev && ns->dev && B > 0 && L > 0, "flamed_pva_persist_ready: bad args");
   std::lock_guard<std::mutex> lk(nd->mu);
   FL_ON_DEVICE(nd->device);
-  return pva_persist_eligible(nd, ns, B * L, st) ? 1 : 0;
+  (void)st;  // the capture state no longer matters: the persistent launch is capturable
+  return pva_persist_eligible(nd, ns, B * L) ? 1 : 0;
 }
 
 FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms) {
   DurNet* n = reinterpret_cast<DurNet*>(dur);
   FL_REQUIRE(n && runs && broken && last_ms, "flamed_pva_persist_info: bad args");
   std::lock_guard<std::mutex> lk(n->mu);
+  DeviceGuard dg(n->device);
+  *last_ms = 0.f;
+  if (n->pev_set) {  // waits for the last uncaptured launch (a diagnostic query, not the call path)
+    FL_HIP(hipEventSynchronize(n->pev[1]));
+    FL_HIP(hipEventElapsedTime(last_ms, n->pev[0], n->pev[1]));
+  }
+  pva_poll_fails(n);
   *runs = n->pruns;
   *broken = n->pbroken ? 1 : 0;
-  *last_ms = n->plast_ms;
+  return kOk;
+}
+
+FLAMED_API int flamed_pva_persist_status(flamed_dur_t dur, int* runs, int* fails) {
+  DurNet* n = reinterpret_cast<DurNet*>(dur);
+  FL_REQUIRE(n && runs && fails, "flamed_pva_persist_status: bad args");
+  std::lock_guard<std::mutex> lk(n->mu);
+  *runs = n->pruns;
+  *fails = n->pfail_host ? __atomic_load_n(n->pfail_host, __ATOMIC_RELAXED) : 0;
+  pva_poll_fails(n);
   return kOk;
 }
 

@@ -249,38 +249,43 @@ __device__ __forceinline__ void dma_panel4(char* dst, const void* base, RowB row
 // (row c, K-quarter q) exactly as a v_mfma_f32_16x16x32_bf16 A operand takes it, so a wave's 16-B/lane load
 // of one K-step is ONE contiguous 1 KB (8 full lines) instead of 16 half-lines of 16 rows; rows past the
 // group's last row are stored as zeros.
-__device__ __forceinline__ unsigned frag_group_bytes(int KST) { return (unsigned)(4 * KST * 1024); }
+__device__ __forceinline__ unsigned frag_group_bytes(int KST) { return (unsigned)(4 * kMaxNTW * KST * 1024); }
 
 template <int K>
+// tile: the group's 16-row tile this wave multiplies (wave + 4 i for chunk i); first: the phase's first tile,
+// which waits for the weight panel's DMA and meets the other waves (the panel is then in LDS for the rest).
 __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[2], int wave, int lane_in,
-                                     unsigned long long* stamp = nullptr, int g = 0, bool frag = false) {
+                                     unsigned long long* stamp = nullptr, int g = 0, bool frag = false, int tile = -1,
+                                     bool first = true) {
   constexpr int KST = K / 32;
   const int lane = opq(lane_in);
+  if (tile < 0) tile = wave;
   acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
   acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int ntile = (nr + 15) >> 4;
   const int c = lane & 15, q = lane >> 4;
   u32x4 a[KST];
-  if (wave < ntile) {
+  if (tile < ntile) {
     if (frag) {
       const __amdgpu_buffer_rsrc_t rs =
           rsrc(reinterpret_cast<const char*>(A) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST));
-      const unsigned base = (unsigned)(((wave * KST) * 64 + lane) * 16);
+      const unsigned base = (unsigned)(((tile * KST) * 64 + lane) * 16);
 #pragma unroll
       for (int ks = 0; ks < KST; ++ks) a[ks] = ld16(rs, base + ks * 1024);
     } else {
       const __amdgpu_buffer_rsrc_t rs = rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
-      const unsigned base = (unsigned)(((16 * wave + c) * K + q * 8) * 2);
+      const unsigned base = (unsigned)(((16 * tile + c) * K + q * 8) * 2);
 #pragma unroll
       for (int ks = 0; ks < KST; ++ks) a[ks] = ld16(rs, base + ks * 64);
     }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KST) : "memory");  // this wave's (older) weight DMA landed
+    if (first) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KST) : "memory");  // this wave's (older) weight DMA landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();  // every wave's DMA: the whole panel is in LDS
-  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // FL_STAMPS timeline only
-  if (wave < ntile) {
+  if (first) __syncthreads();  // every wave's DMA: the whole panel is in LDS
+  if (first && stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // FL_STAMPS timeline only
+  if (tile < ntile) {
     // B fragments read kBP K-steps ahead of the MFMAs that consume them (a ring of registers), so the
     // LDS latency overlaps the matrix pipe instead of one lgkmcnt(0) per MFMA
     constexpr int kBP = 4;
@@ -380,7 +385,7 @@ __device__ __forceinline__ void gemm_kh(const bf16* A, int r0, int nr, char* wl,
 
 // LayerNorm partials (mean, M2 over the slot's 32 columns) of the wave's 16 rows, from the MFMA layout
 // (lane c, q holds rows 4q + i, columns c and 16 + c): write-through 8-B stores.
-__device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int wave, int lane_in,
+__device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int tile, int lane_in,
                                                bool local = false) {
   const int lane = opq(lane_in);
   const int c = lane & 15, q = lane >> 4;
@@ -390,7 +395,7 @@ __device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2
     const float mean = sm * (1.0f / kCols);
     const float d0 = x[0][i] - mean, d1 = x[1][i] - mean;
     const float m2 = wave_sum16(d0 * d0 + d1 * d1);
-    const int row = 16 * wave + 4 * q + i;
+    const int row = 16 * tile + 4 * q + i;
     if (c == 0 && row < nr) {
       const float2 v = make_float2(mean, m2);
       if (local)
@@ -454,7 +459,7 @@ __device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int
                                            bool local = false) {
   constexpr int CPR = kCols * (int)sizeof(OT) / 16;  // 16-B chunks per staged row
   const __amdgpu_buffer_rsrc_t rs = rsrc(dst, (unsigned)T * ld * (unsigned)sizeof(OT));
-  for (int idx = opq(threadIdx.x); idx < kMaxRows * CPR; idx += kThreads) {
+  for (int idx = opq(threadIdx.x); idx < kChunk * CPR; idx += kThreads) {
     const int row = idx / CPR, ch = idx % CPR;
     if (row < ra || row >= rb) continue;
     const u32x4 v = *reinterpret_cast<const u32x4*>(stg + (row * kCols * sizeof(OT)) + ch * 16);
@@ -464,29 +469,31 @@ __device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int
   }
 }
 
-// ... or, fragment-major (persist_opt 64): the staged bf16 tile (rows x this slot's 32 columns = K-step s of
-// the consumer) as group g's fragments (t, s): one contiguous 1 KB per 16-row tile, rows >= nr as zeros.
-__device__ __forceinline__ void flush_frag(const char* stg, bf16* dst, int g, int s, int nr, int KST, bool local) {
+// ... or, fragment-major (persist_opt 64): the staged bf16 chunk (rows x this slot's 32 columns = K-step s of
+// the consumer) as group g's fragments (t0 + t, s): one contiguous 1 KB per 16-row tile, rows >= nr (the
+// chunk's rows) as zeros; t0 = the chunk's first tile.
+__device__ __forceinline__ void flush_frag(const char* stg, bf16* dst, int g, int s, int nr, int KST, bool local, int t0 = 0) {
   const int ntile = (nr + 15) >> 4;
   const __amdgpu_buffer_rsrc_t rs = rsrc(reinterpret_cast<char*>(dst) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST));
   for (int idx = opq(threadIdx.x); idx < ntile * 64; idx += kThreads) {
     const int t = idx >> 6, ln = idx & 63, row = 16 * t + (ln & 15), q = ln >> 4;
     const u32x4 v = row < nr ? *reinterpret_cast<const u32x4*>(stg + row * (kCols * 2) + q * 16) : u32x4{0u, 0u, 0u, 0u};
-    const unsigned off = (unsigned)(((t * KST + s) * 64 + ln) * 16);
+    const unsigned off = (unsigned)((((t0 + t) * KST + s) * 64 + ln) * 16);
     if (local) st16p(rs, off, v);
     else st16(rs, off, v);
   }
 }
 
 // The fp32 residual rows other groups read: only the kHalo rows at each end of a group (the depthwise
-// halo of its neighbours), written through; the middle rows never leave the workgroup's registers.
-__device__ __forceinline__ void flush_halo(const char* stg, float* ximg, int r0, int nr, int col0, int T) {
-  if (nr <= 2 * kHalo) {
-    flush_tile<float>(stg, ximg, kH, r0, 0, nr, col0, T);
-    return;
-  }
-  flush_tile<float>(stg, ximg, kH, r0, 0, kHalo, col0, T);
-  flush_tile<float>(stg, ximg, kH, r0, nr - kHalo, nr, col0, T);
+// halo of its neighbours), written through; the middle rows never leave the workgroup's registers.  The staged
+// chunk holds the group's rows [c0, c0 + nrc) (chunk-local row = group row - c0).
+__device__ __forceinline__ void flush_halo(const char* stg, float* ximg, int r0, int nr, int col0, int T, int c0 = 0,
+                                           int nrc = -1) {
+  if (nrc < 0) nrc = nr;
+  const int a1 = min(c0 + nrc, kHalo);  // the group's first kHalo rows inside this chunk: [c0, a1)
+  if (a1 > c0) flush_tile<float>(stg, ximg, kH, r0 + c0, 0, a1 - c0, col0, T);
+  const int b0 = max(c0, max(nr - kHalo, kHalo)), b1 = c0 + nrc;  // its last kHalo rows (not written above)
+  if (b1 > b0) flush_tile<float>(stg, ximg, kH, r0 + c0, b0 - c0, b1 - c0, col0, T);
 }
 
 __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) {
@@ -498,7 +505,8 @@ __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) 
 
 // KH: GEMM phases split 2 x 2 over the waves (gemm_kh, persist_opt 1024): a template parameter, so each variant
 // gets its own register allocation
-template <bool KH>
+// NTW: chunks of 64 rows per group (template: registers are indexed by it), 1..kMaxNTW; KH only with NTW == 1.
+template <bool KH, int NTW>
 __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -542,7 +550,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   int L = 0;    // group signals so far (the same sequence in every workgroup)
   int ndg = 0;  // GroupNorm hand-offs so far
   int wb = 0;   // LDS buffer holding (or receiving) the weights of the next GEMM phase
-  const int wbase = 16 * wave;  // first tile row of this wave
 #ifdef FL_STAMPS
   int pst_k = 0;
 #endif
@@ -588,12 +595,20 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     }
   };
 
-  // Euler state: thread -> tile row xr_row, channels 8 s + 2 (tid & 3) + {0, 1}
+  // rows of chunk i: [kChunk i, kChunk i + crows(i)) of the group
+  auto crows = [&](int i) { return max(min(kChunk, nr - kChunk * i), 0); };
+  // Euler state: thread -> row kChunk i + xr_row of chunk i, channels 8 s + 2 (tid & 3) + {0, 1}
   const int xr_row = tid >> 2, xch = kCh * s + 2 * (tid & 3);
-  float xs0 = 0.f, xs1 = 0.f;
-  if (xr_row < nr) {
-    xs0 = P.xt[(size_t)(r0 + xr_row) * kC + xch];
-    xs1 = P.xt[(size_t)(r0 + xr_row) * kC + xch + 1];
+  float xs0[NTW], xs1[NTW];
+#pragma unroll
+  for (int i = 0; i < NTW; ++i) {
+    xs0[i] = 0.f;
+    xs1[i] = 0.f;
+    const int row = kChunk * i + xr_row;
+    if (row < nr) {
+      xs0[i] = P.xt[(size_t)(r0 + row) * kC + xch];
+      xs1[i] = P.xt[(size_t)(r0 + row) * kC + xch + 1];
+    }
   }
   // An abandoned solve leaves NaN in this workgroup's part of x (every workgroup leaves through here or
   // finishes normally), so a failure can never pass for a result.
@@ -608,9 +623,13 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
                              reinterpret_cast<int*>(smem + L_FLAG));
   };
   auto fail_exit = [&]() {
-    if (xr_row < nr) {
-      P.xt[(size_t)(r0 + xr_row) * kC + xch] = __builtin_nanf("");
-      P.xt[(size_t)(r0 + xr_row) * kC + xch + 1] = __builtin_nanf("");
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const int row = kChunk * i + xr_row;
+      if (row < nr) {
+        P.xt[(size_t)(r0 + row) * kC + xch] = __builtin_nanf("");
+        P.xt[(size_t)(r0 + row) * kC + xch + 1] = __builtin_nanf("");
+      }
     }
   };
   // weights of the first GEMM (proj_in) while the state is published
@@ -618,24 +637,29 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   // bf16 rows of x (proj_in's operand): 16 B per tile row, staged in LDS
   auto publish_xs = [&]() {
     bf16* t = reinterpret_cast<bf16*>(stg);
-    t[xr_row * kCh + 2 * (tid & 3)] = (bf16)xs0;
-    t[xr_row * kCh + 2 * (tid & 3) + 1] = (bf16)xs1;
-    __syncthreads();
-    if (frag) {  // channels 8 s .. 8 s + 7 = K-step s / 4, quarter s % 4 of proj_in's fragments
-      if (tid < 16 * ((nr + 15) >> 4)) {
-        const __amdgpu_buffer_rsrc_t rs =
-            rsrc(reinterpret_cast<char*>(P.xs) + (size_t)g * frag_group_bytes(kC / 32), frag_group_bytes(kC / 32));
-        const int t = tid >> 4, ln = (tid & 15) + 16 * (s & 3);
-        const u32x4 v = tid < nr ? *reinterpret_cast<const u32x4*>(stg + tid * 16) : u32x4{0u, 0u, 0u, 0u};
-        const unsigned off = (unsigned)(((t * (kC / 32) + (s >> 2)) * 64 + ln) * 16);
-        if (xloc) st16p(rs, off, v);
-        else st16(rs, off, v);
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const int nrc = crows(i);
+      if (i > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+      t[xr_row * kCh + 2 * (tid & 3)] = (bf16)xs0[i];
+      t[xr_row * kCh + 2 * (tid & 3) + 1] = (bf16)xs1[i];
+      __syncthreads();
+      if (frag) {  // channels 8 s .. 8 s + 7 = K-step s / 4, quarter s % 4 of proj_in's fragments
+        if (tid < 16 * ((nrc + 15) >> 4)) {
+          const __amdgpu_buffer_rsrc_t rs =
+              rsrc(reinterpret_cast<char*>(P.xs) + (size_t)g * frag_group_bytes(kC / 32), frag_group_bytes(kC / 32));
+          const int tt = 4 * i + (tid >> 4), ln = (tid & 15) + 16 * (s & 3);
+          const u32x4 v = tid < nrc ? *reinterpret_cast<const u32x4*>(stg + tid * 16) : u32x4{0u, 0u, 0u, 0u};
+          const unsigned off = (unsigned)(((tt * (kC / 32) + (s >> 2)) * 64 + ln) * 16);
+          if (xloc) st16p(rs, off, v);
+          else st16(rs, off, v);
+        }
+      } else if (tid < nrc) {
+        const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)TT * kC * 2);
+        const unsigned off = (unsigned)(((size_t)(r0 + kChunk * i + tid) * kC + kCh * s) * 2);
+        if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
+        else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
       }
-    } else if (tid < nr) {
-      const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)TT * kC * 2);
-      const unsigned off = (unsigned)(((size_t)(r0 + tid) * kC + kCh * s) * 2);
-      if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
-      else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
     }
     seal_put();
     signal(mygrp);
@@ -684,7 +708,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   }
   publish_xs();
 
-  float X[2][4];  // residual stream tile (this wave's 16 rows x 32 columns), MFMA layout
+  float X[NTW][2][4];  // residual stream tiles (this wave's tiles wave + 4 i: 16 rows x 32 columns each), MFMA layout
   f32x4 acc[2];
 
   for (int step = P.s0; step < P.s1; ++step) {
@@ -703,18 +727,23 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     PST(step);
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
-    if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    else gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    PST(step);
-    acc_to(X, acc);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+    for (int ci = 0; ci < NTW; ++ci) {
+      const int tl = wave + 4 * ci;
+      if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+      else gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
+      if (ci == 0) PST(step);
+      acc_to(X[ci], acc);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) X[nt][i] += binv[nt];
-    if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
-    stage_tile<float>(stg, X, wave, lane);
-    __syncthreads();
-    flush_halo(stg, P.ximg, r0, nr, col0, TT);
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X[ci][nt][i] += binv[nt];
+      if (16 * tl < nr) store_partials(P.xpart[0], X[ci], r0, nr, s, tl, lane);
+      if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+      stage_tile<float>(stg, X[ci], wave, lane);
+      __syncthreads();
+      flush_halo(stg, P.ximg, r0, nr, col0, TT, kChunk * ci, crows(ci));
+    }
     seal_put();
     if (dmafirst) {
       next_w(P.blk[0].w2);
@@ -761,74 +790,83 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       const int wa = max(r0 - kHalo, ub), wz = min(r0 + nr + kHalo, ue);  // the utterance's frames only
       // Everything this phase reads that does not wait on another phase goes out first, so the loads'
-      // latencies overlap: the thread's 3 window items (its 4 columns col0 + 4 (tid & 7) are the same in
-      // every item), their modulation vectors, the depthwise taps of channel cc, the row statistics.
-      constexpr int kItems = (kWin * 8 + kThreads - 1) / kThreads;
-      float4 hv[kItems];
+      // latencies overlap: the thread's halo item (its 4 columns col0 + 4 (tid & 7)), their modulation vectors,
+      // the depthwise taps of channel cc, the row statistics.  Halo items: the group's kHalo rows above and
+      // below it (window index hp, frame r0 - kHalo + hp; 30 rows x 8 column quads, threads < 240).
+      const int hid = tid >> 3, hp = hid < kHalo ? hid : nr + hid;
+      float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
       {
         const __amdgpu_buffer_rsrc_t rx = rsrc(P.ximg, (unsigned)TT * H * 4);
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-          const int idx = tid + k * kThreads, p = idx >> 3, r = r0 - kHalo + p;
-          const bool halo = idx < kWin * 8 && (p < kHalo || p >= kHalo + nr) && r >= ub && r < ue;
-          hv[k] = halo ? as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * (tid & 7)) * 4))) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        const int r = r0 - kHalo + hp;
+        if (hid < 2 * kHalo && r >= ub && r < ue) hv = as_f4(ld16(rx, (unsigned)(((size_t)r * H + col0 + 4 * (tid & 7)) * 4)));
       }
       row_stats(P.xpart[0], TT, wa, wz, r0 - kHalo, st);
       __syncthreads();
       PST(step);  // halo rows + row statistics in
-      // window h[p] (frame r0 - 15 + p): own rows from X (registers), halo rows from ximg, 0 outside [0, T)
+      // per chunk: window hs[pw] = frame r0 + c0 - kHalo + pw (pw < kWin): own rows from X (registers), halo rows
+      // from ximg, 0 outside the utterance; then the depthwise conv of the chunk's rows (zero padding at the
+      // utterance edges): thread -> channel cc, chunk rows 8 rg .. 8 rg + 7
+      float d[NTW][8];
 #pragma unroll
-      for (int k = 0; k < kItems; ++k) {
-        const int idx = tid + k * kThreads, p = idx >> 3, r = r0 - kHalo + p;
-        if (idx < kWin * 8 && (p < kHalo || p >= kHalo + nr)) {
-          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r >= ub && r < ue) {
-            const float mean = st[2 * p], rstd = st[2 * p + 1];
-            o.x = ((hv[k].x - mean) * rstd) * hva[0] + hvb[0];
-            o.y = ((hv[k].y - mean) * rstd) * hva[1] + hvb[1];
-            o.z = ((hv[k].z - mean) * rstd) * hva[2] + hvb[2];
-            o.w = ((hv[k].w - mean) * rstd) * hva[3] + hvb[3];
-          }
-          *reinterpret_cast<float4*>(hs + p * kCols + 4 * (tid & 7)) = o;
-        }
-      }
-      if (wbase < nr) {
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = wbase + 4 * q + i;
-            if (row < nr) {
-              const int p = row + kHalo;
-              hs[p * kCols + 16 * nt + c] = ((X[nt][i] - st[2 * p]) * st[2 * p + 1]) * ova[nt] + ovb[nt];
+      for (int ci = 0; ci < NTW; ++ci) {
+        const int c0 = kChunk * ci;
+        if (ci > 0) __syncthreads();  // the previous chunk's window has been read
+        if (hid < 2 * kHalo) {
+          const int pw = hp - c0, r = r0 - kHalo + hp;
+          if (pw >= 0 && pw < kWin) {
+            float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r >= ub && r < ue) {
+              const float mean = st[2 * hp], rstd = st[2 * hp + 1];
+              o.x = ((hv.x - mean) * rstd) * hva[0] + hvb[0];
+              o.y = ((hv.y - mean) * rstd) * hva[1] + hvb[1];
+              o.z = ((hv.z - mean) * rstd) * hva[2] + hvb[2];
+              o.w = ((hv.w - mean) * rstd) * hva[3] + hvb[3];
             }
+            *reinterpret_cast<float4*>(hs + pw * kCols + 4 * (tid & 7)) = o;
           }
-      }
-      __syncthreads();
-      PST(step);  // normalised window in LDS
-      // depthwise conv (zero padding at the utterance edges): thread -> channel cc, tile rows 8 rg .. 8 rg + 7
-      float d[8];
-      {
-        float win[8 + kTaps - 1];
+        }
 #pragma unroll
-        for (int j = 0; j < 8 + kTaps - 1; ++j) win[j] = hs[(8 * rg + j) * kCols + cc];
+        for (int j = 0; j < NTW; ++j) {
+          const int tb = 16 * (wave + 4 * j);  // first row of this wave's tile j
+          if (tb < nr && tb + 16 > c0 - kHalo && tb < c0 + kChunk + kHalo) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float a = dbias;
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-          for (int j = 0; j < kTaps; ++j) a = fmaf(w[j], win[k + j], a);
-          d[k] = a;
+              for (int i = 0; i < 4; ++i) {
+                const int row = tb + 4 * q + i, pw = row - c0 + kHalo;
+                if (row < nr && pw >= 0 && pw < kWin) {
+                  const int p = row + kHalo;
+                  hs[pw * kCols + 16 * nt + c] = ((X[j][nt][i] - st[2 * p]) * st[2 * p + 1]) * ova[nt] + ovb[nt];
+                }
+              }
+          }
+        }
+        __syncthreads();
+        if (ci == 0) PST(step);  // normalised window in LDS
+        {
+          float win[8 + kTaps - 1];
+#pragma unroll
+          for (int j = 0; j < 8 + kTaps - 1; ++j) win[j] = hs[(8 * rg + j) * kCols + cc];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            float a = dbias;
+#pragma unroll
+            for (int j = 0; j < kTaps; ++j) a = fmaf(w[j], win[k + j], a);
+            d[ci][k] = a;
+          }
         }
       }
       PST(step);  // depthwise conv done
       // GroupNorm partials of this group's frames: exact two passes (sum, squared deviations)
-      const int nv = min(max(nr - 8 * rg, 0), 8);
       {
         float sm = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < nv) sm += d[k];
+        for (int ci = 0; ci < NTW; ++ci) {
+          const int nv = min(max(crows(ci) - 8 * rg, 0), 8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k < nv) sm += d[ci][k];
+        }
         red[rg * kCols + cc] = sm;
         __syncthreads();
         float tot = 0.f;
@@ -838,11 +876,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         __syncthreads();
         float m2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < nv) {
-            const float e = d[k] - mg;
-            m2 = fmaf(e, e, m2);
-          }
+        for (int ci = 0; ci < NTW; ++ci) {
+          const int nv = min(max(crows(ci) - 8 * rg, 0), 8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k < nv) {
+              const float e = d[ci][k] - mg;
+              m2 = fmaf(e, e, m2);
+            }
+        }
         red[rg * kCols + cc] = m2;
         __syncthreads();
         if (tid < kCols) {
@@ -937,11 +979,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         const float4 gv = gnv[cc];
         bf16* t = reinterpret_cast<bf16*>(stg);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[(8 * rg + k) * kCols + cc] = (bf16)((d[k] - gv.x) * gv.y + gv.z);
+        for (int ci = 0; ci < NTW; ++ci) {
+          if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t[(8 * rg + k) * kCols + cc] = (bf16)((d[ci][k] - gv.x) * gv.y + gv.z);
+          __syncthreads();
+          if (frag) flush_frag(stg, P.a2, g, s, crows(ci), kH / 32, xloc, 4 * ci);
+          else flush_tile<bf16>(stg, P.a2, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
+        }
       }
-      __syncthreads();
-      if (frag) flush_frag(stg, P.a2, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.a2, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       signal(mygrp);
       PST(step);
@@ -952,21 +998,24 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    else gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-      PST(step);
-      {
+#pragma unroll
+      for (int ci = 0; ci < NTW; ++ci) {
+        const int tl = wave + 4 * ci;
+        if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+        else gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
+        if (ci == 0) PST(step);
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b2v[nt]);
         }
+        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
         stage_tile<bf16>(stg, v, wave, lane);
+        __syncthreads();
+        if (frag) flush_frag(stg, P.u, g, s, crows(ci), kH / 32, xloc, 4 * ci);
+        else flush_tile<bf16>(stg, P.u, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
       }
-      __syncthreads();
-      if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       if (dmafirst) {
         next_w(bw.w3);
@@ -991,28 +1040,31 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-      PST(step);
-      {
+#pragma unroll
+      for (int ci = 0; ci < NTW; ++ci) {
+        const int tl = wave + 4 * ci;
+        if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+        else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
+        if (ci == 0) PST(step);
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int p = wbase + 4 * q + i + kHalo;
-            const float xh = (X[nt][i] - st[2 * p]) * st[2 * p + 1];
+            const int p = 16 * tl + 4 * q + i + kHalo;
+            const float xh = (X[ci][nt][i] - st[2 * p]) * st[2 * p + 1];
             const float h = xh * ova[nt] + ovb[nt];
-            X[nt][i] = X[nt][i] + g3[nt] * (h + (acc[nt][i] + b3v[nt]));
-            v[nt][i] = X[nt][i] * alv[nt];
+            X[ci][nt][i] = X[ci][nt][i] + g3[nt] * (h + (acc[nt][i] + b3v[nt]));
+            v[nt][i] = X[ci][nt][i] * alv[nt];
           }
         }
-        if (wbase < nr) store_partials(P.xpart[1], X, r0, nr, s, wave, lane, xloc);
+        if (16 * tl < nr) store_partials(P.xpart[1], X[ci], r0, nr, s, tl, lane, xloc);
+        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
         stage_tile<bf16>(stg, v, wave, lane);
+        __syncthreads();
+        if (frag) flush_frag(stg, P.xa, g, s, crows(ci), kH / 32, xloc, 4 * ci);
+        else flush_tile<bf16>(stg, P.xa, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
       }
-      __syncthreads();
-      if (frag) flush_frag(stg, P.xa, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.xa, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       if (dmafirst) {
         if (fin) issue_out();  // conv_out's panel (into the other buffer; the flip follows the loop)
@@ -1034,24 +1086,27 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
       row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
-      if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);  // (its barrier orders the statistics)
-      PST(step);
-      {
+#pragma unroll
+      for (int ci = 0; ci < NTW; ++ci) {
+        const int tl = wave + 4 * ci;
+        if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+        else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);  // (the first tile's barrier orders the statistics)
+        if (ci == 0) PST(step);
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int p = wbase + 4 * q + i + kHalo;
+            const int p = 16 * tl + 4 * q + i + kHalo;
             v[nt][i] = silu(st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa0[nt]) + fb0[nt]);
           }
         }
+        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
         stage_tile<bf16>(stg, v, wave, lane);
+        __syncthreads();
+        if (frag) flush_frag(stg, P.u, g, s, crows(ci), kH / 32, xloc, 4 * ci);
+        else flush_tile<bf16>(stg, P.u, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
       }
-      __syncthreads();
-      if (frag) flush_frag(stg, P.u, g, s, nr, kH / 32, xloc);
-      else flush_tile<bf16>(stg, P.u, H, r0, 0, nr, col0, TT, xloc);
       seal_put();
       if (dmafirst) {
         next_w(bw.m2);
@@ -1068,17 +1123,22 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
-      if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-      PST(step);
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int ci = 0; ci < NTW; ++ci) {
+        const int tl = wave + 4 * ci;
+        if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+        else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
+        if (ci == 0) PST(step);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) X[nt][i] = X[nt][i] + g2v[nt] * (acc[nt][i] + bm2[nt]);
-      if (wbase < nr) store_partials(P.xpart[0], X, r0, nr, s, wave, lane);
-      stage_tile<float>(stg, X, wave, lane);
-      __syncthreads();
-      flush_halo(stg, P.ximg, r0, nr, col0, TT);
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) X[ci][nt][i] = X[ci][nt][i] + g2v[nt] * (acc[nt][i] + bm2[nt]);
+        if (16 * tl < nr) store_partials(P.xpart[0], X[ci], r0, nr, s, tl, lane);
+        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+        stage_tile<float>(stg, X[ci], wave, lane);
+        __syncthreads();
+        flush_halo(stg, P.ximg, r0, nr, col0, TT, kChunk * ci, crows(ci));
+      }
       seal_put();
       if (dmafirst) {
         next_w(P.blk[blk + 1].w2);
@@ -1109,18 +1169,30 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
     row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
-    if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-    else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
+    f32x4 acco[NTW][2];  // every tile's products first: with several chunks Y goes into this phase's panel buffer
+#pragma unroll
+    for (int ci = 0; ci < NTW; ++ci) {
+      if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[ci], wave, lane, PSTP(step), g, frag);
+      else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[ci], wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag,
+                    wave + 4 * ci, ci == 0);
+    }
     PST(step);
-    float* yl = reinterpret_cast<float*>(stg);  // Y of the tile: [row][24] fp32 (tap-major x 8 channels)
+    // Y of the group: [row][24] fp32 (tap-major x 8 channels) -- in the staging tile (one chunk), or in the
+    // panel conv_out has just finished reading (several chunks: 320 x 24 x 4 B; the next panel DMA goes to the
+    // other buffer, and this one is not rewritten before the next step's proj_in)
+    float* yl = reinterpret_cast<float*>(NTW == 1 ? stg : smem + wb * kWPanel);
+    if (NTW > 1) __syncthreads();  // every wave is done with the panel
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int n = 16 * nt + c;
-      if (n < 24) {
+    for (int ci = 0; ci < NTW; ++ci) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = wbase + 4 * q + i, p = row + kHalo;
-          yl[row * 24 + n] = st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fac[nt]) + fbc[nt];
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = 16 * nt + c;
+        if (n < 24) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * (wave + 4 * ci) + 4 * q + i, p = row + kHalo;
+            if (NTW == 1 || row < nr) yl[row * 24 + n] = st[2 * p + 1] * (acco[ci][nt][i] - st[2 * p] * fac[nt]) + fbc[nt];
+          }
         }
       }
     }
@@ -1147,44 +1219,52 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     PST(step);
     if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }
     PST(step);
-    if (xr_row < nr) {
-      const int t = r0 + xr_row;
-      int gp = 0, gn_ = 0;  // the groups owning frames r0 - 1 and r0 + nr (nearest non-empty neighbours)
-      for (int k = 0; k < kGroups; ++k) {
-        int a, b;
-        group_rows(k, T, P.B, a, b, P.opt);
-        if (b > 0 && a + b == r0) gp = k;
-        if (b > 0 && a == r0 + nr) gn_ = k;
-      }
-      const __amdgpu_buffer_rsrc_t ry = rsrc(P.yb, kWGs * 16 * 4);
-      float vv[2];
+    int gp = 0, gn_ = 0;  // the groups owning frames r0 - 1 and r0 + nr (nearest non-empty neighbours)
+    for (int k = 0; k < kGroups; ++k) {
+      int a, b;
+      group_rows(k, T, P.B, a, b, P.opt);
+      if (b > 0 && a + b == r0) gp = k;
+      if (b > 0 && a == r0 + nr) gn_ = k;
+    }
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int chl = 2 * (tid & 3) + e, ch = kCh * s + chl;
-        float v = P.bout[ch] + yl[xr_row * 24 + 8 + chl];
-        if (t > ub) {  // zero padding at the utterance's edges (conv_out k3)
-          const float y0 = xr_row > 0 ? yl[(xr_row - 1) * 24 + chl]
-                                      : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            ry, (unsigned)(((gp + kGroups * s) * 16 + chl) * 4), 0, 16));
-          v += y0;
+    for (int ci = 0; ci < NTW; ++ci) {
+      const int row = kChunk * ci + xr_row;
+      if (row < nr) {
+        const int t = r0 + row;
+        const __amdgpu_buffer_rsrc_t ry = rsrc(P.yb, kWGs * 16 * 4);
+        float vv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int chl = 2 * (tid & 3) + e, ch = kCh * s + chl;
+          float v = P.bout[ch] + yl[row * 24 + 8 + chl];
+          if (t > ub) {  // zero padding at the utterance's edges (conv_out k3)
+            const float y0 = row > 0 ? yl[(row - 1) * 24 + chl]
+                                     : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           ry, (unsigned)(((gp + kGroups * s) * 16 + chl) * 4), 0, 16));
+            v += y0;
+          }
+          if (t < ue - 1) {
+            const float y2 = row < nr - 1 ? yl[(row + 1) * 24 + 16 + chl]
+                                          : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                ry, (unsigned)(((gn_ + kGroups * s) * 16 + 8 + chl) * 4), 0, 16));
+            v += y2;
+          }
+          vv[e] = v;
         }
-        if (t < ue - 1) {
-          const float y2 = xr_row < nr - 1 ? yl[(xr_row + 1) * 24 + 16 + chl]
-                                           : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 ry, (unsigned)(((gn_ + kGroups * s) * 16 + 8 + chl) * 4), 0, 16));
-          v += y2;
-        }
-        vv[e] = v;
+        xs0[ci] = __fadd_rn(xs0[ci], __fmul_rn(P.dt, vv[0]));
+        xs1[ci] = __fadd_rn(xs1[ci], __fmul_rn(P.dt, vv[1]));
       }
-      xs0 = __fadd_rn(xs0, __fmul_rn(P.dt, vv[0]));
-      xs1 = __fadd_rn(xs1, __fmul_rn(P.dt, vv[1]));
     }
     __syncthreads();  // yl (staging) is rewritten by publish_xs
     if (step + 1 < P.s1) publish_xs();
   }
-  if (xr_row < nr) {
-    P.xt[(size_t)(r0 + xr_row) * kC + xch] = xs0;
-    P.xt[(size_t)(r0 + xr_row) * kC + xch + 1] = xs1;
+#pragma unroll
+  for (int ci = 0; ci < NTW; ++ci) {
+    const int row = kChunk * ci + xr_row;
+    if (row < nr) {
+      P.xt[(size_t)(r0 + row) * kC + xch] = xs0[ci];
+      P.xt[(size_t)(r0 + row) * kC + xch + 1] = xs1[ci];
+    }
   }
 }
 
@@ -1198,15 +1278,25 @@ int persist_stamps(void* buf, int step) {
 }
 #endif
 
+// Every kernel variant: [0] the 2 x 2 wave-split GEMM (persist_opt 1024, one chunk), [ntw] ntw chunks per group.
+static const void* const* persist_kernels() {
+  static const void* const k[kMaxNTW + 1] = {
+      reinterpret_cast<const void*>(den_persist_kernel<true, 1>), reinterpret_cast<const void*>(den_persist_kernel<false, 1>),
+      reinterpret_cast<const void*>(den_persist_kernel<false, 2>), reinterpret_cast<const void*>(den_persist_kernel<false, 3>),
+      reinterpret_cast<const void*>(den_persist_kernel<false, 4>), reinterpret_cast<const void*>(den_persist_kernel<false, 5>)};
+  static_assert(kMaxNTW == 5, "kernel table");
+  return k;
+}
+
 bool persist_device_ok(int device) {
   int cus = 0, nb = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus != kWGs) return false;
-  int nb2 = 0;
-  if (set_max_lds(reinterpret_cast<const void*>(den_persist_kernel<false>)) != hipSuccess) return false;
-  if (set_max_lds(reinterpret_cast<const void*>(den_persist_kernel<true>)) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, den_persist_kernel<false>, kThreads, kLds) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, den_persist_kernel<true>, kThreads, kLds) != hipSuccess) return false;
-  return nb >= 1 && nb2 >= 1;
+  for (int i = 0; i <= kMaxNTW; ++i) {
+    const void* k = persist_kernels()[i];
+    if (set_max_lds(k) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, kLds) != hipSuccess || nb < 1) return false;
+  }
+  return true;
 }
 
 int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
@@ -1219,8 +1309,11 @@ int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
   // (hipErrorCooperativeLaunchTooLarge) instead of queueing workgroups behind resident ones that wait for
   // them.  Capturable: a captured cooperative launch replays cooperatively (MI355X_MICROARCH.md, Residency).
   void* args[] = {&P};
-  const void* kern = (P.opt & 1024) ? reinterpret_cast<const void*>(den_persist_kernel<true>)
-                                    : reinterpret_cast<const void*>(den_persist_kernel<false>);
+  if (P.ntw < 1 || P.ntw > kMaxNTW || ((P.opt & 1024) && P.ntw != 1)) {
+    set_error("persistent solve: %d row chunks per group (1..%d; the wave-split GEMM variant takes one)", P.ntw, kMaxNTW);
+    return kBadArg;
+  }
+  const void* kern = persist_kernels()[(P.opt & 1024) ? 0 : P.ntw];
   const hipError_t e = cooperative ? hipLaunchCooperativeKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st)
                                    : hipLaunchKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st);
   if (e != hipSuccess) {

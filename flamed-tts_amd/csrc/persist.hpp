@@ -3,9 +3,12 @@
 // in ONE launch of 256 workgroups (one per CU), the phases of a step chained by in-launch hand-offs
 // instead of 25 kernel boundaries.
 //
-// Work split (speed only; correctness never depends on placement).  Workgroup b is (group g = b % 8,
-// slot s = b / 8): under the round-robin dispatch the 32 slots of a group share one XCD and its L2.
-// Group g owns a contiguous range of <= 64 frames (whole 16-row MFMA tiles); slot s owns hidden
+// Work split (speed only; correctness never depends on placement).  Workgroup b is (group g, slot s); with the
+// default persist_opt bit 8 the XCDs form a 2 x 4 grid: the round-robin dispatch puts b on XCD x = b % 8, which
+// holds row groups 4 (x / 4) .. + 3 and slots 8 (x % 4) .. + 7 (so each weight panel is read by 2 XCDs and each
+// group's hand-off rows by 4; without bit 8, g = b % 8 and s = b / 8: one group per XCD, every panel on all 8).
+// Group g owns a contiguous range of <= 320 frames (equal shares of the utterance), processed as chunks of 64
+// (four 16-row MFMA tiles, one per wave; NTW chunks: a kernel variant per chunk count); slot s owns hidden
 // columns [32 s, 32 s + 32) and latent channels [8 s, 8 s + 8).  What stays on chip across phases:
 //   * the residual stream X of the workgroup's (frames x 32 columns) tile, in registers;
 //   * the Euler state x of its (frames x 8 channels), in registers across ALL steps (fp32);
@@ -39,14 +42,16 @@ namespace pk {
 
 constexpr int kGroups = 8, kSlots = 32, kWGs = kGroups * kSlots, kThreads = 256;
 constexpr int kH = 1024, kC = 256, kCols = kH / kSlots, kCh = kC / kSlots;
-constexpr int kMaxRows = 64, kHalo = 15, kTaps = 31, kWin = kMaxRows + 2 * kHalo;
+// A row group holds up to kMaxNTW chunks of kChunk = 64 frames (chunk i = 16-row tiles 4 i .. 4 i + 3, wave w owning
+// tile 4 i + w): T <= 8 x 320 = 2560 frames for one utterance (30 s at 80 Hz is 2400).
+constexpr int kChunk = 64, kMaxNTW = 5, kMaxRows = kChunk * kMaxNTW, kHalo = 15, kTaps = 31, kWin = kChunk + 2 * kHalo;
 constexpr int kMaxNB = 8, kMaxT = kGroups * kMaxRows;
 // LDS carve (bytes): two weight panels, the dwconv window (aliased by the epilogue staging tile), row
 // statistics of the window, GroupNorm reduction scratch, poll flag
 constexpr int kWPanel = kCols * kH * 2;
 constexpr int L_HS = 2 * kWPanel;
 constexpr int L_ST = L_HS + kWin * kCols * 4;
-constexpr int L_RED = L_ST + kWin * 8;
+constexpr int L_RED = L_ST + (kMaxRows + 2 * kHalo) * 8;  // row statistics of the whole group window
 constexpr int L_GNV = L_RED + 8 * kCols * 4;
 constexpr int L_FLAG = L_GNV + kCols * 16;
 constexpr int kLds = (L_FLAG + 16 + 15) / 16 * 16;
@@ -102,6 +107,7 @@ struct Params {
                            // (unsigned tickets), [SY_PFAIL] the last launch whose prologue failed (counted once)
   int inject_step = -1;    // diagnostic (flamed_tune persist_inject): every workgroup fails at this step
   long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
+  int ntw = 1;             // row chunks (64 frames each) per group: the kernel variant (rows per group <= 64 ntw)
   int opt = 0;                        // experiment bits (flamed_tune persist_opt)
   unsigned long long* pst = nullptr;  // FL_STAMPS builds: timeline of step pst_step (persist_timeline.py)
   int pst_step = -1;
@@ -109,6 +115,13 @@ struct Params {
 
 // Host side (persist.hip): whether this device runs the 256-workgroup grid fully resident, and the launch.
 bool persist_device_ok(int device);
+// Row chunks per group for B utterances of T frames (group_rows' largest share; opt bit 2: whole 16-row tiles).
+inline int persist_ntw(int B, int T, int opt) {
+  const int gpu = kGroups / B;
+  int R = (T + gpu - 1) / gpu;
+  if (opt & 2) R = ((T + 15) / 16 + gpu - 1) / gpu * 16;
+  return (R + kChunk - 1) / kChunk;
+}
 int persist_launch(const Params& P, hipStream_t st, bool cooperative = true);
 
 }  // namespace pk

@@ -47,9 +47,16 @@ __device__ __forceinline__ void signal(int* ctr) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Abandon the flow: the first workgroup to set the error word also counts the failed launch in the sticky word.
+__device__ __forceinline__ void raise_err(int* err, int* fails) {
+  int expected = 0;
+  if (__hip_atomic_compare_exchange_strong(err, &expected, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    __hip_atomic_fetch_add(fails, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Wave 0 polls the counters of row groups rg - 1, rg, rg + 1 (those that exist) until each reaches
 // `target`; bounded by tmo, and an error word set by any workgroup ends every wait.  false: abandon.
-__device__ __forceinline__ bool wait3(int* err, long long tmo, int* base, int rg, int RG, int target, int* flag) {
+__device__ __forceinline__ bool wait3(int* err, int* fails, long long tmo, int* base, int rg, int RG, int target, int* flag) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x, g = rg - 1 + lane;
     const bool need = lane < 3 && g >= 0 && g < RG;
@@ -62,7 +69,7 @@ __device__ __forceinline__ bool wait3(int* err, long long tmo, int* base, int rg
       if ((it & 31) == 31) {
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
         if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
-          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) raise_err(err, fails);
           ok = false;
           break;
         }
@@ -231,7 +238,32 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   int* h1 = P.ctr + CT_H1 + net * kMaxRG * kLine;
   int* h2 = P.ctr + CT_H2 + net * kMaxRG * kLine;
   int* errw = P.ctr + CT_ERR;
+  int* fails = P.sticky;
   const long long tmo = P.tmo;
+  // Every workgroup leaves through here, after its last counter access: a failed flow writes NaN into its rows
+  // of x_t (slice-0 workgroups own the write-back); the last workgroup to count its exit zeroes the counters
+  // this launch used, for the next launch.
+  auto leave = [&](bool ok) {
+    if (!ok && cs == 0)
+      for (int i = tid; i < nr; i += kThreads) N.xt[r0 + i] = __builtin_nanf("");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      flag[1] = __hip_atomic_fetch_add(P.ctr + CT_EXIT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == P.grid - 1;
+    __syncthreads();
+    if (flag[1]) {
+      const int n = 2 * P.RG;  // per net and row group: an H1 and an H2 counter
+      if (tid < 2 * n) {
+        const int which = tid / n, k = tid - which * n, nn = k / P.RG, g = k - nn * P.RG;
+        __hip_atomic_store(P.ctr + (which ? CT_H2 : CT_H1) + (nn * kMaxRG + g) * kLine, 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      } else if (tid == 2 * n) {
+        __hip_atomic_store(P.ctr + CT_ERR, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (tid == 2 * n + 1) {
+        __hip_atomic_store(P.ctr + CT_EXIT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
 
   // ---- resident state: this workgroup's weight columns of both convs, shared vectors, x_t window
   for (int i = tid; i < kCols * K1 / 4; i += kThreads) {
@@ -305,6 +337,11 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
 #ifdef FL_STAMPS
     int pst_k = 0;
 #endif
+    if (s == P.inject_step) {  // diagnostic failure injection
+      if (tid == 0) raise_err(errw, fails);
+      leave(false);
+      return;
+    }
     for (int i = tid; i < D; i += kThreads) vte[i] = N.temb[(size_t)s * D + i];
     if (nt == 1)  // conv1's P window rows (constant, but the staging area is shared with conv2's rows)
       for (int i = tid; i < nw * (D / 4); i += kThreads) {
@@ -342,7 +379,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
     PVST();
     signal(h1 + rg * kLine);
     PVST();
-    if (!wait3(errw, tmo, h1, rg, P.RG, CS * (s + 1), flag)) return;
+    if (!wait3(errw, fails, tmo, h1, rg, P.RG, CS * (s + 1), flag)) { leave(false); return; }
     PVST();
 
     // LN1 statistics of the window rows from the CS partials (equal-count combine, as the launch path)
@@ -418,7 +455,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
     PVST();
     signal(h2 + rg * kLine);
     PVST();
-    if (!wait3(errw, tmo, h2, rg, P.RG, CS * (s + 1), flag)) return;
+    if (!wait3(errw, fails, tmo, h2, rg, P.RG, CS * (s + 1), flag)) { leave(false); return; }
     PVST();
 
     // ---- head (LN2 . lw + lb, masked_fill) + Euler update of the window rows (pva.py:104-109, 234-238)
@@ -451,6 +488,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   }
   if (cs == 0)
     for (int i = tid; i < nr; i += kThreads) N.xt[r0 + i] = xs[i + 1];
+  leave(true);
 }
 
 size_t pva_persist_lds() { return (size_t)Lds<192, 384>::BYTES; }
@@ -471,11 +509,17 @@ int pva_persist_launch(const Params& Pin, hipStream_t st) {
   P.pst = g_pva_pst;
   P.pst_step = g_pva_pst_step;
 #endif
-  const int grid = 2 * Lds<192, 384>::CS * P.RG;
-  auto kern = pva_persist_kernel<192, 384>;
-  constexpr unsigned lds = Lds<192, 384>::BYTES;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st, P);
-  FL_LAUNCH_CHECK();
+  P.grid = 2 * Lds<192, 384>::CS * P.RG;
+  // cooperative: the runtime checks the grid against the occupancy and refuses it up front; a captured
+  // cooperative launch replays cooperatively
+  void* args[] = {&P};
+  const void* kern = reinterpret_cast<const void*>(pva_persist_kernel<192, 384>);
+  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3(P.grid), dim3(kThreads), args, Lds<192, 384>::BYTES, st);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("persistent PVA flow: hipLaunchCooperativeKernel -> %s", hipGetErrorString(e));
+    return e == hipErrorCooperativeLaunchTooLarge ? kBadArg : kHip;
+  }
   return kOk;
 }
 

@@ -24,8 +24,13 @@
 // barrier, relaxed agent-scope ticket; consumers poll and read with sc1 loads).  WAR safety without double
 // buffers: a row group rewrites R1 / S1 only after H2 of the previous step, i.e. after every reader of
 // those rows (itself and its two neighbours) has finished conv2; S2 only after H1 of the next step, i.e.
-// after every reader has finished its head.  Every spin is bounded (timeout -> error word -> all exit);
-// the host then restores x_t and runs the launch path.
+// after every reader has finished its head.  The launch is cooperative (every workgroup co-resident, or the
+// runtime refuses it up front) and only enqueued: no host synchronisation, so it can be captured.  Every spin is
+// bounded: a timeout sets the error word (the first to set it adds one to a sticky failure count the host reads
+// asynchronously), every workgroup leaves, and x_t is written as NaN -- a failed flow is loud, never silently
+// wrong (the Python wrapper waits for the flow, re-runs a failed one on the graph path, and after 3 failures the
+// pair stays there).  The counter block resets itself: each workgroup counts its exit, the last one zeroes the
+// block, so no memset node has to precede the kernel in a captured graph.
 #pragma once
 #include "common.hpp"
 
@@ -35,7 +40,8 @@ namespace pv {
 constexpr int kThreads = 256, kCols = 16, kMaxRG = 5, kMaxTiles = 8, kMaxRowsWG = 16 * kMaxTiles;
 constexpr int kMaxM = kMaxRG * kMaxRowsWG;  // 640 phoneme rows (B * L)
 constexpr int kLine = 16;                   // ints per counter (one 64-B line each)
-constexpr int CT_H1 = 0, CT_H2 = 2 * kMaxRG * kLine, CT_ERR = 4 * kMaxRG * kLine, kCtrInts = CT_ERR + kLine;
+constexpr int CT_H1 = 0, CT_H2 = 2 * kMaxRG * kLine, CT_ERR = 4 * kMaxRG * kLine, CT_EXIT = CT_ERR + kLine,
+              kCtrInts = CT_EXIT + kLine;
 
 struct NetP {
   const float *P, *w0, *temb, *c1w, *c1b, *g1, *b1, *c2w, *c2b, *g2, *b2, *lw, *lb;
@@ -49,8 +55,12 @@ struct Params {
   float dt;
   const uint8_t* mask;
   NetP net[2];
-  int* ctr;
+  int* ctr;       // hand-off counters, error word, exit count: zero at launch start; the last workgroup to leave
+                  // zeroes them again for the next launch (stream-ordered after this one)
+  int* sticky;    // [0] failed launches so far (never reset; the host reads it asynchronously)
+  int grid;       // workgroups of this launch (2 nets x CS slices x RG row groups)
   long long tmo;  // poll timeout, s_memrealtime ticks (100 MHz)
+  int inject_step = -1;  // diagnostic (flamed_tune pva_inject): every workgroup abandons the flow at this step
   unsigned long long* pst = nullptr;  // FL_STAMPS builds: per-workgroup timeline of step pst_step
   int pst_step = -1;
 };

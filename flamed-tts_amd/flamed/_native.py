@@ -57,6 +57,7 @@ SIGNATURES = {
     "flamed_pva_flow": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, P]),
     "flamed_pva_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_float)]),
     "flamed_pva_persist_ready": (c_int, [P, P, c_int, c_int, P]),
+    "flamed_pva_persist_status": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "flamed_lr_lengths": (c_int, [P, P, P, c_int, c_int, c_int, P, P, P]),
     "flamed_lr_expand": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "flamed_fac_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), c_int, ctypes.POINTER(P)]),

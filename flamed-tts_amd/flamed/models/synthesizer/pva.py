@@ -10,6 +10,7 @@ CPU tensors and autograd training use the modules' own torch ops.
 from __future__ import annotations
 
 import ctypes
+import warnings
 import math
 from collections import OrderedDict
 from typing import List
@@ -254,6 +255,12 @@ class PvaHIP:
         self._keep = []
         self.ws = nat.Workspace()
         self._bufs = {}
+        # after a persistent flow: wait for it and re-run it on the graph path if the kernel reported a failure
+        # (NaN states), so a failed launch never reaches the length regulator; skipped inside a stream capture
+        # (the caller then owns the check: persist_status).  The length regulator reads max(tgt_len) on the
+        # host right after the flow anyway (pva.py:158), so the wait costs little.
+        self.check_persist = True
+        self._fails_seen = 0
         self.oid = ops.register(self)  # torch.ops.flamed_hip.pva_flow
 
     def __del__(self):
@@ -306,10 +313,30 @@ class PvaHIP:
             s = sil_t.float().clone(memory_format=torch.contiguous_format)
             tsc = ts.float().contiguous()
             ws = self.ws.get(Lb.flamed_pva_workspace_size(self.handles[0], B, L, nfe), dev)
+            runs0, _ = self.persist_status()
             nat.check(Lb.flamed_pva_flow(self.handles[0], self.handles[1], nat.ptr(enc), nat.ptr(mask), nat.ptr(d),
                                          nat.ptr(s), nat.ptr(tsc), nfe, B, L, nat.ptr(ws), ws.numel(), 1,
                                          nat.stream_ptr(dev)), "flamed_pva_flow")
-            return d, s
+            if not (self.check_persist and not torch.cuda.is_current_stream_capturing()):
+                return d, s
+            runs1, _ = self.persist_status()
+            if runs1 == runs0:  # the grid was refused: the call took the graph path
+                return d, s
+            torch.cuda.current_stream(dev).synchronize()  # also completes the failure count's copy
+            _, fails = self.persist_status()
+            if fails <= self._fails_seen:
+                return d, s
+            self._fails_seen = fails
+            warnings.warn(f"flamed: persistent PVA flow failed ({fails} so far on this pair); "
+                          "re-running it on the graph path")
+            return self._graph_flow(x, src_mask, dur_t, sil_t, ts, nfe, 1 | 2)
+        return self._graph_flow(x, src_mask, dur_t, sil_t, ts, nfe, int(bool(self.pva.hip_graph)))
+
+    def _graph_flow(self, x, src_mask, dur_t, sil_t, ts, nfe, use_graph):
+        dev = x.device
+        self._ensure(dev)
+        B, L, D = x.shape
+        Lb = nat.lib()
         key = (B, L, nfe)
         bufs = self._bufs.get(key)
         if bufs is None:
@@ -327,9 +354,18 @@ class PvaHIP:
         ws = self.ws.get(Lb.flamed_pva_workspace_size(self.handles[0], B, L, nfe), dev)
         nat.check(Lb.flamed_pva_flow(self.handles[0], self.handles[1], nat.ptr(bufs["enc"]), nat.ptr(bufs["mask"]),
                                      nat.ptr(bufs["dur"]), nat.ptr(bufs["sil"]), nat.ptr(bufs["ts"]), nfe, B, L,
-                                     nat.ptr(ws), ws.numel(), int(bool(self.pva.hip_graph)), nat.stream_ptr(dev)),
+                                     nat.ptr(ws), ws.numel(), use_graph, nat.stream_ptr(dev)),
                   "flamed_pva_flow")
         return bufs["dur"].clone(), bufs["sil"].clone()
+
+    def persist_status(self):
+        """(persistent flows enqueued, failed launches as of the last completed copy) of this pair; never waits."""
+        if self.handles[0] is None:
+            return 0, 0
+        runs, fails = ctypes.c_int(), ctypes.c_int()
+        nat.check(nat.lib().flamed_pva_persist_status(self.handles[0], ctypes.byref(runs), ctypes.byref(fails)),
+                  "flamed_pva_persist_status")
+        return runs.value, fails.value
 
     def persist_info(self):
         """(persistent flows completed, timed out, device ms of the last one) on this pair (pvaflow.hip)."""

@@ -8,7 +8,7 @@
  * Conventions: every tensor argument is a DEVICE pointer owned by the caller, row-major, fp32
  * unless stated; work is enqueued on `stream` and is stream-ordered (no host synchronisation
  * inside, so every call is hipGraph-capturable except the *_load / *_create calls and the documented
- * diagnostic queries; flamed_pva_flow's persistent launch waits for its error word).  Scratch memory
+ * diagnostic queries).  Scratch memory
  * comes from a caller-provided workspace sized by the matching *_workspace_size query.
  * Handles: *_load copies or packs every weight and vector into the handle's own device arena (the
  * caller's tensors may be freed afterwards) on the device those tensors live on; each call on a
@@ -246,10 +246,14 @@ FLAMED_API int flamed_dur_load(flamed_dur_t h, const float* const* weights, int 
 FLAMED_API size_t flamed_pva_workspace_size(flamed_dur_t h, int B, int L, int nfe);
 /* Whole nfe-step flow of both generators, in place on dur_t / sil_t (B*L, the initial noise *
  * temperature).  enc: (B*L) x input_size encoder output; mask: uint8 B*L, 1 = padding (src_mask);
- * ts: nfe+1 fp32 time grid (torch.linspace(0, 1, nfe+1)).  use_graph != 0: the fast path -- one
- * persistent launch for every step of both nets (pvaflow.hpp; input 192, filter 384, B*L <= 640, all its
- * workgroups resident, stream not capturing, knob "pva_persist"; the call then waits for the launch to
- * check its error word), else a cached hipGraph replay; use_graph == 0: plain launches. */
+ * ts: nfe+1 fp32 time grid (torch.linspace(0, 1, nfe+1)).  use_graph bit 1: the fast path -- one
+ * persistent launch for every step of both nets (pvaflow.hpp; input 192, filter 384, B*L <= 640, knob
+ * "pva_persist"): cooperative (all workgroups co-resident, or refused up front and this row-group count then
+ * takes the graph path), only enqueued (no host synchronisation; capturable once the pair has run one
+ * uncaptured flow), self-resetting; a launch whose in-kernel wait times out leaves NaN in dur_t / sil_t and adds
+ * one to a sticky failure count read asynchronously by later calls (flamed_pva_persist_status), and after 3
+ * failures the pair takes the graph path -- else a cached hipGraph replay; bit 2: never the persistent launch
+ * (a caller's re-run of a failed flow); use_graph == 0: plain launches. */
 FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* enc, const uint8_t* mask, float* dur_t,
                                float* sil_t, const float* ts, int nfe, int B, int L, void* ws, size_t ws_bytes,
                                int use_graph, hipStream_t stream);
@@ -257,9 +261,12 @@ FLAMED_API int flamed_pva_flow(flamed_dur_t dur, flamed_dur_t sil, const float* 
  * counts), would run as the persistent launch (the caller may then pass its own buffers: no graph keyed on
  * their addresses), 0 otherwise. */
 FLAMED_API int flamed_pva_persist_ready(flamed_dur_t dur, flamed_dur_t sil, int B, int L, hipStream_t stream);
-/* (diagnostic) persistent PVA flows completed on the duration handle, whether one timed out (the pair
- * then stays on the graph path), device ms of the last one. */
+/* (diagnostic) persistent PVA flows enqueued on the duration handle, whether the pair has given up the
+ * persistent path (3 failed launches), device ms of the last uncaptured one (waits for it). */
 FLAMED_API int flamed_pva_persist_info(flamed_dur_t dur, int* runs, int* broken, float* last_ms);
+/* Never waits: persistent flows enqueued on this pair, and its failed launches as of the last completed
+ * asynchronous copy of the device's failure count (exact once the flow's stream has been synchronised). */
+FLAMED_API int flamed_pva_persist_status(flamed_dur_t dur, int* runs, int* fails);
 /* Length regulator, phase 1: per-utterance interleaved [phone_l, silence_l] repeat counts
  * (padding phonemes -> 1 frame, 0 silence), exclusive prefix sums cum (int64 B x (2L+1)) and
  * tgt_len (int64 B).  phone/sil are frame counts, or final log-durations when log_domain != 0

@@ -370,3 +370,39 @@ def test_persist_multi_utterance(pgb, B, T):
     errs = [rel_l2(out[b:b + 1], orc.euler_solve(sd, x0[b:b + 1], spk[b:b + 1], 8)) for b in range(B)]
     print(f"persistent B={B} T={T} 8 steps: vs oracle per utterance max {max(errs):.3e}; vs launch path {el:.3e}")
     assert max(errs) < BF16_SOLVE and el < 4e-3
+
+
+@pytest.mark.parametrize("B,T", [(1, 520), (1, 1000), (1, 2400), (2, 400), (4, 300), (2, 1111)])
+def test_persist_multi_chunk(pgb, B, T):
+    """the persistent solve beyond 64 frames per row group -- each group's rows as up to five
+    64-frame chunks (one 16-row tile per wave per chunk; a kernel variant per chunk count), so long-form
+    utterances (configs[4]: T = 2400) and B = 2 at T = 400 take one launch.  It must take the persistent path,
+    be bitwise deterministic, match the graph of launches (same bf16 operands, other fp32 order) at 4e-3 and
+    every utterance the one-utterance oracle solve at the bf16 solve bar (8 steps)."""
+    pg, sd = pgb
+    x0, spk = _inputs(50 + B + T, B, T)
+    r0 = _runs(pg)
+    a = _solve(pg, x0, spk, 8)
+    b = _solve(pg, x0, spk, 8)
+    assert _runs(pg) == r0 + 2, "the multi-chunk solve did not take the persistent path"
+    with knob("persist", 0, 1):
+        launch = _solve(pg, x0, spk, 8)
+    assert torch.isfinite(a).all() and torch.equal(a, b)
+    el = rel_l2(a, launch)
+    errs = [rel_l2(a[u:u + 1], orc.euler_solve(sd, x0[u:u + 1], spk[u:u + 1], 8)) for u in range(B)]
+    print(f"persistent multi-chunk B={B} T={T}: vs launch path {el:.3e}, vs oracle per utterance max {max(errs):.3e}")
+    assert el < 4e-3 and max(errs) < BF16_SOLVE
+
+
+def test_persist_multi_chunk_variants_bitwise(pgb):
+    """The multi-chunk kernel's hand-off variants (fragment-major off, counter-form GroupNorm) change data movement
+    only: bitwise equal to the default at T = 1000 (two chunks per group)."""
+    pg, _ = pgb
+    x0, spk = _inputs(61, 1, 1000)
+    a = _solve(pg, x0, spk, 8)
+    for flip in (64, 512):
+        with knob("persist_opt", PERSIST_DEFAULT ^ flip, PERSIST_DEFAULT):
+            r0 = _runs(pg)
+            b = _solve(pg, x0, spk, 8)
+            assert _runs(pg) == r0 + 1
+        assert torch.equal(a, b), flip

@@ -230,3 +230,88 @@ def test_pva_flow_default_nsteps_ragged(pva):
         flips += int((gf[safe] != rf[safe]).sum())
     print(f"PVA nfe=64 L=285 B=4: non-boundary flips {flips}, positions near a .5 boundary {near}")
     assert flips == 0
+
+
+def _flow_inputs(seed, B, L):
+    gen = torch.Generator().manual_seed(seed)
+    enc = torch.randn(B, L, 192, generator=gen).to(DEV)
+    lens = torch.tensor([L] + [max(1, L - 29 * i) for i in range(1, B)])
+    mask = (torch.arange(L)[None, :] >= lens[:, None]).to(DEV)
+    d = (torch.randn(B, L, generator=gen) * 0.3).to(DEV)
+    s = (torch.randn(B, L, generator=gen) * 0.3).to(DEV)
+    return enc, mask, d, s
+
+
+def test_pva_persist_graph_capture(pva):
+    """the persistent PVA flow keeps the C-ABI contract -- only enqueued (no host sync) and
+    capturable.  A torch.cuda.graph capture of the flow (after one uncaptured flow) takes the persistent launch
+    (the cooperative node; the kernel resets its own counters), and replays with changed inputs equal the eager
+    persistent flow bitwise."""
+    m, _ = pva
+    hp = m.hip()
+    B, L, nfe = 2, 70, 16
+    enc, mask, d0, s0 = _flow_inputs(61, B, L)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        hp.flow(enc, mask, d0, s0, ts, nfe)  # warm: scratch, handles
+        torch.cuda.synchronize()
+        r0 = hp.persist_status()[0]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            hp.flow(enc, mask, d0, s0, ts, nfe)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            od, os_ = hp.flow(enc, mask, d0, s0, ts, nfe)
+        assert hp.persist_status()[0] == r0 + 2, "the captured flow did not take the persistent launch"
+        outs = []
+        for rep in range(3):
+            e2, _, d2, s2 = _flow_inputs(70 + rep, B, L)
+            enc.copy_(e2), d0.copy_(d2), s0.copy_(s2)
+            g.replay()
+            torch.cuda.synchronize()
+            outs.append((od.clone(), os_.clone()))
+            ed, es = hp.flow(enc, mask, d0, s0, ts, nfe)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[-1][0], ed) and torch.equal(outs[-1][1], es), rep
+            assert torch.isfinite(ed).all()
+    assert not torch.equal(outs[0][0], outs[1][0])
+
+
+def test_pva_persist_failure_rerun_and_budget(pva):
+    """A persistent flow that gives up (diagnostic knob pva_inject: every workgroup abandons at that step) leaves
+    NaN in both states and is counted, without a host sync on the call path; the Python wrapper (check on, the
+    default) waits, warns and re-runs it on the graph path, so the caller gets the graph path's exact result;
+    after 3 failures the pair takes the graph path for good."""
+    import warnings
+    from flamed.models.synthesizer.pva import PvaHIP
+    m, _ = pva
+    hp = PvaHIP(m)  # a fresh pair: the module's own stays on the persistent path
+    B, L, nfe = 1, 60, 8
+    enc, mask, d0, s0 = _flow_inputs(81, B, L)
+    ts = torch.linspace(0, 1, nfe + 1, device=DEV)
+    with torch.inference_mode():
+        ref = hp._graph_flow(enc, mask, d0, s0, ts, nfe, 1 | 2)
+        try:
+            _tune("pva_inject", 3)
+            hp.check_persist = False
+            raw = hp.flow(enc, mask, d0, s0, ts, nfe)
+            torch.cuda.synchronize()
+            assert torch.isnan(raw[0]).all() and torch.isnan(raw[1]).all()
+            assert hp.persist_status()[1] == 1
+            hp.check_persist = True
+            with warnings.catch_warnings(record=True) as wl:
+                warnings.simplefilter("always")
+                out = hp.flow(enc, mask, d0, s0, ts, nfe)
+            assert any("persistent PVA flow failed" in str(w.message) for w in wl)
+            assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+            hp.flow(enc, mask, d0, s0, ts, nfe)  # third failure: the pair gives up the persistent path
+        finally:
+            _tune("pva_inject", -1)
+        runs, broken, _ = hp.persist_info()
+        assert runs == 3 and broken
+        after = hp.flow(enc, mask, d0, s0, ts, nfe)
+        assert hp.persist_info()[0] == 3
+    assert torch.equal(after[0], ref[0]) and torch.equal(after[1], ref[1])
