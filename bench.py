@@ -87,6 +87,7 @@ def parse():
     ap.add_argument("--persist-opt", type=int, default=None, help="flamed_tune persist_opt (persistent kernel experiment bits)")
     ap.add_argument("--split-batch", type=int, default=None, help="flamed_tune split_batch (large-M sub-batch chains, 1 = off)")
     ap.add_argument("--persist-capmode", type=int, default=None, help="flamed_tune persist_capmode")
+    ap.add_argument("--coop", type=int, default=None, help="flamed_tune coop (0: plain launches of the persistent kernels, for rocprofv3 runs)")
     ap.add_argument("--persist-multi", type=int, default=None, help="flamed_tune persist_multi (persistent solve for B = 2 / 4 / 8)")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured STREAM-copy / library-GEMM peaks")
     ap.add_argument("--plumbing", action="store_true",
@@ -681,7 +682,7 @@ def main():
     from flamed.utils.seeded_init import randomize_module
     from flamed import _native as nat
 
-    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler", "persist", "persist_opt", "split_batch", "persist_capmode", "persist_multi"):
+    for key in ("splitk_target", "splitk_max", "dup_class", "small_stages", "dma", "noctr", "bn32", "big", "big_ns", "dw_tc", "big_rows", "dw_cg32", "dw_cg", "dma_ns", "lnfold", "graph_steps", "xcd_strips", "x16", "g8p_rows", "dwgn", "dwgn_small", "fuse_euler", "persist", "persist_opt", "split_batch", "persist_capmode", "persist_multi", "coop"):
         v = getattr(args, key)
         if v is not None:
             nat.check(nat.lib().flamed_tune(key.encode(), v), "flamed_tune")

@@ -87,6 +87,9 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"pva_split", &Tune::pva_split, 0, 1, nullptr},
       {"persist", &Tune::persist, 0, 1, nullptr},
       {"split_batch", &Tune::split_batch, 1, 4, nullptr},
+      {"split_graph", &Tune::split_graph, 0, 1, nullptr},
+      {"split_prio", &Tune::split_prio, 0, 2, nullptr},
+      {"prio_all", &Tune::prio_all, 0, 1, nullptr},
       {"split_min_rows", &Tune::split_min_rows, 1024, 1 << 30, nullptr},
       {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
@@ -97,6 +100,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"attn_mfma", &Tune::attn_mfma, 0, 1, nullptr},
       {"prior_split", &Tune::prior_split, 0, 1, nullptr},
       {"stop_after", &Tune::stop_after, -1, 1 << 20, nullptr},
+      {"coop", &Tune::coop, 0, 1, nullptr},
       {"dwgn_var", &Tune::dwgn_var, 0, 2, nullptr},
       {"pva_inject", &Tune::pva_inject, -1, 1 << 20, nullptr},
   };

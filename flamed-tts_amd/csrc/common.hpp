@@ -173,7 +173,10 @@ struct Tune {
   int dwgn_small = 1;      // small-M bf16 path: one-workgroup-per-8-channels depthwise conv + GroupNorm (T <= 576)
   int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in
   int persist = 1;         // B = 1 bf16 solves: one persistent launch for all steps (persist.hpp)
-  int split_batch = 1;     // large-M bf16 solves: sub-batch chains as parallel graph branches (den_split; opt-in)
+  int split_batch = 2;     // large-M bf16 solves: sub-batch chains as parallel graph branches (den_split)
+  int split_graph = 0;     // split chains: 0 one graph per chain on its own (priority) stream, 1 one graph with branches
+  int prio_all = 0;       // experiment: every graph-path solve replays on the handle's chain-0 stream of split_prio
+  int split_prio = 2;      // split chains' replay streams (den_chain_streams): 0 caller + highest, 1 all low, 2 all high
   int split_min_rows = 6144;  // ... when every chain still has this many rows
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
@@ -188,7 +191,8 @@ struct Tune {
   int attn_mfma = 1;       // transformer attention (prior stack, timbre encoder) on fp32 MFMA (xfmr.hpp)
   int prior_split = 1;     // bf16 prior decoders: split-K of the GEMMs with small tile grids
   int pva_inject = -1;     // diagnostic: every persistent PVA flow fails at this step (-1 = never)
-  int dwgn_var = 0;        // diagnostic: dwgn kernel variant (1 scalar fp32 math, 2 scalar LDS accesses; T in (384, 448])
+  int dwgn_var = 1;        // dwgn kernel variant: 1 scalar fp32 pair math (default), diagnostics for T in (384, 448]: 0 packed, 2 scalar LDS accesses
+  int coop = 1;            // persistent kernels as cooperative launches (0: plain launches, for profiling runs)
   int stop_after = -1;     // diagnostic: a denoiser evaluation returns after this many kernel-class launches (-1 = never)
 };
 int tune_apply(Tune& t, const char* key, int value);  // kOk or kBadArg (message set)

@@ -740,8 +740,13 @@ static int launch_dwconv_stats(const XT* X, int H, const float* S, int NT, int t
 // chunks are in flight while the current one is convolved.
 constexpr int kDgMaxT = 512;  // frames covered by the register-resident path (NCH <= 8)
 typedef float dg_f2 __attribute__((ext_vector_type(2)));
-// Diagnostic variants (tune dwgn_var, T in (384, 448] only): VAR 1 computes the staging and the conv with scalar
-// fp32 FMAs (no v_pk_*), VAR 2 moves the staged window through LDS with scalar (volatile) accesses.
+// fp32 pair arithmetic.  VAR 1 (the default, every T) does it with scalar fp32 ops kept apart by empty asm
+// barriers: on gfx950 a v_pk_*_f32 that consumes a VGPR pair written by a 64-bit LDS read (ds_read_b64)
+// was measured to return a wrong low dword for one channel parity of one 64-frame chunk when waves of
+// our fp32-MFMA GEMMs were co-resident on the CU (two handles on two streams, tools/conc_dwgn3.py,
+// DESIGN.md "dwgn concurrency").  Diagnostic variants (tune dwgn_var, T in (384, 448] only): VAR 0 is
+// the packed form that showed it, VAR 2 keeps the packed math and moves the staged window through LDS
+// with scalar (volatile) accesses (also clean, 1.3x slower).
 template <int VAR>
 __device__ __forceinline__ dg_f2 dg_fma(dg_f2 a, dg_f2 b, dg_f2 c) {
   if constexpr (VAR == 1) {
@@ -764,7 +769,24 @@ __device__ __forceinline__ dg_f2 dg_lnmod(dg_f2 x, dg_f2 mean, dg_f2 rstd, dg_f2
     return ((x - mean) * rstd) * a + b;
   }
 }
-template <bool AFF, int NCH, typename XT, int VAR = 0>
+template <int VAR>
+__device__ __forceinline__ dg_f2 dg_apply(dg_f2 x, dg_f2 mu, dg_f2 sc, dg_f2 sh) {  // (x - mu) * sc + sh
+  if constexpr (VAR == 1) {
+    float u = x.x - mu.x, v = x.y - mu.y;
+    asm volatile("" : "+v"(u), "+v"(v));
+    float o0 = u * sc.x + sh.x, o1 = v * sc.y + sh.y;
+    asm volatile("" : "+v"(o0), "+v"(o1));
+    return dg_f2{o0, o1};
+  } else {
+    return (x - mu) * sc + sh;
+  }
+}
+__device__ __forceinline__ dg_f2 dg_add1(dg_f2 a, dg_f2 b) {  // scalar pair add (no v_pk_add_f32)
+  float x = a.x + b.x, y = a.y + b.y;
+  asm volatile("" : "+v"(x), "+v"(y));
+  return dg_f2{x, y};
+}
+template <bool AFF, int NCH, typename XT, int VAR = 1>
 __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int H, const float* __restrict__ S, int NT, int tw,
                                                    float eps_ln, ModRef mod, const float* __restrict__ lnw,
                                                    const float* __restrict__ lnb, const float* __restrict__ dww,
@@ -917,7 +939,7 @@ __global__ __launch_bounds__(256) void dwgn_kernel(const XT* __restrict__ X, int
   for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-      const dg_f2 o = (dv[ch][q] - mu) * sc + sh;
+      const dg_f2 o = dg_apply<VAR>(dv[ch][q], mu, sc, sh);
       ob[ch][q] = bf16x2{(bf16)o.x, (bf16)o.y};
     }
   bf16* ap = A + ((size_t)b * T + rg * RPT) * H + c;
@@ -937,7 +959,7 @@ static int launch_dwgn(const XT* X, int H, const float* S, int NT, int tw, ModRe
   const dim3 g(H / 32, B), blk(256);
 #define FL_DWGN(N) hipLaunchKernelGGL((dwgn_kernel<AFF, N, XT>), g, blk, 0, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, A, T)
 #define FL_DWGN_V(N, V) hipLaunchKernelGGL((dwgn_kernel<AFF, N, XT, V>), g, blk, 0, st, X, H, S, NT, tw, 1e-6f, mod, lnw, lnb, dww, dwb, gnw, gnb, A, T)
-  if (tn().dwgn_var == 1 && nch == 7) FL_DWGN_V(7, 1);
+  if (tn().dwgn_var == 0 && nch == 7) FL_DWGN_V(7, 0);
   else if (tn().dwgn_var == 2 && nch == 7) FL_DWGN_V(7, 2);
   else if (nch <= 2) FL_DWGN(2);
   else if (nch <= 4) FL_DWGN(4);
@@ -1063,7 +1085,7 @@ __global__ __launch_bounds__(256) void dwgn_small_kernel(const float* __restrict
   for (int q = 0; q < RPT; ++q) {
     dg_f2 a = bias;
 #pragma unroll
-    for (int j = 0; j < KS; ++j) a = __builtin_elementwise_fma(w[j], win[q + j], a);
+    for (int j = 0; j < KS; ++j) a = dg_fma<1>(w[j], win[q + j], a);  // scalar: see dg_fma
     dv[q] = a;
     if (q < nv) s += a;
   }
@@ -1075,7 +1097,7 @@ __global__ __launch_bounds__(256) void dwgn_small_kernel(const float* __restrict
     }
     if ((tid & 63) < 4) red[slot][tid >> 6][p] = v;
     __syncthreads();
-    return ((red[slot][0][p] + red[slot][1][p]) + red[slot][2][p]) + red[slot][3][p];
+    return dg_add1(dg_add1(dg_add1(red[slot][0][p], red[slot][1][p]), red[slot][2][p]), red[slot][3][p]);
   };
   FL_STAMP(3);
   const float invT = 1.0f / (float)T;
@@ -1660,8 +1682,14 @@ struct Den {
   hipGraphExec_t gexec = nullptr;
   hipStream_t cap_stream = nullptr;
   static constexpr int kMaxSplit = 4;          // sub-batch chains of a large-M solve (den_split)
-  hipStream_t cap_aux[kMaxSplit] = {};         // capture streams of chains 1..S-1
-  hipEvent_t cap_ev[kMaxSplit] = {};           // fork / join events of the chains' capture
+  hipStream_t cap_aux[kMaxSplit] = {};         // (unused since round 5: each chain is captured on cap_stream)
+  hipEvent_t cap_ev[kMaxSplit] = {};           // fork / join events of the chains' replays
+  hipGraphExec_t gexec_c[kMaxSplit] = {};      // graphs of chains 1..S-1 (chain 0's is gexec)
+  hipStream_t run_aux[3][kMaxSplit] = {};      // replay streams of the chains per tune split_prio (den_chain_streams)
+  static constexpr int kMaxParked = 8;
+  hipStream_t parked[kMaxParked] = {};         // streams the queue probe found serialising with a chain's (kept alive)
+  int n_parked = 0, qprobe_retries = 0;
+  int* qprobe = nullptr;                       // probe flag + result words
   int g_B = -1, g_T = -1, g_nfe = -1, g_epoch = -1;
   const void *g_xt = nullptr, *g_mods = nullptr, *g_ws = nullptr;
   int* ctr = nullptr;  // device Euler step counter for graph replay
@@ -1799,17 +1827,14 @@ static size_t den_ws_layout(const Den* d, int B, int T, void* base, DenWs* w) {
 }
 static size_t den_ws_bytes(const Den* d, int B, int T) { return den_ws_layout(d, B, T, nullptr, nullptr); }
 
-// Large-M solves as concurrent sub-batches (tune split_batch, opt-in, default 1): utterances are independent in
-// the denoiser (GroupNorm statistics and the depthwise halo never cross an utterance: prob_generator.py:81-89),
+// Large-M solves as concurrent sub-batches (tune split_batch, default 2): utterances are independent in the
+// denoiser (GroupNorm statistics and the depthwise halo never cross an utterance: prob_generator.py:81-89),
 // so the batch's Euler steps run as S chains of B / S utterances, captured as S parallel branches of one graph.
 // One chain's inter-kernel gaps and the partly filled last round of its GEMM tiles are then covered by the
-// other chain's kernels (B = 64: 336 -> 302 ms).  Opt-in because overlapped chains are NOT bitwise
-// reproducible: with the whole-utterance dwgn kernel on, a velocity evaluation run while another handle's (or
-// chain's) kernels run on a second stream differs from the same evaluation run alone (up to 5e-2 in v, whole
-// utterances; tools/conc_vel2.py), although the chains share no memory (own workspace, counters, step
-// counter) and in-kernel canaries saw neither dwgn's inputs change nor its LDS corrupted; with dwgn = 0 (or
-// the chains captured serially) every run is bitwise equal.  Cause not found.  fp8
-// handles keep one chain (their MX GEMMs need the large tiles of the whole batch).
+// other chain's kernels (B = 64: 336 -> 295 ms, B = 32: 189 -> 159 ms; S = 4: 307 / 189).  The chains are
+// bitwise equal to the single chain (test_cfg2_split_batch_bitwise) since dwgn's pair math is scalar (dg_fma:
+// the packed form was perturbed by co-resident fp32-MFMA waves, DESIGN.md "dwgn concurrency").  fp8 handles
+// keep one chain (their MX GEMMs need the large tiles of the whole batch).
 static int den_split(const Den* d, int B, int T) {
   const Tune& tu = tn();
   const int S = tu.split_batch;
@@ -1827,11 +1852,15 @@ static size_t den_solve_ws(const Den* d, int B, int T) {
   return one > split ? one : split;
 }
 
+static bool stream_capturing(hipStream_t st);
+
 }  // namespace fl
 
 using namespace fl;
 
 extern "C" {
+
+static int den_chain_streams(Den* d, int S, hipStream_t st);
 
 FLAMED_API int flamed_den_create(int C, int H, int n_blocks, int kernel, int spk_dim, int dtype, flamed_den_t* out) {
   FL_REQUIRE(out, "flamed_den_create: null out");
@@ -1860,9 +1889,15 @@ FLAMED_API int flamed_den_destroy(flamed_den_t h) {
     std::lock_guard<std::recursive_mutex> lk(d->mu);
     DeviceGuard dg(d->device);
     retire_graph(d->gexec);
+    for (auto& g : d->gexec_c) retire_graph(g);
     if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
     for (auto& a : d->cap_aux)
       if (a) (void)hipStreamDestroy(a);
+    for (auto& r : d->run_aux)
+      for (auto& a : r)
+        if (a) (void)hipStreamDestroy(a);
+    for (int i = 0; i < d->n_parked; ++i) (void)hipStreamDestroy(d->parked[i]);
+    if (d->qprobe) (void)hipFree(d->qprobe);
     for (auto& e : d->cap_ev)
       if (e) (void)hipEventDestroy(e);
     if (d->ctr) (void)hipFree(d->ctr);
@@ -1911,9 +1946,16 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
   if (d->device >= 0 && d->device != wdev) {  // re-load onto another device: drop the old device's state
     DeviceGuard og(d->device);
     retire_graph(d->gexec);
+    for (auto& g : d->gexec_c) retire_graph(g);
     if (d->cap_stream) { (void)hipStreamDestroy(d->cap_stream); d->cap_stream = nullptr; }
     for (auto& a : d->cap_aux)
       if (a) { (void)hipStreamDestroy(a); a = nullptr; }
+    for (auto& r : d->run_aux)
+      for (auto& a : r)
+        if (a) { (void)hipStreamDestroy(a); a = nullptr; }
+    for (int i = 0; i < d->n_parked; ++i) (void)hipStreamDestroy(d->parked[i]);
+    d->n_parked = 0;
+    if (d->qprobe) { (void)hipFree(d->qprobe); d->qprobe = nullptr; }
     for (auto& e : d->cap_ev)
       if (e) { (void)hipEventDestroy(e); e = nullptr; }
     if (d->ctr) { (void)hipFree(d->ctr); d->ctr = nullptr; }
@@ -2041,7 +2083,16 @@ FLAMED_API int flamed_den_load(flamed_den_t h, const float* const* w, int n, hip
     const int prc = persist_alloc(d, st);
     if (prc) return prc;
   }
+  // the split chains' replay streams now, ahead of any persistent (cooperative) launch of this handle: streams
+  // created after one replayed the chains with little overlap (B = 64: 334-343 vs 298-312 ms when created
+  // before; tools/solve_time.py runs r05t/r05x)
+  if (d->dt == FLAMED_BF16 && !d->f8 && !stream_capturing(st)) {
+    TuneScope ts(den_tune_sync(d));
+    const int crc = den_chain_streams(d, std::max(2, std::min(tn().split_batch, (int)Den::kMaxSplit)), st);
+    if (crc) return crc;
+  }
   retire_graph(d->gexec);
+  for (auto& g : d->gexec_c) retire_graph(g);
   return kOk;
 }
 
@@ -2118,6 +2169,16 @@ FLAMED_API int flamed_den_ws_offsets(flamed_den_t h, int B, int T, size_t* off) 
   den_ws_layout(d, B, T, base, &w);
   const void* p[12] = {w.X, w.S0, w.S1, w.D, w.U, w.GP, w.GNS, w.Y, w.SL, w.A16, w.XA, w.XP};
   for (int i = 0; i < 12; ++i) off[i] = p[i] ? (size_t)((const char*)p[i] - base) : SIZE_MAX;
+  return kOk;
+}
+
+// Diagnostic (include/flamed_diag.h): the split-chain stream probe's record (den_chain_streams).
+FLAMED_API int flamed_den_chain_info(flamed_den_t h, int* parked, int* retries) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && parked && retries, "flamed_den_chain_info: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  *parked = d->n_parked;
+  *retries = d->qprobe_retries;
   return kOk;
 }
 
@@ -2606,6 +2667,79 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
   return flamed_den_solve_part(h, xt, mods, nfe, B, T, ws, ws_bytes, use_graph, 0, nfe, st);
 }
 
+// Hardware-queue probe for two streams: a one-lane kernel on stream a waits (bounded: 2 ms of s_memrealtime)
+// for a flag that a kernel on stream b sets.  If b's launch sits on a's hardware queue it cannot start until
+// a's kernel has timed out, and the pair is reported as serialising.
+__global__ void qprobe_wait_kernel(int* w) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int ok = 0;
+  while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < 200000) {
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = 1; break; }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(w + 1, ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void qprobe_set_kernel(int* w) {
+  if (threadIdx.x == 0) __hip_atomic_store(w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static int streams_concurrent(int* w, hipStream_t a, hipStream_t b, bool* conc) {
+  int h[2] = {0, 0};
+  FL_HIP(hipMemcpy(w, h, sizeof(h), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(qprobe_wait_kernel, dim3(1), dim3(64), 0, a, w);
+  FL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(qprobe_set_kernel, dim3(1), dim3(64), 0, b, w);
+  FL_LAUNCH_CHECK();
+  FL_HIP(hipStreamSynchronize(a));
+  FL_HIP(hipStreamSynchronize(b));
+  FL_HIP(hipMemcpy(h, w, sizeof(h), hipMemcpyDeviceToHost));
+  *conc = h[1] == 1;
+  return kOk;
+}
+
+// Replay streams of the split chains (tune split_prio).  HIP maps each stream to one of GPU_MAX_HW_QUEUES (4)
+// hardware queues by current use, so two normal-priority streams -- or a graph's own branch streams -- can
+// share the launch stream's queue and serialise the chains: the round-4 single graph with parallel branches
+// (split_graph 1) measured 295-322 ms at B = 64 on some process histories and 341-348 ms on others (e.g. with
+// its streams created after a cooperative launch; tools/coop_stream_probe.py shows stream pairs that
+// serialise).  Priority streams come from queues of their own (probe: every high / low pair concurrent), so
+// the chains replay on them.  split_prio 0: chain 0 on the caller's stream, chain 1 at the highest priority
+// (chains 2 / 3 low / normal); 1: every chain on a low-priority stream of its own; 2: every chain on a
+// high-priority stream.
+static int den_chain_streams(Den* d, int S, hipStream_t st) {
+  const int pm = tn().split_prio;
+  int plo = 0, phi = 0;
+  FL_HIP(hipDeviceGetStreamPriorityRange(&plo, &phi));
+  const int k0 = pm == 0 && !tn().prio_all ? 1 : 0;
+  for (int k = k0; k < S; ++k) {  // (S = 1: chain 0's stream only)
+    if (d->run_aux[pm][k]) continue;
+    const int pr = pm == 1 ? plo : pm == 2 ? phi : (k == 1 ? phi : k == 2 ? plo : 0);
+    // a new stream that serialises with an earlier chain's is parked (kept alive, so its hardware queue stays
+    // counted as used) and another one is created; the probe needs host syncs, so it is skipped inside a capture
+    const bool probe = k > k0 && !stream_capturing(st);
+    if (probe && !d->qprobe) FL_HIP(hipMalloc(&d->qprobe, 64));
+    for (int tries = 0;; ++tries) {
+      hipStream_t sk = nullptr;
+      FL_HIP(hipStreamCreateWithPriority(&sk, hipStreamNonBlocking, pr));
+      bool ok = true;
+      for (int j = k0; probe && ok && j < k; ++j) {
+        bool c1 = false, c2 = false;
+        const int rc1 = streams_concurrent(d->qprobe, d->run_aux[pm][j], sk, &c1);
+        const int rc2 = rc1 ? rc1 : streams_concurrent(d->qprobe, sk, d->run_aux[pm][j], &c2);
+        if (rc2) { (void)hipStreamDestroy(sk); return rc2; }
+        ok = c1 && c2;
+      }
+      if (ok || tries >= Den::kMaxParked || d->n_parked >= Den::kMaxParked) {
+        d->run_aux[pm][k] = sk;
+        d->qprobe_retries += tries;
+        break;
+      }
+      d->parked[d->n_parked++] = sk;
+    }
+  }
+  return kOk;
+}
+
 FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                      size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t st) {
   Den* d = reinterpret_cast<Den*>(h);
@@ -2665,6 +2799,7 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
   // state ping-pongs between xt (even steps) and the workspace's XP (odd steps), so G must be even
   const bool fused = S == 1 && den_fused_ok(d, B, T) && G % 2 == 0;
   const bool fbig = !fused && den_fused_big(d, Bk, T);  // large M: in-place fused steps, per chain
+  const bool br = S > 1 && tn().split_graph == 1;
   DenWs w;
   den_ws_layout(d, B, T, ws, &w);
   // the graph bakes in dt = 1/nfe, so nfe is part of the key
@@ -2672,37 +2807,58 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
                    d->g_epoch == d->tune_ver;
   if (!hit) {
     retire_graph(d->gexec);
+    for (auto& g : d->gexec_c) retire_graph(g);
     if (!d->cap_stream) FL_HIP(hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking));
-    for (int k = 1; k < S; ++k)
-      if (!d->cap_aux[k]) FL_HIP(hipStreamCreateWithFlags(&d->cap_aux[k], hipStreamNonBlocking));
+    if (S > 1 && !br) {
+      const int rc = den_chain_streams(d, S, st);
+      if (rc) return rc;
+    }
     for (int k = 0; k < Den::kMaxSplit; ++k)
       if (!d->cap_ev[k]) FL_HIP(hipEventCreateWithFlags(&d->cap_ev[k], hipEventDisableTiming));
-    FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
-    int rc = kOk;
-    if (S > 1) {  // fork: chains 1..S-1 on their own capture streams
+    if (br) {  // tune split_graph 1 (round 4): one graph, the chains as parallel branches (fork / join events)
+      for (int k = 1; k < S; ++k)
+        if (!d->cap_aux[k]) FL_HIP(hipStreamCreateWithFlags(&d->cap_aux[k], hipStreamNonBlocking));
+      FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
       FL_HIP(hipEventRecord(d->cap_ev[0], d->cap_stream));
       for (int k = 1; k < S; ++k) FL_HIP(hipStreamWaitEvent(d->cap_aux[k], d->cap_ev[0], 0));
+      int rc = kOk;
+      for (int k = 0; k < S && rc == kOk; ++k) {
+        float* xk; const float* mk; void* wk;
+        sub(k, xk, mk, wk);
+        hipStream_t cs = k == 0 ? d->cap_stream : d->cap_aux[k];
+        for (int s = 0; s < G && rc == kOk; ++s) rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, fbig ? xk : nullptr, B, k, S);
+      }
+      for (int k = 1; k < S && rc == kOk; ++k) {
+        FL_HIP(hipEventRecord(d->cap_ev[k], d->cap_aux[k]));
+        FL_HIP(hipStreamWaitEvent(d->cap_stream, d->cap_ev[k], 0));
+      }
+      hipGraph_t g = nullptr;
+      hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+      if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+      FL_HIP(e);
+      hipError_t ie = hipGraphInstantiate(&d->gexec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      FL_HIP(ie);
     }
-    for (int k = 0; k < S && rc == kOk; ++k) {
+    // one graph per chain (G steps of its sub-batch), captured one after another on cap_stream
+    for (int k = 0; k < (br ? 0 : S); ++k) {
+      FL_HIP(hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed));
+      int rc = kOk;
       float* xk; const float* mk; void* wk;
       sub(k, xk, mk, wk);
-      hipStream_t cs = k == 0 ? d->cap_stream : d->cap_aux[k];
       for (int s = 0; s < G && rc == kOk; ++s) {
-        if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, cs, d->ctr, s % 2 ? xt : w.XP);
-        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, cs, d->ctr + 16 * k, fbig ? xk : nullptr, B, k, S);
+        if (fused) rc = den_step(d, s % 2 ? w.XP : xt, mods, T, B, T, dt, nullptr, ws, d->cap_stream, d->ctr, s % 2 ? xt : w.XP);
+        else rc = den_step(d, xk, mk, T, Bk, T, dt, nullptr, wk, d->cap_stream, d->ctr + 16 * k, fbig ? xk : nullptr, B, k, S);
       }
+      hipGraph_t g = nullptr;
+      hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
+      if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+      FL_HIP(e);
+      hipGraphExec_t& ex = k == 0 ? d->gexec : d->gexec_c[k];
+      hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      FL_HIP(ie);
     }
-    for (int k = 1; k < S && rc == kOk; ++k) {  // join
-      FL_HIP(hipEventRecord(d->cap_ev[k], d->cap_aux[k]));
-      FL_HIP(hipStreamWaitEvent(d->cap_stream, d->cap_ev[k], 0));
-    }
-    hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(d->cap_stream, &g);
-    if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
-    FL_HIP(e);
-    hipError_t ie = hipGraphInstantiate(&d->gexec, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    FL_HIP(ie);
     d->g_B = B; d->g_T = T; d->g_nfe = nfe; d->g_epoch = d->tune_ver; d->g_xt = xt; d->g_mods = mods; d->g_ws = ws;
   }
   const size_t n = (size_t)B * T * d->C;
@@ -2726,8 +2882,31 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
       FL_HIP(hipMemsetAsync(d->ctr, 0, 256, st));  // the step counters of every chain (16 ints apart)
     }
   }
-  for (int r = s0 / G; r < s1 / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
+  if ((S > 1 && !br) || tn().prio_all) {  // fork: every chain replays its graph for the whole range on its stream, then join
+    const int NG = br ? 1 : S;  // graphs to replay
+    if (NG == 1) {
+      const int rc = den_chain_streams(d, 1, st);  // (prio_all: the single graph on a chain stream too)
+      if (rc) return rc;
+    }
+    const int pm = tn().split_prio;
+    const bool own0 = pm != 0 || tn().prio_all;  // chain 0 off the caller's stream
+    FL_HIP(hipEventRecord(d->cap_ev[0], st));
+    for (int k = 0; k < NG; ++k) {
+      hipStream_t cs = (k == 0 && !own0) ? st : d->run_aux[pm][k];
+      if (cs != st) FL_HIP(hipStreamWaitEvent(cs, d->cap_ev[0], 0));
+      for (int r = s0 / G; r < s1 / G; ++r) FL_HIP(hipGraphLaunch(k == 0 ? d->gexec : d->gexec_c[k], cs));
+    }
+    for (int k = 0; k < NG; ++k) {
+      hipStream_t cs = (k == 0 && !own0) ? st : d->run_aux[pm][k];
+      if (cs == st) continue;
+      FL_HIP(hipEventRecord(d->cap_ev[1 + k % (Den::kMaxSplit - 1)], cs));  // (S <= kMaxSplit: k < 3 or pm == 0)
+      FL_HIP(hipStreamWaitEvent(st, d->cap_ev[1 + k % (Den::kMaxSplit - 1)], 0));
+    }
+  } else {
+    for (int r = s0 / G; r < s1 / G; ++r) FL_HIP(hipGraphLaunch(d->gexec, st));
+  }
   note_graph_use(d->gexec, st);
+  for (int k = 1; k < (br ? 1 : S); ++k) note_graph_use(d->gexec_c[k], st);  // st has joined chain k's replays
   if (fused && s1 == nfe) {  // the last step's combine + Euler update: x_nfe = XP + dt * v (nfe even: XP holds x_{nfe-1})
     hipLaunchKernelGGL(conv3_combine_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w.Y, d->bout, xt, nullptr, B * T, T,
                        d->C, dt, nullptr, w.XP);

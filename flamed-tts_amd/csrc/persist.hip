@@ -308,6 +308,74 @@ __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* 
   }
 }
 
+// Several chunks (NTW > 1): every tile of the wave (wave + 4 i) in one pass, the A fragments streamed in half-tile
+// units (K / 2 deep) through a two-unit register ring, so the next unit's loads are in flight during this unit's
+// MFMAs (and no epilogue stores sit in the wave's vmcnt queue between them: the epilogues run after the pass).
+// Per tile the K-steps accumulate in the same order as gemm(): bitwise the same products.
+template <int K, int NTW>
+__device__ __forceinline__ void gemm_multi(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[NTW][2], int wave,
+                                           int lane_in, unsigned long long* stamp, int g, bool frag) {
+  constexpr int KST = K / 32, KU = KST / 2, U = 2 * NTW;
+  static_assert(KST % 2 == 0, "half-tile units");
+  const int lane = opq(lane_in);
+  const int ntile = (nr + 15) >> 4;
+  const int c = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rs = frag ? rsrc(reinterpret_cast<const char*>(A) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST))
+                                         : rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
+  u32x4 a[2][KU];
+  auto load = [&](u32x4 (&dst)[KU], int u) __attribute__((always_inline)) {
+    const int tile = wave + 4 * (u >> 1), k0 = (u & 1) * KU;
+    if (tile >= ntile) return;
+    if (frag) {
+      const unsigned base = (unsigned)(((tile * KST + k0) * 64 + lane) * 16);
+#pragma unroll
+      for (int ks = 0; ks < KU; ++ks) dst[ks] = ld16(rs, base + ks * 1024);
+    } else {
+      const unsigned base = (unsigned)(((16 * tile + c) * K + k0 * 32 + q * 8) * 2);
+#pragma unroll
+      for (int ks = 0; ks < KU; ++ks) dst[ks] = ld16(rs, base + ks * 64);
+    }
+  };
+  load(a[0], 0);
+  if (wave < ntile) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KU) : "memory");  // this wave's (older) weight DMA landed
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's DMA: the whole panel is in LDS
+  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // FL_STAMPS timeline only
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int tile = wave + 4 * (u >> 1), k0 = (u & 1) * KU;
+    const bool next = u + 1 < U && wave + 4 * ((u + 1) >> 1) < ntile;
+    if (u + 1 < U) load(a[(u + 1) & 1], u + 1);
+    if (next) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(KU) : "memory");  // this unit's loads (older) have landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    f32x4(&ac)[2] = acc[u >> 1];
+    if (k0 == 0) {
+      ac[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ac[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (tile < ntile) {
+      constexpr int kBP = 4;
+      u32x4 b0[kBP], b1[kBP];
+#pragma unroll
+      for (int p = 0; p < kBP; ++p) {
+        b0[p] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (k0 + p) + q));
+        b1[p] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (k0 + p) + q));
+      }
+#pragma unroll
+      for (int ks = 0; ks < KU; ++ks) {
+        const u32x4 x0 = b0[ks % kBP], x1 = b1[ks % kBP];
+        if (ks + kBP < KU) {
+          b0[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (k0 + ks + kBP) + q));
+          b1[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (k0 + ks + kBP) + q));
+        }
+        const u32x4 av = a[u & 1][ks];
+        ac[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, x0), ac[0], 0, 0, 0);
+        ac[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, x1), ac[1], 0, 0, 0);
+      }
+    }
+  }
+}
+
 // The same product with the work split 2 x 2 (persist_opt 1024): wave w = (pair p, half h) multiplies row tiles
 // 2p and 2p + 1 by K-steps [h KST/2, (h + 1) KST/2), so each B fragment read from LDS feeds two row tiles and
 // the panel is read twice per workgroup instead of four times; the two halves of tile w are then summed
@@ -454,13 +522,16 @@ __device__ __forceinline__ void stage_tile(char* stg, const float (&v)[2][4], in
   }
 }
 // ... then write it through with 16-B sc1 stores (rows [ra, rb) of the tile) into dst (row stride ld).
+// Each wave writes the rows it staged itself ([16 w, 16 w + 16) of the chunk), so a stage -> flush pair needs no
+// workgroup barrier (persist_opt 32768: the wave's own LDS writes are ordered before its reads).
 template <typename OT>
 __device__ __forceinline__ void flush_tile(const char* stg, OT* dst, int ld, int r0, int ra, int rb, int col0, int T,
                                            bool local = false) {
   constexpr int CPR = kCols * (int)sizeof(OT) / 16;  // 16-B chunks per staged row
   const __amdgpu_buffer_rsrc_t rs = rsrc(dst, (unsigned)T * ld * (unsigned)sizeof(OT));
-  for (int idx = opq(threadIdx.x); idx < kChunk * CPR; idx += kThreads) {
-    const int row = idx / CPR, ch = idx % CPR;
+  const int w16 = 16 * (threadIdx.x >> 6);
+  for (int it = opq(threadIdx.x & 63); it < 16 * CPR; it += 64) {
+    const int row = w16 + it / CPR, ch = it % CPR;
     if (row < ra || row >= rb) continue;
     const u32x4 v = *reinterpret_cast<const u32x4*>(stg + (row * kCols * sizeof(OT)) + ch * 16);
     const unsigned off = (unsigned)(((size_t)(r0 + row) * ld + col0) * sizeof(OT) + ch * 16);
@@ -632,6 +703,14 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
     }
   };
+  // Staged hand-off rows are written and flushed by the same wave (stage_tile / GroupNorm apply rows 16 w .. 16 w + 15,
+  // flush_frag / flush_tile / publish_xs by wave): persist_opt 32768 orders them with the wave's own LDS wait instead
+  // of a workgroup barrier.
+  const bool wlocal = (P.opt & 32768) != 0;
+  auto stage_sync = [&]() {
+    if (wlocal) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else __syncthreads();
+  };
   // weights of the first GEMM (proj_in) while the state is published
   dma_panel<kC>(smem, [&](int n) { return P.win + (size_t)(col0 + n) * kC; }, wave, lane, P.opt);
   // bf16 rows of x (proj_in's operand): 16 B per tile row, staged in LDS
@@ -640,25 +719,27 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
       const int nrc = crows(i);
-      if (i > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+      if (i > 0) stage_sync();  // the previous chunk's rows have left the staging tile
       t[xr_row * kCh + 2 * (tid & 3)] = (bf16)xs0[i];
       t[xr_row * kCh + 2 * (tid & 3) + 1] = (bf16)xs1[i];
-      __syncthreads();
+      stage_sync();
+      // each wave writes the 16 rows it staged (lanes 0..15: one row of 16 B each)
+      const int prow = 16 * wave + lane;
       if (frag) {  // channels 8 s .. 8 s + 7 = K-step s / 4, quarter s % 4 of proj_in's fragments
-        if (tid < 16 * ((nrc + 15) >> 4)) {
+        if (lane < 16 && 16 * wave < nrc) {
           const __amdgpu_buffer_rsrc_t rs =
               rsrc(reinterpret_cast<char*>(P.xs) + (size_t)g * frag_group_bytes(kC / 32), frag_group_bytes(kC / 32));
-          const int tt = 4 * i + (tid >> 4), ln = (tid & 15) + 16 * (s & 3);
-          const u32x4 v = tid < nrc ? *reinterpret_cast<const u32x4*>(stg + tid * 16) : u32x4{0u, 0u, 0u, 0u};
+          const int tt = 4 * i + wave, ln = lane + 16 * (s & 3);
+          const u32x4 v = prow < nrc ? *reinterpret_cast<const u32x4*>(stg + prow * 16) : u32x4{0u, 0u, 0u, 0u};
           const unsigned off = (unsigned)(((tt * (kC / 32) + (s >> 2)) * 64 + ln) * 16);
           if (xloc) st16p(rs, off, v);
           else st16(rs, off, v);
         }
-      } else if (tid < nrc) {
+      } else if (lane < 16 && prow < nrc) {
         const __amdgpu_buffer_rsrc_t rs = rsrc(P.xs, (unsigned)TT * kC * 2);
-        const unsigned off = (unsigned)(((size_t)(r0 + kChunk * i + tid) * kC + kCh * s) * 2);
-        if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
-        else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + tid * 16));
+        const unsigned off = (unsigned)(((size_t)(r0 + kChunk * i + prow) * kC + kCh * s) * 2);
+        if (xloc) st16p(rs, off, *reinterpret_cast<const u32x4*>(stg + prow * 16));
+        else st16(rs, off, *reinterpret_cast<const u32x4*>(stg + prow * 16));
       }
     }
     seal_put();
@@ -709,7 +790,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   publish_xs();
 
   float X[NTW][2][4];  // residual stream tiles (this wave's tiles wave + 4 i: 16 rows x 32 columns each), MFMA layout
-  f32x4 acc[2];
 
   for (int step = P.s0; step < P.s1; ++step) {
     const float* md = P.mods + (size_t)(step * P.B + utt) * P.MS;  // this utterance's modulation row
@@ -727,21 +807,24 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     PST(step);
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
+    f32x4 accm[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
+    if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
+    else if constexpr (NTW == 1) gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
+    else gemm_multi<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
+    PST(step);
 #pragma unroll
     for (int ci = 0; ci < NTW; ++ci) {
       const int tl = wave + 4 * ci;
-      if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-      else gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
-      if (ci == 0) PST(step);
+      const f32x4(&acc)[2] = accm[ci];
       acc_to(X[ci], acc);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) X[ci][nt][i] += binv[nt];
       if (16 * tl < nr) store_partials(P.xpart[0], X[ci], r0, nr, s, tl, lane);
-      if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+      if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
       stage_tile<float>(stg, X[ci], wave, lane);
-      __syncthreads();
+      stage_sync();
       flush_halo(stg, P.ximg, r0, nr, col0, TT, kChunk * ci, crows(ci));
     }
     seal_put();
@@ -980,10 +1063,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         bf16* t = reinterpret_cast<bf16*>(stg);
 #pragma unroll
         for (int ci = 0; ci < NTW; ++ci) {
-          if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+          if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
 #pragma unroll
           for (int k = 0; k < 8; ++k) t[(8 * rg + k) * kCols + cc] = (bf16)((d[ci][k] - gv.x) * gv.y + gv.z);
-          __syncthreads();
+          stage_sync();
           if (frag) flush_frag(stg, P.a2, g, s, crows(ci), kH / 32, xloc, 4 * ci);
           else flush_tile<bf16>(stg, P.a2, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
         }
@@ -998,21 +1081,24 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
+      f32x4 accm_c2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
+      if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
+      else if constexpr (NTW == 1) gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
+      else gemm_multi<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
+      PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
         const int tl = wave + 4 * ci;
-        if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-        else gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
-        if (ci == 0) PST(step);
+        const f32x4(&acc)[2] = accm_c2[ci];
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b2v[nt]);
         }
-        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
         stage_tile<bf16>(stg, v, wave, lane);
-        __syncthreads();
+        stage_sync();
         if (frag) flush_frag(stg, P.u, g, s, crows(ci), kH / 32, xloc, 4 * ci);
         else flush_tile<bf16>(stg, P.u, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
       }
@@ -1040,12 +1126,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
+      f32x4 accm_c3[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
+      if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
+      else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
+      else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
+      PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
         const int tl = wave + 4 * ci;
-        if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-        else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
-        if (ci == 0) PST(step);
+        const f32x4(&acc)[2] = accm_c3[ci];
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
@@ -1059,9 +1148,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           }
         }
         if (16 * tl < nr) store_partials(P.xpart[1], X[ci], r0, nr, s, tl, lane, xloc);
-        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
         stage_tile<bf16>(stg, v, wave, lane);
-        __syncthreads();
+        stage_sync();
         if (frag) flush_frag(stg, P.xa, g, s, crows(ci), kH / 32, xloc, 4 * ci);
         else flush_tile<bf16>(stg, P.xa, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
       }
@@ -1086,12 +1175,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
       row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
+      f32x4 accm_m0[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
+      if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
+      else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
+      else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);  // (the first tile's barrier orders the statistics)
+      PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
         const int tl = wave + 4 * ci;
-        if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-        else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);  // (the first tile's barrier orders the statistics)
-        if (ci == 0) PST(step);
+        const f32x4(&acc)[2] = accm_m0[ci];
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
@@ -1101,9 +1193,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
             v[nt][i] = silu(st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa0[nt]) + fb0[nt]);
           }
         }
-        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
         stage_tile<bf16>(stg, v, wave, lane);
-        __syncthreads();
+        stage_sync();
         if (frag) flush_frag(stg, P.u, g, s, crows(ci), kH / 32, xloc, 4 * ci);
         else flush_tile<bf16>(stg, P.u, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
       }
@@ -1123,20 +1215,23 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
+      f32x4 accm_m2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
+      if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
+      else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
+      else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
+      PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
         const int tl = wave + 4 * ci;
-        if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, PSTP(step), g, frag);
-        else gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), acc, wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag, tl, ci == 0);
-        if (ci == 0) PST(step);
+        const f32x4(&acc)[2] = accm_m2[ci];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
           for (int i = 0; i < 4; ++i) X[ci][nt][i] = X[ci][nt][i] + g2v[nt] * (acc[nt][i] + bm2[nt]);
         if (16 * tl < nr) store_partials(P.xpart[0], X[ci], r0, nr, s, tl, lane);
-        if (ci > 0) __syncthreads();  // the previous chunk's rows have left the staging tile
+        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
         stage_tile<float>(stg, X[ci], wave, lane);
-        __syncthreads();
+        stage_sync();
         flush_halo(stg, P.ximg, r0, nr, col0, TT, kChunk * ci, crows(ci));
       }
       seal_put();
@@ -1170,12 +1265,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     PST(step);
     row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
     f32x4 acco[NTW][2];  // every tile's products first: with several chunks Y goes into this phase's panel buffer
-#pragma unroll
-    for (int ci = 0; ci < NTW; ++ci) {
-      if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[ci], wave, lane, PSTP(step), g, frag);
-      else gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[ci], wave, lane, ci == 0 ? PSTP(step) : nullptr, g, frag,
-                    wave + 4 * ci, ci == 0);
-    }
+    if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
+    else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
+    else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
     PST(step);
     // Y of the group: [row][24] fp32 (tap-major x 8 channels) -- in the staging tile (one chunk), or in the
     // panel conv_out has just finished reading (several chunks: 320 x 24 x 4 B; the next panel DMA goes to the
@@ -1314,7 +1406,9 @@ int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
     return kBadArg;
   }
   const void* kern = persist_kernels()[(P.opt & 1024) ? 0 : P.ntw];
-  const hipError_t e = cooperative ? hipLaunchCooperativeKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st)
+  // tune coop 0: plain launch (profiling: rocprofv3's teardown faults after cooperative launches, README);
+  // residency was checked by persist_eligible either way
+  const hipError_t e = cooperative && tn().coop ? hipLaunchCooperativeKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st)
                                    : hipLaunchKernel(kern, dim3(kWGs), dim3(kThreads), args, kLds, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();

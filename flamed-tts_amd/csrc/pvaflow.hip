@@ -514,7 +514,9 @@ int pva_persist_launch(const Params& Pin, hipStream_t st) {
   // cooperative launch replays cooperatively
   void* args[] = {&P};
   const void* kern = reinterpret_cast<const void*>(pva_persist_kernel<192, 384>);
-  const hipError_t e = hipLaunchCooperativeKernel(kern, dim3(P.grid), dim3(kThreads), args, Lds<192, 384>::BYTES, st);
+  // tune coop 0: plain launch (profiling, README "Known issues"); residency checked by pva_persist_eligible
+  const hipError_t e = tn().coop ? hipLaunchCooperativeKernel(kern, dim3(P.grid), dim3(kThreads), args, Lds<192, 384>::BYTES, st)
+                                 : hipLaunchKernel(kern, dim3(P.grid), dim3(kThreads), args, Lds<192, 384>::BYTES, st);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     set_error("persistent PVA flow: hipLaunchCooperativeKernel -> %s", hipGetErrorString(e));

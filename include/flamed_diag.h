@@ -65,6 +65,9 @@ FLAMED_API int flamed_den_ws_offsets(flamed_den_t h, int B, int T, size_t* off);
  * completes the launch of `ticket` (a fetch_add result), and whether counter value `cur` has reached it
  * (wrap-safe across 2^32). */
 FLAMED_API int flamed_persist_ticket(unsigned ticket, unsigned cur, unsigned* target, int* reached);
+/* Split-chain replay streams of this handle: how many the hardware-queue probe parked (they serialised with an
+ * earlier chain's stream) and how many re-creations it took in total. */
+FLAMED_API int flamed_den_chain_info(flamed_den_t h, int* parked, int* retries);
 
 #ifdef __cplusplus
 }

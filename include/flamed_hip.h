@@ -184,12 +184,20 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "persist_opt"   — persistent kernel variant bits (diagnostic A/B; default 585);
  *   "persist_inject"— diagnostic: every persistent launch fails at this step (-1 default = never), to
  *                     exercise the NaN poisoning / failure count / retry budget;
- *   "persist_multi" — 1 (default): B = 2 / 4 / 8 equal-length utterances with at most 64 frames per row
- *                     group (T <= 512 / B) also run as one persistent launch; 0: B = 1 only;
+ *   "persist_multi" — 1 (default): B = 2 / 4 / 8 equal-length utterances also run as one persistent
+ *                     launch (rows per group <= 64 x persist_ntw: B x T <= 2560); 0: B = 1 only;
+ *   "persist_ntw"   — 64-frame chunks per persistent row group, 1..5 (default 5: T <= 2560 at B = 1);
  *   "persist_capmode" — persistent launch inside a stream capture: 0 (default) cooperative node, 1 plain;
+ *   "coop"          — 1 (default): the persistent denoiser solve and PVA flow are cooperative launches;
+ *                     0: plain launches after the same residency check (profiling runs: rocprofv3's
+ *                     teardown faults after a cooperative launch, README "Known issues");
  *   "split_batch"   — large-M bf16 solves as this many concurrent sub-batch chains (parallel graph
- *                     branches; 1 = default, off: overlapped chains are not bitwise reproducible);
+ *                     branches; default 2, bitwise equal to 1 = one chain);
  *   "split_min_rows"— ... only when every chain keeps at least this many rows (default 6144);
+ *   "split_graph"   — 0 (default): one graph per chain, chains 1.. replayed on priority streams of their
+ *                     own; 1: one graph with the chains as parallel branches (round 4);
+ *   "split_prio"    — split chains' replay streams: 0 (default) chain 0 on the caller's stream, chain 1
+ *                     on a highest-priority stream; 1 every chain on a low-priority stream; 2 all high;
  *   "pva_split"     — 1: the PVA nets' small-M exact-fp32 GEMMs split K over workgroups
  *                     (per-handle slabs, fixed slice order: deterministic); 0 (default: measured
  *                     no faster): one K chain;

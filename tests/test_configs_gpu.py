@@ -14,6 +14,8 @@ prob_generator.py:434-447; SURVEY.md §8(c) tolerances, stated at 128 steps):
 The measured errors are printed (pytest -s) so the tolerances can be checked against them.
 """
 import numpy as np
+import os
+
 import pytest
 import torch
 
@@ -30,6 +32,7 @@ C = 256
 BF16_VEL = 8e-3
 BF16_SOLVE = 6e-3   # SURVEY.md §8(c) allows 2e-2 at 128 / 256 steps; measured 2.1e-3 .. 2.9e-3 (r02)
 F32_SOLVE = 1e-4
+SPLIT_DEFAULT = 2   # flamed_tune split_batch default (csrc/common.hpp Tune::split_batch)
 
 
 @pytest.fixture(scope="module")
@@ -147,20 +150,23 @@ def test_cfg2_solve_128(pg_bf16, cfg2):
 
 
 def test_cfg2_split_batch_within_bf16_bar(pg_bf16, cfg2):
-    """Opt-in split_batch 2 (two sub-batch chains as parallel graph branches, denoiser.hip den_split): the
-    chains overlap on the device and are not bitwise reproducible, so the opt-in path is
-    held to the bf16 bars instead: against the single-chain solve (same bf16 operands) at the persistent-vs-
-    launch bar, and utterances 0 / 63 (one per chain) against the oracle at the solve bar."""
+    """split_batch 2 (the default: two sub-batch chains as parallel graph branches, denoiser.hip den_split)
+    against the single-chain solve at the persistent-vs-launch bar, and utterances 0 / 63 (one per chain)
+    against the oracle at the solve bar (test_cfg2_split_batch_bitwise holds it to bitwise at 32 steps)."""
     from flamed import _native as nat
     pg, sd = pg_bf16
     x0, spk = cfg2
-    base = _solve(pg, x0, spk, 128)
     L = nat.lib()
+    nat.check(L.flamed_tune(b"split_batch", 1), "flamed_tune")
+    try:
+        base = _solve(pg, x0, spk, 128)
+    finally:
+        nat.check(L.flamed_tune(b"split_batch", SPLIT_DEFAULT), "flamed_tune")
     nat.check(L.flamed_tune(b"split_batch", 2), "flamed_tune")
     try:
         sp = _solve(pg, x0, spk, 128)
     finally:
-        nat.check(L.flamed_tune(b"split_batch", 1), "flamed_tune")
+        nat.check(L.flamed_tune(b"split_batch", SPLIT_DEFAULT), "flamed_tune")
     assert torch.isfinite(sp).all()
     e = rel_l2(sp, base)
     print(f"configs[2] split_batch 2 vs 1 rel-L2 {e:.3e}")
@@ -218,12 +224,24 @@ def _partial_solve(pg, x0, spk, nfe, steps):
 
 
 def test_cfg4_solve_256_graph_equals_eager(pg_bf16, cfg4):
+    """configs[4] B = 1 T = 2400: the graph of launches equals the eager launches bitwise; the default path (since
+    round 5 one persistent launch, five 64-frame chunks per row group) is held to the persistent-vs-launch bar."""
+    from flamed import _native as nat
     pg, _ = pg_bf16
     x0, spk = cfg4
-    a = _solve(pg, x0, spk, 256)
+    L = nat.lib()
+    nat.check(L.flamed_tune(b"persist", 0), "flamed_tune")
+    try:
+        a = _solve(pg, x0, spk, 256)
+    finally:
+        nat.check(L.flamed_tune(b"persist", 1), "flamed_tune")
     e = _solve(pg, x0, spk, 256, graph=False)
-    assert torch.isfinite(a).all()
+    p = _solve(pg, x0, spk, 256)
+    assert torch.isfinite(a).all() and torch.isfinite(p).all()
     assert torch.equal(a, e)
+    err = rel_l2(p, a)
+    print(f"configs[4] persistent vs graph of launches rel-L2 {err:.3e}")
+    assert err < 4e-3
 
 
 @pytest.mark.parametrize("x16", [0, 1])
@@ -267,3 +285,67 @@ def test_cfg4_bf16_solve_256_vs_oracle(pg_bf16, cfg4):
     print(f"configs[4] bf16 B=1 T=2400 256-step rel-L2 {e:.3e}, max|d| {amax:.3e} (|ref|max {float(ref.abs().max()):.2f})")
     assert torch.isfinite(out).all()
     assert e < BF16_SOLVE and amax < 0.1
+
+
+def test_concurrent_handles_bitwise(pg_bf16):
+    """a large-M velocity evaluation (B = 32, T = 400: the whole-utterance depthwise conv +
+    GroupNorm kernel) gives the same bits whether it runs alone or while another handle's work runs on a second
+    stream -- that handle's AdaLN GEMMs (the strongest trigger of the round-4 perturbation: co-resident fp32-MFMA
+    waves corrupted the low lane of dwgn's 64-bit-LDS-fed packed-fp32 FMAs) or its full velocity."""
+    from flamed import _native as nat
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
+    pg, _ = pg_bf16
+    hA = pg.denoiser.hip()
+    hB = DenoiserHIP(pg.denoiser, "bf16")  # a second native handle (own workspace) over the same weights
+    # negative control (FLAMED_TEST_DWGN_VAR=0: the packed dwgn conv of rounds 1-4) -- this test then fails
+    var = int(os.environ.get("FLAMED_TEST_DWGN_VAR", "1"))
+    nat.check(nat.lib().flamed_tune(b"dwgn_var", var), "flamed_tune")
+    B, T = 32, 400
+    g = torch.Generator().manual_seed(77)
+    xa, xb = (torch.randn(B, T, C, generator=g).to(DEV) for _ in range(2))
+    ca, cb = (torch.randn(B, C, generator=g).to(DEV) for _ in range(2))
+    t = torch.full((B, 1), 0.3, device=DEV)
+    r = torch.arange(B, device=DEV, dtype=torch.int32)
+    tv = torch.full((B,), 0.3, device=DEV)
+    with torch.inference_mode():
+        solo = hA.velocity(xa, t, ca).clone()
+        hB.velocity(xb, t, cb)
+        torch.cuda.synchronize()
+        bad = 0
+        for mode in ("adaln", "velocity"):
+            for rep in range(6):
+                sA, sB = torch.cuda.Stream(), torch.cuda.Stream()
+                torch.cuda.synchronize()
+                with torch.cuda.stream(sB):
+                    if mode == "adaln":
+                        for _ in range(40):
+                            hB.adaln(tv, cb, r, r)
+                    else:
+                        for _ in range(2):
+                            hB.velocity(xb, t, cb)
+                with torch.cuda.stream(sA):
+                    torch.cuda._sleep(15000 * rep)
+                    got = hA.velocity(xa, t, ca)
+                torch.cuda.synchronize()
+                bad += int(not torch.equal(got, solo))
+    nat.check(nat.lib().flamed_tune(b"dwgn_var", 1), "flamed_tune")
+    assert bad == 0, f"{bad} of 12 overlapped evaluations differ from the solo one"
+
+
+def test_cfg2_split_batch_bitwise(pg_bf16, cfg2):
+    """With the dwgn fix, two concurrent sub-batch chains (split_batch 2: parallel graph branches) give exactly the
+    single-chain solve (each utterance's arithmetic is independent of the batch split, and concurrency no longer
+    perturbs a kernel)."""
+    from flamed import _native as nat
+    pg, _ = pg_bf16
+    x0, spk = cfg2
+    L = nat.lib()
+    nat.check(L.flamed_tune(b"split_batch", 1), "flamed_tune")
+    one = _solve(pg, x0, spk, 32)
+    nat.check(L.flamed_tune(b"split_batch", 2), "flamed_tune")
+    try:
+        two = _solve(pg, x0, spk, 32)
+        again = _solve(pg, x0, spk, 32)
+    finally:
+        nat.check(L.flamed_tune(b"split_batch", SPLIT_DEFAULT), "flamed_tune")
+    assert torch.equal(two, again) and torch.equal(two, one)

@@ -55,6 +55,8 @@ def _solve(pg, x0, spk, nfe):
 
 
 def _runs(pg):
+    if pg.denoiser.hip().handle is None:  # no solve on this module yet (e.g. a -k selection)
+        return 0
     runs, broken = pg.denoiser.hip().persist_info()
     assert not broken, "the handle gave up the persistent path (failed launches)"
     return runs

@@ -57,16 +57,18 @@ def main():
         modes = [("adaln", lambda: [hB.adaln(tv, spk[1], r, r) for _ in range(40)]),
                  ("mm_f32", lambda: [torch.mm(f32a, f32a) for _ in range(4)]),
                  ("mm_bf16", lambda: [torch.mm(bfa, bfa) for _ in range(3)]),
-                 ("ew_f32", lambda: [ew.mul_(1.0001).add_(1e-6) for _ in range(20)])]
+                 ("ew_f32", lambda: [ew.mul_(1.0001).add_(1e-6) for _ in range(20)]),
+                 ("velB", lambda: [hB.velocity(xs[1], t, spk[1]) for _ in range(2)])]
         dtune(hA, "stop_after", 2)
-        for var in (0, 1, 2):
+        ref0 = var0 = None
+        for var in [int(v) for v in os.environ.get("VARS", "0,1,2").split(",")]:
             dtune(hA, "dwgn_var", var)
             hA.velocity(xs[0], t, spk[0])
             torch.cuda.synchronize()
             ref = a16()
-            if var == 0:
-                ref0 = ref
-            print(f"var {var}: solo vs var 0 bitwise equal: {bool(torch.equal(ref, ref0))}", flush=True)
+            if ref0 is None:
+                ref0, var0 = ref, var
+            print(f"var {var}: solo vs var {var0} bitwise equal: {bool(torch.equal(ref, ref0))}", flush=True)
             for name, fn in modes:
                 nbad, tot = 0, 0
                 for rep in range(8):
