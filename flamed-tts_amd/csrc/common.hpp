@@ -178,13 +178,17 @@ struct Tune {
   int prio_all = 0;       // experiment: every graph-path solve replays on the handle's chain-0 stream of split_prio
   int split_prio = 2;      // split chains' replay streams (den_chain_streams): 0 caller + highest, 1 all low, 2 all high
   int split_min_rows = 6144;  // ... when every chain still has this many rows
+  int persist_seal_skip = -1;  // diagnostic: one workgroup skips its hand-off seals in this step (seal modes must fail)
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
-  int persist_opt = 585;   // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
+  int persist_opt = 328265;  // persistent kernel variant bits (pk::Params::opt): 1 = 4-wave weight DMA, 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
-                           // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms)
+                           // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms), 65536 = deferred hand-off
+                           // seals (default-on verification, +2.5 %), 262144 = one gemm() per 64-frame chunk
+                           // (multi-chunk solves 8 % faster than gemm_multi); A/B bits: 16384 blocking seals (+12 %),
+                           // 32768 wave-local staging order, 1024 2 x 2 wave split, 4096 drain behind the DMA
   int pva_split = 0;       // PVA nets: split-K of their small-M fp32 GEMMs (fixed slice order); measured
                            // neutral (L = 60 / 247, 64 steps: 2.70 / 2.94 vs 2.61 / 2.92 ms), so off
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)

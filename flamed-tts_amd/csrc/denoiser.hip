@@ -2533,6 +2533,7 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, i
   P.opt = tn().persist_opt;
   P.ntw = pk::persist_ntw(B, T, P.opt);
   P.inject_step = tn().persist_inject;
+  P.seal_skip = tn().persist_seal_skip;
   hipEvent_t* ev = nullptr;
   if (!cap) {
     ev = d->pring[d->pring_n % Den::kPRing];

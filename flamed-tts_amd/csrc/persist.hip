@@ -111,6 +111,10 @@ __device__ __forceinline__ bool wait_ge(int* err, int* fails, long long tmo, int
     for (unsigned it = 0;; ++it) {
       bool mine = true;
       if (lane < n) mine = __hip_atomic_load(base + lane * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
+      // the last lane watches the error word in the same poll: a wait whose counters are already complete still
+      // stops once any workgroup has given the launch up (a deferred seal check, persist_opt 65536, fails
+      // without stalling anyone)
+      else if (lane == 63) mine = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
       if (__all(mine)) break;
       if ((it & 31) == 31) {  // the error word and the clock only every 32 polls: one round trip per poll
         if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
@@ -374,6 +378,15 @@ __device__ __forceinline__ void gemm_multi(const bf16* A, int r0, int nr, const 
       }
     }
   }
+}
+
+// Several chunks, one gemm() per chunk (persist_opt 262144, A/B against gemm_multi): each chunk's whole A tile is in
+// flight at once (32 loads per wave) before its MFMAs, the panel already in LDS after the first chunk.
+template <int K, int NTW>
+__device__ __forceinline__ void gemm_seq(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[NTW][2], int wave,
+                                         int lane_in, unsigned long long* stamp, int g, bool frag) {
+#pragma unroll
+  for (int ci = 0; ci < NTW; ++ci) gemm<K>(A, r0, nr, wl, acc[ci], wave, lane_in, ci == 0 ? stamp : nullptr, g, frag, wave + 4 * ci, ci == 0);
 }
 
 // The same product with the work split 2 x 2 (persist_opt 1024): wave w = (pair p, half h) multiplies row tiles
@@ -685,11 +698,36 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   // finishes normally), so a failure can never pass for a result.
   // seal mode: this workgroup's seal, written before each group signal; the check after each group wait
   const bool seal = (P.opt & 16384) != 0;
+  // deferred seals (persist_opt 65536): the same seals, but wave 0 only ISSUES the seal loads after the counter
+  // wait (they travel with the phase's A fetch) and checks them at the next seal_put, a phase later; a seal
+  // behind its counter then fails the launch (error 4, NaN at every workgroup's next wait) instead of being
+  // waited for -- detection without a round trip on the hand-off chain
+  const bool dseal = (P.opt & 65536) != 0;
+  int dseal_v = 0x7fffffff, dseal_tgt = 0;  // wave 0: min of the seals loaded at the last wait, and its target
+  auto dseal_check = [&]() {
+    if (dseal && wave == 0) {
+      const bool ok = __all(dseal_v >= dseal_tgt);
+      if (!ok && lane == 0) raise_err(errw, fails, 4);
+      return ok;
+    }
+    return true;
+  };
   auto seal_put = [&]() {
-    if (seal && tid == 0)
+    dseal_check();
+    if ((seal || dseal) && tid == 0 && !(cur_step == P.seal_skip && blockIdx.x == 5))
       __hip_atomic_store(P.seal + 4 * (g * kSlots + s), L + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   auto seal_wait = [&](int g0, int ng) -> bool {
+    if (dseal) {
+      if (wave == 0) {
+        // one load per lane: the group's 32 seals (twice), or for the all-group waits (depthwise halo, Euler
+        // boundary rows) the seals of the two neighbouring groups whose rows this workgroup reads
+        const int gi = ng == 1 ? g0 : (lane < 32 ? (g + kGroups - 1) % kGroups : (g + 1) % kGroups);
+        dseal_v = __hip_atomic_load(P.seal + 4 * (gi * kSlots + (lane & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dseal_tgt = L;
+      }
+      return true;
+    }
     return !seal || seals_ok(P.seal + 4 * g0 * kSlots, ng * kSlots, L, P.ctr + CT_ERR, P.sticky + SY_FAILS, P.tmo,
                              reinterpret_cast<int*>(smem + L_FLAG));
   };
@@ -810,7 +848,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     f32x4 accm[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
     if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
-    else gemm_multi<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
+    else if (P.opt & 262144) gemm_seq<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
+      else gemm_multi<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
     PST(step);
 #pragma unroll
     for (int ci = 0; ci < NTW; ++ci) {
@@ -1084,6 +1123,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_c2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
       PST(step);
 #pragma unroll
@@ -1129,6 +1169,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_c3[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
       PST(step);
 #pragma unroll
@@ -1178,6 +1219,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_m0[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);  // (the first tile's barrier orders the statistics)
       PST(step);
 #pragma unroll
@@ -1218,6 +1260,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_m2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
       PST(step);
 #pragma unroll
@@ -1267,7 +1310,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     f32x4 acco[NTW][2];  // every tile's products first: with several chunks Y goes into this phase's panel buffer
     if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
-    else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
+    else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
+      else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
     PST(step);
     // Y of the group: [row][24] fp32 (tap-major x 8 channels) -- in the staging tile (one chunk), or in the
     // panel conv_out has just finished reading (several chunks: 320 x 24 x 4 B; the next panel DMA goes to the
@@ -1349,6 +1393,14 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     }
     __syncthreads();  // yl (staging) is rewritten by publish_xs
     if (step + 1 < P.s1) publish_xs();
+  }
+  if (dseal) {  // the last wait's seals (no later seal_put checks them)
+    int* okf = reinterpret_cast<int*>(smem + L_FLAG);
+    if (tid == 0) *okf = 1;
+    __syncthreads();
+    if (!dseal_check() && lane == 0) *okf = 0;
+    __syncthreads();
+    if (*okf == 0) { fail_exit(); return; }
   }
 #pragma unroll
   for (int ci = 0; ci < NTW; ++ci) {

@@ -106,6 +106,7 @@ struct Params {
                            // (the host reads it after the fact), [SY_ARRIVE0/1] the reset prologue's arrivals
                            // (unsigned tickets), [SY_PFAIL] the last launch whose prologue failed (counted once)
   int inject_step = -1;    // diagnostic (flamed_tune persist_inject): every workgroup fails at this step
+  int seal_skip = -1;      // diagnostic (flamed_tune persist_seal_skip): workgroup 5 does not store its seals in this step
   long long tmo;           // poll timeout, s_memrealtime ticks (100 MHz)
   int ntw = 1;             // row chunks (64 frames each) per group: the kernel variant (rows per group <= 64 ntw)
   int opt = 0;                        // experiment bits (flamed_tune persist_opt)

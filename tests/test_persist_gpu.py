@@ -139,17 +139,19 @@ def test_persist_knob_off_uses_launch_path(pgb):
     assert _runs(pg) == r0
 
 
-PERSIST_DEFAULT = 585  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
+PERSIST_DEFAULT = 328265  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
 
 
 @pytest.mark.parametrize("T", [400, 131, 16])
-@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 4096, 16384])
+@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 4096, 16384, 32768, 65536])
 def test_persist_variants_bitwise(pgb, T, flip):
     """Hand-off variants change where and how data moves, never the arithmetic: the default equals, bitwise,
     the default with row-major instead of fragment-major A images (bit 64), counter-based instead of
     tagged-granule GroupNorm exchange (bit 512), both plus the other weight-DMA wave split (bit 1), the
-    hand-off drain issued behind the next weight DMA (bit 4096), and the seal verification mode (bit 16384:
-    every group wait also checks the producers' hand-off seals), for full, partial-tile and nearly-empty
+    hand-off drain issued behind the next weight DMA (bit 4096), the seal verification modes (bit 16384:
+    every group wait also checks the producers' hand-off seals; bit 65536: the same seals loaded with the
+    phase's operands and checked a phase later), wave-local staging order (bit 32768), for full, partial-tile
+    and nearly-empty
     row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm)."""
     pg, _ = pgb
     x0, spk = _inputs(11, 1, T)
@@ -317,21 +319,46 @@ def test_solve_part_without_step0_rejected(pgb):
     assert rc == 1001
 
 
-def test_persist_seal_mode_cfg1(pgb):
-    """the configs[1] solve with every group hand-off sealed (persist_opt bit 16384: each
-    producer stores its hand-off number write-through ahead of the drain that precedes its counter add, and
-    every consumer checks the seals of all the producers it reads after its counter wait).  No seal may lag
-    its counter (a lag spins, then fails the launch with error 4 and NaN), and the result equals the unsealed
-    solve bitwise."""
+@pytest.mark.parametrize("bit", [16384, 65536])
+def test_persist_seal_mode_cfg1(pgb, bit):
+    """the configs[1] solve with every group hand-off sealed: each producer stores
+    its hand-off number write-through ahead of the drain that precedes its counter add, and every consumer checks
+    the seals of all the producers it reads -- after its counter wait, spinning on a lagging one (bit 16384), or
+    loaded with the phase's operands and checked a phase later (bit 65536, no round trip on the chain).  No seal
+    may lag its counter (a lag fails the launch with error 4 and NaN), and the result equals the unsealed solve
+    bitwise."""
     pg, _ = pgb
     hip = pg.denoiser.hip()
     x0, spk = _inputs(26, 1, 400)
     f0 = hip.persist_fails()
-    a = _solve(pg, x0, spk, 128)
-    with knob("persist_opt", PERSIST_DEFAULT ^ 16384, PERSIST_DEFAULT):
+    with knob("persist_opt", PERSIST_DEFAULT & ~(16384 | 65536), PERSIST_DEFAULT):
+        a = _solve(pg, x0, spk, 128)
+    with knob("persist_opt", (PERSIST_DEFAULT & ~(16384 | 65536)) | bit, PERSIST_DEFAULT):
         b = _solve(pg, x0, spk, 128)
     assert hip.persist_fails() == f0
     assert torch.isfinite(b).all() and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("bit", [16384, 65536])
+def test_persist_seal_lag_detected(pgb, bit):
+    """The seal modes catch a hand-off whose producer did not seal it (diagnostic knob persist_seal_skip: one
+    workgroup skips its seal stores in step 3): the launch fails (NaN-poisoned x, failure counted) instead of
+    returning a result; without a seal mode the same skip is invisible (the counters alone still complete)."""
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
+    pg, _ = pgb
+    h = DenoiserHIP(pg.denoiser, "bf16")
+    h.check_persist = False
+    x0, spk = _inputs(27, 1, 200)
+    ts = torch.linspace(0, 1, 9, device=DEV)
+    base = PERSIST_DEFAULT & ~(16384 | 65536)
+    with torch.inference_mode():
+        with knob("persist_opt", base, PERSIST_DEFAULT), knob("persist_seal_skip", 3, -1):
+            plain = h.solve(x0.to(DEV), ts, spk.to(DEV), 8)
+        assert torch.isfinite(plain).all() and h.persist_fails() == 0
+        with knob("persist_opt", base | bit, PERSIST_DEFAULT), knob("persist_seal_skip", 3, -1):
+            bad = h.solve(x0.to(DEV), ts, spk.to(DEV), 8)
+        assert torch.isnan(bad).all(), "a seal lag must fail the launch"
+        assert h.persist_fails() == 1
 
 
 @pytest.mark.parametrize("B,T", [(2, 200), (4, 100)])
