@@ -109,14 +109,17 @@ FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe);
 FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                      size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t stream);
 /* The persistent solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken by
- * flamed_den_solve / _solve_part with use_graph != 0 on a bf16 handle for one utterance of 16..512 frames,
- * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances of at most 512 / B frames;
+ * flamed_den_solve / _solve_part with use_graph != 0 on a bf16 handle for one utterance of 16..2560 frames,
+ * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances with B x T <= 2560;
  * decided once per solve by its step-0 part, and later parts follow it).  The launch is
  * cooperative (all workgroups co-resident or refused up front, then this device uses the graph of launches)
  * and is only ENQUEUED: no host synchronisation, so it may be captured into a hipGraph (the captured node
  * replays cooperatively).  A launch whose in-kernel wait times out leaves NaN in xt and adds one to a sticky
  * device failure count that later calls read asynchronously; after 3 failures the handle uses the graph of
- * launches.  flamed_den_persist_info: *runs = persistent launches enqueued on this handle, *broken = 1 once
+ * launches.  Lifetime: a solve captured into a caller's graph (persistent or not) points at this handle's
+ * scratch, counters and graph execs, which flamed_den_destroy / _load free after waiting only for the handle's
+ * own uncaptured work -- keep the handle alive while a captured graph can still replay.
+ * flamed_den_persist_info: *runs = persistent launches enqueued on this handle, *broken = 1 once
  * it has given up the persistent path, *last_ms = device time of the last uncaptured launch (HIP events
  * around the kernel on the launch stream; waits for it). */
 FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, float* last_ms);
