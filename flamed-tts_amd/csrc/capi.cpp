@@ -103,6 +103,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"stop_after", &Tune::stop_after, -1, 1 << 20, nullptr},
       {"coop", &Tune::coop, 0, 1, nullptr},
       {"dwgn_var", &Tune::dwgn_var, 0, 2, nullptr},
+      {"pva_stage", &Tune::pva_stage, 0, 3, nullptr},
       {"pva_inject", &Tune::pva_inject, -1, 1 << 20, nullptr},
   };
   for (const Knob& k : knobs) {

@@ -194,6 +194,7 @@ struct Tune {
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)
   int attn_mfma = 1;       // transformer attention (prior stack, timbre encoder) on fp32 MFMA (xfmr.hpp)
   int prior_split = 1;     // bf16 prior decoders: split-K of the GEMMs with small tile grids
+  int pva_stage = 1;       // PVA persistent flow: conv A windows of >= 2-tile row groups staged through LDS in chunks
   int pva_inject = -1;     // diagnostic: every persistent PVA flow fails at this step (-1 = never)
   int dwgn_var = 1;        // dwgn kernel variant: 1 scalar fp32 pair math (default), diagnostics for T in (384, 448]: 0 packed, 2 scalar LDS accesses
   int coop = 1;            // persistent kernels as cooperative launches (0: plain launches, for profiling runs)

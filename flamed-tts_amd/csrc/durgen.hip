@@ -341,6 +341,7 @@ static int pva_persist_run(DurNet* nd, DurNet* ns, const PvaWs& w, const uint8_t
   }
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
   P.inject_step = tn().pva_inject;
+  P.stage = tn().pva_stage;
   if (!cap) {
     if (!nd->pev[0]) FL_HIP(hipEventCreate(&nd->pev[0]));
     if (!nd->pev[1]) FL_HIP(hipEventCreate(&nd->pev[1]));

@@ -205,7 +205,9 @@ struct AConv2S {
   }
 };
 
-template <int D, int F>
+// ST (Params::stage): row groups of >= 2 tiles take conv_st (the per-lane gather loops of those groups are not
+// compiled in, so the staged kernel does not carry their registers)
+template <int D, int F, bool ST>
 __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   using LY = Lds<D, F>;
   constexpr int K1 = LY::K1, K2 = LY::K2, CS = LY::CS, NB1 = K1 / 16, NB2 = K2 / 16;
@@ -296,6 +298,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   const float gl = N.g2[col0 + c] * N.lw[col0 + c];
   const float lb = N.lb[0];
   const __amdgpu_buffer_rsrc_t rR1 = rsrc(N.R1, (unsigned)M * F * 4);
+  const __amdgpu_buffer_rsrc_t rP = rsrc(N.P, (unsigned)M * D * 4);  // conv1's P rows (constant during the flow)
   const __amdgpu_buffer_rsrc_t rS1 = rsrc(N.S1, (unsigned)M * CS * 8);
   const __amdgpu_buffer_rsrc_t rS2 = rsrc(N.S2, (unsigned)M * CS * 16);
   __syncthreads();
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
       const int t = wave / KS;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       if (KS == 4) kloop<B4>(acc, W, K, part * NB / 4, (part + 1) * NB / 4, c, q, afs(t));
-      else kloop<B2>(acc, W, K, part * NB / 2, (part + 1) * NB / 2, c, q, af(t));
+      else if constexpr (!ST) kloop<B2>(acc, W, K, part * NB / 2, (part + 1) * NB / 2, c, q, af(t));
       red[wave * 64 + lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
       __syncthreads();
       if (part == 0) {
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
         }
         epi(t, acc);
       }
-    } else {
+    } else if constexpr (!ST) {
       for (int t = wave; t < nt; t += 4) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         kloop<B1>(acc, W, K, 0, NB, c, q, af(t));
@@ -332,6 +335,142 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
       }
     }
   };
+
+  // Row groups of >= 2 tiles (Params::stage): the conv's A window (rows xa .. xa + nw - 1, C channels) goes
+  // through LDS in 64-channel chunks.  Each chunk is one coalesced pass of 16-B row loads (a wave instruction =
+  // 4 rows x 256 B, instead of 16 lanes gathering 16 rows each), transformed by xf (conv1: P + w0 x + temb;
+  // conv2: LayerNorm_1) while written to one of two LDS buffers, further chunks' loads in flight in registers;
+  // then every wave runs the chunk's 3 taps x 2 K-blocks of its tiles (w, w + 4).  K is summed chunk-major
+  // (the launch path sums it tap-major: the same terms, fp32 rounding apart, inside the parity bar).
+  // One barrier per chunk: a buffer is rewritten two chunks later, after the next chunk's barrier, which
+  // every wave reaches only when done with this chunk.
+  // IPT 16-B items per thread per chunk cover a 66-row window (4 tiles + halo); RD - 1 chunks' loads in flight
+  // ahead of the one being staged.  Groups of 5..8 tiles run two passes (tiles w and w + 4, window rows
+  // from 0 and from 64), so every wave holds one tile's accumulator at a time.
+  constexpr int FC = LY::FC, CBS = LY::CBS, PROWS = LY::PROWS, RD = 3;
+  constexpr int IPT = (PROWS * (FC / 4) + kThreads - 1) / kThreads;
+  static_assert(2 * 64 + 2 >= LY::WMAX, "two passes cover a group");
+  auto conv_st = [&](const float* W, int K, auto ctag, auto ld, auto xf, auto epi, auto tick) {  // tick: FL_STAMPS
+    constexpr int C = decltype(ctag)::value, NCH = C / FC;
+    constexpr int NBT = FC / 16;  // K-blocks per tap in a chunk
+    static_assert(C % FC == 0 && NBT % 2 == 0, "chunks of an even number of K-blocks per tap");
+    // two-tile groups: waves (tile w & 1, part w >> 1) split each chunk by K-block (part kp takes blocks kp, kp + 2,
+    // ... of every tap), the two parts summed through LDS at the end (part 0 + part 1: deterministic)
+    const bool kh = nt == 2;
+    const int tw = kh ? (wave & 1) : wave, kp = kh ? (wave >> 1) : 0;
+    const int npass = nt > 4 ? 2 : 1;
+    for (int pass = 0; pass < npass; ++pass) {
+      const int w0 = 64 * pass, nwp = min(nw - w0, PROWS);  // this pass's window rows (window index w0 + row)
+      float4 ring[RD][IPT];
+      // every load is issued unconditionally (rows outside the pass window or the batch read past the buffer's
+      // range, which returns zeros): with no branch around them the compiler's vmcnt waits stay counted, so chunk
+      // k waits only for its own loads, not for the chunks in flight behind it
+      auto issue = [&](float4 (&dst)[IPT], int k) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+          const int i = tid + kThreads * j, row = i / (FC / 4), c4 = i - row * (FC / 4);
+          const int r = xa + w0 + row;
+          dst[j] = ld(row < nwp && r >= 0 && r < M ? r : -1, FC * k + 4 * c4);
+        }
+      };
+      // two accumulators (even / odd units), so consecutive MFMA groups do not wait on each other's result;
+      // summed once at the end (acc0 + acc1: deterministic)
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const int t = tw + 4 * pass;
+      const int m = r0 + 16 * t + c;
+      const bool live = t < nt && m < r0 + nr;
+      const int lm = live ? m % L : 0;
+      auto stage = [&](int k) __attribute__((always_inline)) {
+        float* buf = sa + (k & 1) * (PROWS + 1) * CBS;
+        // branch-free: items past the pass window go to the buffer's spare row PROWS (a load consumed only inside
+        // a branch was sunk into it by the compiler, and its wait became vmcnt(0) behind the chunks in flight)
+#pragma unroll
+        for (int j = 0; j < IPT; ++j) {
+          const int i = tid + kThreads * j, row = i / (FC / 4), c4 = i - row * (FC / 4);
+          const int r = xa + w0 + row;
+          const bool inw = row < nwp;
+          const float4 v = P.stage == 3 ? ring[k % RD][j] : xf(w0 + (inw ? row : 0), FC * k + 4 * c4, ring[k % RD][j]);  // (3: no transform)
+          // rows outside the batch are zero: a bit mask, not a select (a select became a branch again)
+          const unsigned msk = (r >= 0 && r < M) ? ~0u : 0u;
+          const float4 o = make_float4(__uint_as_float(__float_as_uint(v.x) & msk), __uint_as_float(__float_as_uint(v.y) & msk),
+                                       __uint_as_float(__float_as_uint(v.z) & msk), __uint_as_float(__float_as_uint(v.w) & msk));
+          *reinterpret_cast<float4*>(buf + (inw ? row : PROWS) * CBS + 4 * c4) = o;
+        }
+      };
+      auto compute = [&](int k, auto khtag) __attribute__((always_inline)) {
+        const float* buf = sa + (k & 1) * (PROWS + 1) * CBS;
+        constexpr bool KH = decltype(khtag)::value;  // compile-time: no branch around the MFMAs
+        constexpr int NU = 3 * (KH ? NBT / 2 : NBT);  // (tap, K-block) units of this wave in the chunk
+        if (t >= nt) return;
+        // unit u = (tap u / NB, block): its A fragment (the window row of tap, zeroed outside the utterance by a
+        // bit mask on an always-issued read -- the row is inside the pass window for every t < nt) and its B
+        // fragment (weight columns c, the block's 4 K per lane)
+        auto frag = [&](int u, float4& a, float4& b) __attribute__((always_inline)) {
+          constexpr int NB = KH ? NBT / 2 : NBT;
+          const int tap = u / NB, bi = u - tap * NB, blk = KH ? 2 * bi + kp : bi;
+          a = *reinterpret_cast<const float4*>(buf + (m + tap - 1 - xa - w0) * CBS + 4 * q + 16 * blk);
+          const int kb = (tap * C + FC * k) / 16 + blk;
+          b = *reinterpret_cast<const float4*>(W + c * K + 4 * ((4 * kb + q) ^ c));
+        };
+        // units in groups of UG: the group's 2 UG LDS reads are issued together, then its 4 UG MFMAs
+        constexpr int UG = NU % 4 == 0 ? 4 : 3;
+#pragma unroll
+        for (int u0 = 0; u0 < NU; u0 += UG) {
+          float4 ar[UG], br[UG];
+#pragma unroll
+          for (int v = 0; v < UG; ++v) frag(u0 + v, ar[v], br[v]);
+          __builtin_amdgcn_sched_barrier(0);  // the scheduler would sink each read to its MFMAs (one LDS latency each)
+#pragma unroll
+          for (int v = 0; v < UG; ++v) {
+            const int u = u0 + v, tap = u / (NU / 3), l = lm + tap - 1;
+            const unsigned vm = (live && l >= 0 && l < L) ? ~0u : 0u;
+            const float4 a = make_float4(__uint_as_float(__float_as_uint(ar[v].x) & vm), __uint_as_float(__float_as_uint(ar[v].y) & vm),
+                                         __uint_as_float(__float_as_uint(ar[v].z) & vm), __uint_as_float(__float_as_uint(ar[v].w) & vm));
+            const float4 b = br[v];
+            f32x4& ac = (u & 1) ? acc1 : acc;
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, ac, 0, 0, 0);
+          }
+        }
+      };
+      // software pipeline, one barrier per chunk: iteration k stages chunk k + 1 (into the other buffer, last read by
+      // chunk k - 1's MFMAs, which every wave finished before the previous barrier) and runs chunk k's MFMAs, so a
+      // wave's staging VALU / LDS work can issue in the MFMA gaps
+#pragma unroll
+      for (int k = 0; k < RD - 1; ++k)
+        if (k < NCH) issue(ring[k], k);
+      stage(0);
+      __syncthreads();
+      if (pass == 0) tick();
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        if (k + RD - 1 < NCH) issue(ring[(k + RD - 1) % RD], k + RD - 1);
+        if (k + 1 < NCH) stage(k + 1);
+        if (P.stage != 2) {  // (diagnostic 2: no MFMAs)
+          if (kh) compute(k, std::true_type{});
+          else compute(k, std::false_type{});
+        }
+        __syncthreads();
+        if (pass == 0 && (k & 1)) tick();
+      }
+      acc[0] += acc1[0]; acc[1] += acc1[1]; acc[2] += acc1[2]; acc[3] += acc1[3];
+      if (kh) {
+        red[wave * 64 + lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        __syncthreads();
+        if (kp == 0) {
+          const float4 o = red[(wave + 2) * 64 + lane];
+          acc[0] += o.x; acc[1] += o.y; acc[2] += o.z; acc[3] += o.w;
+          epi(tw, acc);
+        }
+      } else if (t < nt) {
+        epi(t, acc);
+      }
+      __syncthreads();  // the chunk buffers (sa) and red are reused by the next pass / conv / step
+    }
+  };
+  const bool staged = ST && nt >= 2;
 
   for (int s = 0; s < P.nfe; ++s) {
 #ifdef FL_STAMPS
@@ -353,6 +492,31 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
     PVST();
 
     // ---- conv1 (pva.py:221-230: proj(cat(x_t, enc)) + temb -> Conv k3 -> ReLU) + LN1 partials
+    auto epi1 = [&](int t, const f32x4& acc) {
+#pragma unroll
+           for (int i = 0; i < 4; ++i) {
+             const int row = 16 * t + 4 * q + i;
+             const float v = fmaxf(acc[i] + bias1, 0.f);
+             if (row < nr) st4_wt(rR1, (unsigned)(((r0 + row) * F + col0 + c) * 4), v);
+             const float mean = wave_sum16(v) * (1.0f / kCols);
+             const float d = v - mean;
+             const float m2 = wave_sum16(d * d);
+             if (c == 0 && row < nr) st8_wt(rS1, (unsigned)(((r0 + row) * CS + cs) * 8), mean, m2);
+           }
+         };
+    if (staged) {
+      conv_st(W1, K1, std::integral_constant<int, D>{},
+              [&](int r, int ch) {  // r < 0: past the range (zeros)
+                return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rP, r < 0 ? 0xfffffff0u : (unsigned)((r * D + ch) * 4), 0, 0));
+              },
+              [&](int row, int ch, float4 p) {
+                const float4 w = *reinterpret_cast<const float4*>(vw0 + ch);
+                const float4 e = *reinterpret_cast<const float4*>(vte + ch);
+                const float x = xs[row];
+                return make_float4((p.x + w.x * x) + e.x, (p.y + w.y * x) + e.y, (p.z + w.z * x) + e.z, (p.w + w.w * x) + e.w);
+              },
+              epi1, [] {});
+    } else {
     conv(W1, K1, std::integral_constant<int, NB1>{},
          [&](int t) {
            const int m = r0 + 16 * t + c;
@@ -364,18 +528,8 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
            const bool live = m < r0 + nr;
            return AConv1S<D, F>{sa, vw0, vte, xs, m, live ? m % L : 0, L, xa, q, live};
          },
-         [&](int t, const f32x4& acc) {
-#pragma unroll
-           for (int i = 0; i < 4; ++i) {
-             const int row = 16 * t + 4 * q + i;
-             const float v = fmaxf(acc[i] + bias1, 0.f);
-             if (row < nr) st4_wt(rR1, (unsigned)(((r0 + row) * F + col0 + c) * 4), v);
-             const float mean = wave_sum16(v) * (1.0f / kCols);
-             const float d = v - mean;
-             const float m2 = wave_sum16(d * d);
-             if (c == 0 && row < nr) st8_wt(rS1, (unsigned)(((r0 + row) * CS + cs) * 8), mean, m2);
-           }
-         });
+         epi1);
+    }
     PVST();
     signal(h1 + rg * kLine);
     PVST();
@@ -429,6 +583,30 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
     PVST();
 
     // ---- conv2 (Conv k3 over LN1 -> ReLU) + head partials over the slice
+    auto epi2 = [&](int t, const f32x4& acc) {
+#pragma unroll
+           for (int i = 0; i < 4; ++i) {
+             const int row = 16 * t + 4 * q + i;
+             const float v = fmaxf(acc[i] + bias2, 0.f);
+             const float mean = wave_sum16(v) * (1.0f / kCols);
+             const float d = v - mean;
+             const float m2 = wave_sum16(d * d);
+             const float sg = wave_sum16(d * gl);
+             if (c == 0 && row < nr) st16_wt(rS2, (unsigned)(((r0 + row) * CS + cs) * 16), make_float4(mean, m2, sg, 0.f));
+           }
+         };
+    if (staged) {
+      conv_st(W2, K2, std::integral_constant<int, F>{},
+              [&](int r, int ch) { return ld16_sc1(rR1, r < 0 ? 0xfffffff0u : (unsigned)((r * F + ch) * 4)); },
+              [&](int row, int ch, float4 v) {
+                const float mean = st[2 * row], rstd = st[2 * row + 1];
+                const float4 g = *reinterpret_cast<const float4*>(vg1 + ch);
+                const float4 b = *reinterpret_cast<const float4*>(vb1 + ch);
+                return make_float4(((v.x - mean) * rstd) * g.x + b.x, ((v.y - mean) * rstd) * g.y + b.y,
+                                   ((v.z - mean) * rstd) * g.z + b.z, ((v.w - mean) * rstd) * g.w + b.w);
+              },
+              epi2, [&] { PVST(); });
+    } else {
     conv(W2, K2, std::integral_constant<int, NB2>{},
          [&](int t) {
            const int m = r0 + 16 * t + c;
@@ -440,18 +618,8 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
            const bool live = m < r0 + nr;
            return AConv2S<F>{sa, m, live ? m % L : 0, L, xa, q, live};
          },
-         [&](int t, const f32x4& acc) {
-#pragma unroll
-           for (int i = 0; i < 4; ++i) {
-             const int row = 16 * t + 4 * q + i;
-             const float v = fmaxf(acc[i] + bias2, 0.f);
-             const float mean = wave_sum16(v) * (1.0f / kCols);
-             const float d = v - mean;
-             const float m2 = wave_sum16(d * d);
-             const float sg = wave_sum16(d * gl);
-             if (c == 0 && row < nr) st16_wt(rS2, (unsigned)(((r0 + row) * CS + cs) * 16), make_float4(mean, m2, sg, 0.f));
-           }
-         });
+         epi2);
+    }
     PVST();
     signal(h2 + rg * kLine);
     PVST();
@@ -496,11 +664,13 @@ size_t pva_persist_lds() { return (size_t)Lds<192, 384>::BYTES; }
 bool pva_persist_device_ok(int device, int grid) {
   int cus = 0, nb = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < grid) return false;
-  const void* k = reinterpret_cast<const void*>(pva_persist_kernel<192, 384>);
-  if (set_max_lds(k) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pva_persist_kernel<192, 384>, kThreads, Lds<192, 384>::BYTES) != hipSuccess)
-    return false;
-  return nb >= 1;
+  for (const void* k : {reinterpret_cast<const void*>(pva_persist_kernel<192, 384, true>),
+                        reinterpret_cast<const void*>(pva_persist_kernel<192, 384, false>)}) {
+    if (set_max_lds(k) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, Lds<192, 384>::BYTES) != hipSuccess || nb < 1)
+      return false;
+  }
+  return true;
 }
 
 int pva_persist_launch(const Params& Pin, hipStream_t st) {
@@ -513,7 +683,8 @@ int pva_persist_launch(const Params& Pin, hipStream_t st) {
   // cooperative: the runtime checks the grid against the occupancy and refuses it up front; a captured
   // cooperative launch replays cooperatively
   void* args[] = {&P};
-  const void* kern = reinterpret_cast<const void*>(pva_persist_kernel<192, 384>);
+  const void* kern = P.stage ? reinterpret_cast<const void*>(pva_persist_kernel<192, 384, true>)
+                             : reinterpret_cast<const void*>(pva_persist_kernel<192, 384, false>);
   // tune coop 0: plain launch (profiling, README "Known issues"); residency checked by pva_persist_eligible
   const hipError_t e = tn().coop ? hipLaunchCooperativeKernel(kern, dim3(P.grid), dim3(kThreads), args, Lds<192, 384>::BYTES, st)
                                  : hipLaunchKernel(kern, dim3(P.grid), dim3(kThreads), args, Lds<192, 384>::BYTES, st);

@@ -61,6 +61,7 @@ struct Params {
   int grid;       // workgroups of this launch (2 nets x CS slices x RG row groups)
   long long tmo;  // poll timeout, s_memrealtime ticks (100 MHz)
   int inject_step = -1;  // diagnostic (flamed_tune pva_inject): every workgroup abandons the flow at this step
+  int stage = 1;         // row groups of >= 2 tiles: conv A windows staged through LDS in 32-channel chunks (tune pva_stage)
   unsigned long long* pst = nullptr;  // FL_STAMPS builds: per-workgroup timeline of step pst_step
   int pst_step = -1;
 };
@@ -72,8 +73,11 @@ struct Lds {
   static constexpr int K1 = 3 * D, K2 = 3 * F, CS = F / kCols, XR = kMaxRowsWG + 4;
   static constexpr int W1 = 0, W2 = W1 + kCols * K1 * 4, W0 = W2 + kCols * K2 * 4, G1 = W0 + D * 4, B1 = G1 + F * 4,
                        TE = B1 + F * 4, XS = TE + D * 4, ST = XS + XR * 4, GS = ST + 2 * XR * 4, RED = GS + 32 * 4,
-                       FLAG = RED + 4 * 64 * 16, SA = FLAG + 16, SAS = F + 4 /* staged row stride (floats) */,
-                       BYTES = SA + 18 * SAS * 4;  // one-tile groups: the conv A window (18 rows) staged in LDS
+                       FLAG = RED + 4 * 64 * 16, SA = FLAG + 16, SAS = F + 4 /* staged row stride (floats) */;
+  // one-tile groups: the conv A window (18 rows) staged in LDS; larger groups (Params::stage): two buffers of a
+  // 64-channel chunk of a 4-tile pass window (66 rows, padded by 16 B), in the same bytes
+  static constexpr int FC = 64, CBS = FC + 4, WMAX = kMaxRowsWG + 2, PROWS = 4 * 16 + 2, SA1 = 18 * SAS * 4,
+                       SA2 = 2 * (PROWS + 1) * CBS * 4, BYTES = SA + (SA1 > SA2 ? SA1 : SA2);  // (+ a spare row)
   static_assert(K1 % 64 == 0 && K2 % 64 == 0 && D % 16 == 0 && F % kCols == 0, "pva persist dims");
   static_assert(RED % 16 == 0 && BYTES <= 160 * 1024, "pva persist LDS");
 };

@@ -209,6 +209,9 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     no faster): one K chain;
  *   "pva_persist"   — 1 (default): the PVA flow of both nets runs as one persistent launch when it
  *                     fits (see flamed_pva_flow); 0: hipGraph of launches;
+ *   "pva_stage"     — 1 (default): in that launch, row groups of >= 2 tiles stage their conv A windows
+ *                     through LDS in 64-channel chunks (coalesced rows); 0: per-lane gathers (round 4);
+ *   "pva_inject"    — diagnostic: every persistent PVA flow fails at this step (-1 default = never);
  *   "attn_mfma"     — 1 (default): transformer attention (prior stack, timbre encoder) on fp32 MFMA;
  *                     0: the LDS-broadcast FMA kernel;
  *   "prior_split"   — 1 (default): bf16 prior decoders split K of the GEMMs whose tile grid leaves CUs

@@ -19,6 +19,8 @@ from flamed import _native as nat  # noqa: E402
 
 SLOTS = 16
 NAMES = ["start", "conv1", "h1.signal", "h1.wait", "ln1.stats", "conv2", "h2.signal", "h2.wait", "head"]
+# staged conv2 (pva_stage, row groups of >= 2 tiles): four more stamps inside conv2
+NAMES_ST = NAMES[:5] + ["c2.stage0", "c2.chunk1", "c2.chunk3", "c2.chunk5"] + NAMES[5:]
 
 
 def main():
@@ -27,6 +29,7 @@ def main():
     ap.add_argument("--nfe", type=int, default=64)
     ap.add_argument("--step", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--knob", action="append", default=[], help="flamed_tune key=value before the flow")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from flamed.models.synthesizer.pva import PVA
@@ -41,6 +44,9 @@ def main():
     mask = torch.zeros(1, L, dtype=torch.bool, device=dev)
     buf = torch.zeros(256 * SLOTS, dtype=torch.int64, device=dev)
     lib = nat.lib()
+    for kv in a.knob:
+        k, v = kv.split("=")
+        nat.check(lib.flamed_tune(k.encode(), int(v)), "flamed_tune")
     with torch.inference_mode():
         pva.flow(enc, mask, a.nfe, 0.3)
         nat.check(lib.flamed_pva_stamps(nat.ptr(buf), a.step), "flamed_pva_stamps")
@@ -61,7 +67,7 @@ def main():
              f"({ms * 1e3 / a.nfe:.2f} us/step), step span (median) {med[-1] - med[0]:.2f} us",
              "  k  point        median_us  d_med  max_us"]
     for k in range(n):
-        lines.append(f"{k:3d}  {NAMES[k] if k < len(NAMES) else '?':12s} {med[k]:9.2f} {med[k] - (med[k - 1] if k else 0):6.2f} {mx[k]:7.2f}")
+        lines.append(f"{k:3d}  {(NAMES_ST if n == len(NAMES_ST) else NAMES)[k] if k < max(len(NAMES), n) and k < len(NAMES_ST if n == len(NAMES_ST) else NAMES) else '?':12s} {med[k]:9.2f} {med[k] - (med[k - 1] if k else 0):6.2f} {mx[k]:7.2f}")
     txt = "\n".join(lines)
     print(txt)
     if a.out:
