@@ -225,6 +225,7 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   float* gs = reinterpret_cast<float*>(smem + LY::GS);   // G_s of the CS slices, [CS] = sum b2 lw
   float4* red = reinterpret_cast<float4*>(smem + LY::RED);
   float* sa = reinterpret_cast<float*>(smem + LY::SA);  // staged A window (one-tile groups)
+  float* uv = reinterpret_cast<float*>(smem + LY::UV);  // staged conv1: U[tap][c] = W1_tap,c . w0, V[tap][c] = W1_tap,c . temb_s
   int* flag = reinterpret_cast<int*>(smem + LY::FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -472,6 +473,38 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
   };
   const bool staged = ST && nt >= 2;
 
+  // conv1 is linear in its input A[src] = P[src] + w0 x_t[src] + temb_s (pva.py:227-230; the conv taps cut at
+  // the utterance edges), so for the staged groups it is split once per flow:
+  //   conv1[m, n] = CP[m, n] + sum_tap valid(m, tap) (x_t[m + tap - 1] U[tap][n] + V_s[tap][n])
+  // with CP = conv1 of the constant P rows (one MFMA pass here, kept in registers in the accumulator layout),
+  // U[tap][n] = W1[n, tap, :] . w0 (once) and V_s[tap][n] = W1[n, tap, :] . temb_s (per step, 48 dots of D).  A
+  // step's conv1 is then elementwise; the sums are regrouped (fp32 rounding apart, inside the parity bar).
+  f32x4 cp[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // dot of weight column c, tap `tap` with an LDS vector v over D (the W1 panel is 16-B-chunk swizzled by column)
+  auto w1dot = [&](int tap, int cc, const float* v, int d0, int d1) {
+    float acc = 0.f;
+    for (int d = d0; d < d1; d += 4) {
+      const int k = tap * D + d;
+      const float4 w = *reinterpret_cast<const float4*>(W1 + cc * K1 + 4 * ((k >> 2) ^ (cc & 15)));
+      const float4 x = *reinterpret_cast<const float4*>(v + d);
+      acc = fmaf(w.x, x.x, acc);
+      acc = fmaf(w.y, x.y, acc);
+      acc = fmaf(w.z, x.z, acc);
+      acc = fmaf(w.w, x.w, acc);
+    }
+    return acc;
+  };
+  if (staged) {
+    conv_st(W1, K1, std::integral_constant<int, D>{},
+            [&](int r, int ch) {  // r < 0: past the range (zeros)
+              return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rP, r < 0 ? 0xfffffff0u : (unsigned)((r * D + ch) * 4), 0, 0));
+            },
+            [&](int, int, float4 p) { return p; },
+            [&](int t, const f32x4& acc) { cp[t >= 4 ? 1 : 0] = acc; }, [] {});
+    if (tid < 3 * kCols) uv[tid] = w1dot(tid / kCols, tid % kCols, vw0, 0, D);
+    __syncthreads();
+  }
+
   for (int s = 0; s < P.nfe; ++s) {
 #ifdef FL_STAMPS
     int pst_k = 0;
@@ -505,17 +538,38 @@ __global__ __launch_bounds__(kThreads, 1) void pva_persist_kernel(Params P) {
            }
          };
     if (staged) {
-      conv_st(W1, K1, std::integral_constant<int, D>{},
-              [&](int r, int ch) {  // r < 0: past the range (zeros)
-                return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rP, r < 0 ? 0xfffffff0u : (unsigned)((r * D + ch) * 4), 0, 0));
-              },
-              [&](int row, int ch, float4 p) {
-                const float4 w = *reinterpret_cast<const float4*>(vw0 + ch);
-                const float4 e = *reinterpret_cast<const float4*>(vte + ch);
-                const float x = xs[row];
-                return make_float4((p.x + w.x * x) + e.x, (p.y + w.y * x) + e.y, (p.z + w.z * x) + e.z, (p.w + w.w * x) + e.w);
-              },
-              epi1, [] {});
+      // V_s: 48 dots of D = 192, four threads per dot (quarters of D, combined in order by shuffles)
+      if (tid < 4 * 3 * kCols) {
+        const int o = tid >> 2, part = tid & 3;
+        float v = w1dot(o / kCols, o % kCols, vte, part * (D / 4), (part + 1) * (D / 4));
+        const float v1 = __shfl_xor(v, 1);
+        v = (part & 1) ? v1 + v : v + v1;  // (p0 + p1), (p2 + p3) in every lane of the pair
+        const float v2 = __shfl_xor(v, 2);
+        v = (part & 2) ? v2 + v : v + v2;  // (p0 + p1) + (p2 + p3)
+        if (part == 0) uv[3 * kCols + o] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        const int t = wave + 4 * ti;
+        if (t >= nt) break;
+        f32x4 acc = cp[ti];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * t + 4 * q + i, m = r0 + row;
+          const int lm = m < M ? m % L : 0;
+          float sum = 0.f;
+#pragma unroll
+          for (int tap = 0; tap < 3; ++tap) {
+            const int l = lm + tap - 1;
+            const float x = xs[row + tap];  // window index of frame m + tap - 1 (xa = r0 - 1)
+            const float term = fmaf(x, uv[tap * kCols + c], uv[3 * kCols + tap * kCols + c]);
+            sum += (m < r0 + nr && l >= 0 && l < L) ? term : 0.f;
+          }
+          acc[i] += sum;
+        }
+        epi1(t, acc);
+      }
     } else {
     conv(W1, K1, std::integral_constant<int, NB1>{},
          [&](int t) {

@@ -73,7 +73,8 @@ struct Lds {
   static constexpr int K1 = 3 * D, K2 = 3 * F, CS = F / kCols, XR = kMaxRowsWG + 4;
   static constexpr int W1 = 0, W2 = W1 + kCols * K1 * 4, W0 = W2 + kCols * K2 * 4, G1 = W0 + D * 4, B1 = G1 + F * 4,
                        TE = B1 + F * 4, XS = TE + D * 4, ST = XS + XR * 4, GS = ST + 2 * XR * 4, RED = GS + 32 * 4,
-                       FLAG = RED + 4 * 64 * 16, SA = FLAG + 16, SAS = F + 4 /* staged row stride (floats) */;
+                       FLAG = RED + 4 * 64 * 16, UV = FLAG + 16, SA = UV + 2 * 3 * kCols * 4,
+                       SAS = F + 4 /* staged row stride (floats) */;
   // one-tile groups: the conv A window (18 rows) staged in LDS; larger groups (Params::stage): two buffers of a
   // 64-channel chunk of a 4-tile pass window (66 rows, padded by 16 B), in the same bytes
   static constexpr int FC = 64, CBS = FC + 4, WMAX = kMaxRowsWG + 2, PROWS = 4 * 16 + 2, SA1 = 18 * SAS * 4,
