@@ -881,23 +881,31 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const bool fin = blk == P.NB;
       const BlockW& bw = P.blk[blk];
       const float* mb = md + (size_t)blk * 6 * H;  // [sh, sc, gate] of the ConvNeXt LN (+ [sh, sc, gate] of the next)
-      // per-column LN affine + AdaLN modulation: va = w (1 + sc), vb = b (1 + sc) + sh (no affine: w = 1, b = 0)
-      auto vab = [&](int col, float& va, float& vb) {
-        const float sc1 = 1.0f + mb[H + col];
-        va = fin ? sc1 : bw.lnw[col] * sc1;
-        vb = fin ? mb[col] : bw.lnb[col] * sc1 + mb[col];
-      };
 
       // -------- LN + modulate + depthwise k31 + GroupNorm(H, H) over T (prob_generator.py:81-89, 153-156)
       // what this phase reads that no other workgroup writes goes out before the wait (its latency hides in
       // the poll): the modulation vectors of the thread's columns, the depthwise taps and bias of channel cc,
       // the GroupNorm affine of the GN-combining lanes
       const int cc = tid & 31, rg = tid >> 5;
-      float hva[4], hvb[4], ova[2], ovb[2];
+      // raw loads only before the wait (the arithmetic that consumes them after it: computed here, the compiler
+      // put the loads' wait ahead of the poll instead of behind it)
+      float hsc[4], hsh[4], hlw[4], hlb[4], osc[2], osh[2], olw[2], olb[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) vab(col0 + 4 * (tid & 7) + e, hva[e], hvb[e]);
+      for (int e = 0; e < 4; ++e) {
+        const int col = col0 + 4 * (tid & 7) + e;
+        hsc[e] = mb[H + col];
+        hsh[e] = mb[col];
+        hlw[e] = fin ? 1.0f : bw.lnw[col];
+        hlb[e] = fin ? 0.0f : bw.lnb[col];
+      }
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) vab(col0 + 16 * nt + c, ova[nt], ovb[nt]);
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = col0 + 16 * nt + c;
+        osc[nt] = mb[H + col];
+        osh[nt] = mb[col];
+        olw[nt] = fin ? 1.0f : bw.lnw[col];
+        olb[nt] = fin ? 0.0f : bw.lnb[col];
+      }
       float w[kTaps];
 #pragma unroll
       for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col0 + cc];
@@ -910,6 +918,20 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
+      // va = w (1 + sc), vb = b (1 + sc) + sh (vab's arithmetic; w = 1, b = 0 without the affine)
+      float hva[4], hvb[4], ova[2], ovb[2];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sc1 = 1.0f + hsc[e];
+        hva[e] = fin ? sc1 : hlw[e] * sc1;
+        hvb[e] = fin ? hsh[e] : hlb[e] * sc1 + hsh[e];
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const float sc1 = 1.0f + osc[nt];
+        ova[nt] = fin ? sc1 : olw[nt] * sc1;
+        ovb[nt] = fin ? osh[nt] : olb[nt] * sc1 + osh[nt];
+      }
       const int wa = max(r0 - kHalo, ub), wz = min(r0 + nr + kHalo, ue);  // the utterance's frames only
       // Everything this phase reads that does not wait on another phase goes out first, so the loads'
       // latencies overlap: the thread's halo item (its 4 columns col0 + 4 (tid & 7)), their modulation vectors,
@@ -1128,7 +1150,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
-        const int tl = wave + 4 * ci;
         const f32x4(&acc)[2] = accm_c2[ci];
         float v[2][4];
 #pragma unroll
