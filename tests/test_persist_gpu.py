@@ -139,7 +139,7 @@ def test_persist_knob_off_uses_launch_path(pgb):
     assert _runs(pg) == r0
 
 
-PERSIST_DEFAULT = 328265  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
+PERSIST_DEFAULT = 328264  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
 
 
 @pytest.mark.parametrize("T", [400, 131, 16])
