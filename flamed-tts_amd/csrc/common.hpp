@@ -168,7 +168,8 @@ struct Tune {
   int fold_big_rows = 6144;
   int graph_steps = 16;    // Euler steps per captured solve graph
   int x16 = 0;             // large-M path: bf16 residual stream X and depthwise output D
-  int g8p_rows = 16384;    // large-M GEMMs from this many rows on 256 x 256 8-phase tiles (0 = off)
+  int g8p_rows = 12800;    // large-M GEMMs from this many rows on 256 x 256 8-phase tiles (0 = off); 12800: the B = 64
+                           // split chains (2 x 12800 rows) take them too (311 -> 278 ms, r05bi)
   int dwgn = 1;            // large-M path: whole-utterance depthwise conv + GroupNorm kernel (T <= 512)
   int dwgn_small = 1;      // small-M bf16 path: one-workgroup-per-8-channels depthwise conv + GroupNorm (T <= 576)
   int fuse_euler = 1;      // small-M solve graphs: conv_out combine + Euler update inside the next proj_in

@@ -34,7 +34,7 @@ extern "C" {
 /* Compute dtypes.  FLAMED_FP8 (denoiser handles only): FLAMED_BF16 everywhere, plus MX-fp8 (OCP e4m3 with
  * one e8m0 scale per 32 input channels, weights and activations) for the four H x H pointwise GEMMs of
  * every block (conv_2, conv_3, mlp.0, mlp.2; BASELINE configs[4]) on the large-M path (B*T >= the
- * g8p_rows knob, default 16384); below it the handle computes exactly as FLAMED_BF16. */
+ * g8p_rows knob, default 12800); below it the handle computes exactly as FLAMED_BF16. */
 enum { FLAMED_F32 = 0, FLAMED_BF16 = 1, FLAMED_FP8 = 2 };
 
 FLAMED_API const char* flamed_last_error(void);
@@ -177,7 +177,7 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     groups of "dw_cg" channels (16 or 32; default 32);
  *   "xcd_strips"    — XCD strip width of small/mid-M register-staged tile placement (0 = off);
  *   "x16"           — 1: bf16 residual stream / depthwise output on the large-M path (0 default);
- *   "g8p_rows"      — large-M GEMMs from this many rows on 256 x 256 8-phase tiles (16384; 0 off);
+ *   "g8p_rows"      — large-M GEMMs from this many rows on 256 x 256 8-phase tiles (12800; 0 off);
  *   "dwgn"          — 1 (default): large-M whole-utterance depthwise conv + GroupNorm kernel;
  *   "dwgn_small"    — 1 (default): small-M one-workgroup-per-8-channels depthwise conv + GroupNorm;
  *   "fuse_euler"    — 1 (default): small-M solve graphs compute the conv_out tap combine + Euler

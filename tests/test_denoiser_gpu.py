@@ -206,7 +206,7 @@ def test_velocity_tuning_paths_bf16(knobs, B, T, pg_bf16):
     ref = orc.denoiser_forward(sd, x, t, c)
     L = nat.lib()
     defaults = {"dma": 1, "bn32": 1, "big": 1, "big_ns": 2, "dw_tc": 64, "dw_cg": 32, "dw_cg32": 1536, "dma_ns": 3, "lnfold": 1,
-                "g8p_rows": 16384, "x16": 0, "dwgn": 1, "dwgn_small": 1}
+                "g8p_rows": 12800, "x16": 0, "dwgn": 1, "dwgn_small": 1}
     try:
         for k, v in knobs.items():
             nat.check(L.flamed_tune(k.encode(), v), "tune")
