@@ -19,6 +19,7 @@ With --strict, exit status 1 when a product kernel (anything but the diagnostic 
 """
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -42,10 +43,14 @@ def regs(op):
 
 
 def code_objects(so):
-    fb = tempfile.mktemp(suffix=".fatbin")
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", so], check=True)
+    # objcopy rewrites its input file when no output file is given: work on a private copy, never on the library
+    # a process may have mapped
+    work = tempfile.mkdtemp()
+    cp, fb = os.path.join(work, "lib.so"), os.path.join(work, "fatbin")
+    shutil.copyfile(so, cp)
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", cp, os.path.join(work, "out.so")], check=True)
     data = open(fb, "rb").read()
-    os.unlink(fb)
+    shutil.rmtree(work, ignore_errors=True)
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
     for i, s in enumerate(starts):
         chunk = data[s:starts[i + 1] if i + 1 < len(starts) else len(data)]
