@@ -184,14 +184,19 @@ struct Tune {
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
-  int persist_opt = 328264;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
+  int persist_opt = 361032;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
                            // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms), 65536 = deferred hand-off
                            // seals (default-on verification, +2.5 %), 262144 = one gemm() per 64-frame chunk
-                           // (multi-chunk solves 8 % faster than gemm_multi); A/B bits: 1 = four-wave weight DMA (round 3
+                           // (multi-chunk solves 8 % faster than gemm_multi), 32768 = wave-local staging order (default since
+                           // r05bn: B = 2 T = 400 32.1 -> 31.7 ms, long-form 156 -> 152.6 ms, B = 1 neutral);
+                           // 2 = row groups of whole 16-row tiles (A/B: B = 1 T = 400 21.1 -> 20.7 ms, B = 2 32.1 ->
+                           // 31.2 ms, but with it the counter-form GroupNorm (bit 512 off) no longer equals the granule
+                           // form bitwise at B = 4 T = 100 (r05bn) -- not default until that is understood);
+                           // A/B bits: 1 = four-wave weight DMA (round 3
                            // default; since round 5 waves 1..3 issue, so wave 0's poll never waits behind weight loads:
                            // 21.50 -> 21.18 ms), 16384 blocking seals (+12 %),
-                           // 32768 wave-local staging order, 1024 2 x 2 wave split, 4096 drain behind the DMA
+                           // 1024 2 x 2 wave split, 4096 drain behind the DMA
   int pva_split = 0;       // PVA nets: split-K of their small-M fp32 GEMMs (fixed slice order); measured
                            // neutral (L = 60 / 247, 64 steps: 2.70 / 2.94 vs 2.61 / 2.92 ms), so off
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)

@@ -52,10 +52,11 @@ __device__ __forceinline__ int opq(int v) {
   return v;
 }
 
-// Row range of group g: ceil(T / 8) consecutive frames (the last groups may be short or empty).  Equal
-// shares, not whole 16-row tiles: every group's GEMM operand then moves the same bytes (T = 400: 50 rows
-// each, instead of one 64-row group pacing seven 48-row ones); rows past nr in a wave's last 16-row
-// fragment read as zero through the buffer range and are never stored.
+// Row range of group g.  Default: ceil(T / 8) consecutive frames per group (T = 400: 50 rows each, the last
+// groups short or empty).  persist_opt bit 2: whole 16-row tiles, group gi of an utterance taking tiles
+// [gi MT / gpu, (gi + 1) MT / gpu) (T = 400: seven 48-row groups and one 64-row group); measured faster (r05bm:
+// 20.7 vs 21.1 ms at B = 1 T = 400) but not default yet (csrc/common.hpp Tune::persist_opt).  Rows
+// past nr in a wave's last 16-row fragment read as zero through the buffer range and are never stored.
 // Several utterances (B = 2, 4 or 8, each of T frames; rows u T .. u T + T - 1): utterance u owns the 8 / B
 // groups u 8/B .. + 8/B - 1 and splits its frames among them the same way, so a group never spans two
 // utterances (its modulation row, GroupNorm statistics and zero padding are its utterance's).
