@@ -181,6 +181,7 @@ struct Tune {
   int split_min_rows = 6144;  // ... when every chain still has this many rows
   int persist_seal_skip = -1;  // diagnostic: one workgroup skips its hand-off seals in this step (seal modes must fail)
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
+  int persist_pad = 1;     // persistent solve for B = 3 / 5..7 as B = 4 / 8 with idle utterances (persist_batch)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
@@ -298,6 +299,21 @@ __device__ __forceinline__ float wave_sum64(float v) {
 
 // Chan et al. parallel combine of (count, mean, M2) partials.
 // An empty partial (nb <= 0) contributes nothing, whatever its mean / M2 words hold.
+// chan_combine with every operation rounded on its own (no FMA contraction): the persistent solve's two GroupNorm
+// exchange forms each inline their own copy of the combine, and -ffp-contract=fast let the compiler fuse
+// `mean + d * (nb / nn)` in one copy and not in the other, so the forms parted by an ulp whenever the groups' counts
+// were unequal (persist_opt bit 2 at B = 4 T = 100: groups of 48 and 52 frames; tools/rowpart_probe.py --dump).
+__device__ __forceinline__ void chan_combine_rn(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+#pragma clang fp contract(off)
+  if (nb <= 0.f) return;
+  const float nn = n + nb;
+  if (nn <= 0.f) return;
+  const float d = meanb - mean;
+  mean = mean + d * (nb / nn);
+  m2 = m2 + (m2b + (d * d) * ((n * nb) / nn));
+  n = nn;
+}
+
 __device__ __forceinline__ void chan_combine(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
   if (nb <= 0.f) return;
   float nn = n + nb;

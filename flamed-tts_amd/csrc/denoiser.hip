@@ -1708,10 +1708,13 @@ struct Den {
   int pruns = 0;             // persistent launches enqueued
   int ppath = -1;            // path of the solve whose step 0 ran last: 1 persistent, 0 graph of launches
   int ppath_key[3] = {-1, -1, -1};  // its (B, T, nfe)
-  // device time of the most recent uncaptured persistent launches: a ring of HIP event pairs around the kernel
+  // the most recent uncaptured persistent launches, a ring: HIP events around the kernel ([0], [1]: device time) and
+  // behind the async copies that follow it ([2]), and each launch's own error word (pinned; 0 = the launch
+  // succeeded), so a caller can ask after one launch without waiting (flamed_den_persist_query)
   static constexpr int kPRing = 64;
-  hipEvent_t pring[kPRing][2] = {};
-  int pring_n = 0;           // pairs recorded so far (slot = n % kPRing)
+  hipEvent_t pring[kPRing][3] = {};
+  int* perr_host = nullptr;  // kPRing pinned ints: the error word of the launch in that slot
+  long long pring_n = 0;     // launches recorded so far (slot = n % kPRing)
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1720,12 +1723,13 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // scratch, the pinned failure word and the timing events (handle destroy / re-load on another device).
 static void persist_release(Den* d) {
   if (d->pring_n > 0) {
-    hipEvent_t last = d->pring[(d->pring_n - 1) % Den::kPRing][1];
+    hipEvent_t last = d->pring[(d->pring_n - 1) % Den::kPRing][2];
     if (last) (void)hipEventSynchronize(last);
   }
   if (d->pmem) { (void)hipFree(d->pmem); d->pmem = nullptr; }
   d->pfail = nullptr;
   if (d->pfail_host) { (void)hipHostFree(d->pfail_host); d->pfail_host = nullptr; }
+  if (d->perr_host) { (void)hipHostFree(d->perr_host); d->perr_host = nullptr; }
   for (auto& pr : d->pring)
     for (hipEvent_t& e : pr)
       if (e) { (void)hipEventDestroy(e); e = nullptr; }
@@ -2461,6 +2465,8 @@ static int persist_alloc(Den* d, hipStream_t st) {
   FL_HIP(hipMemsetAsync(d->pmem, 0, bytes, st));
   FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&d->pfail_host), 16, hipHostMallocDefault));
   *d->pfail_host = 0;
+  FL_HIP(hipHostMalloc(reinterpret_cast<void**>(&d->perr_host), Den::kPRing * sizeof(int), hipHostMallocDefault));
+  for (int i = 0; i < Den::kPRing; ++i) d->perr_host[i] = 0;
   d->pfails_seen = 0;
   return kOk;
 }
@@ -2489,6 +2495,16 @@ static void persist_poll_fails(Den* d) {
 // The persistent solve covers one utterance of 16..512 frames on a bf16 handle with the LayerNorm fold and
 // the shipped dims, on a device where all 256 workgroups are resident at once (one per CU: the cooperative
 // launch checks it again).  Stream capture is allowed: nothing on the call path waits on the device.
+// A batch of 3 or 5..7 utterances runs as the persistent launch of the next supported size (4 / 8) with idle
+// zero utterances in the spare row groups (knob persist_pad): the reference's metadata mode batches 4 utterances and
+// leaves a trailing batch of 1..3 (synthesize.py:268-291, 344).  Time is set by the most-loaded group, the same as
+// for the padded size.
+static int persist_batch(int B) {
+  if (B == 3) return 4;
+  if (B >= 5 && B <= 7) return 8;
+  return B;
+}
+
 static bool persist_eligible(Den* d, int B, int T) {
   const Tune& tu = tn();
   persist_poll_fails(d);
@@ -2496,6 +2512,7 @@ static bool persist_eligible(Den* d, int B, int T) {
   if (d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps || T < 16) return false;
   // one utterance, or (knob persist_multi) B in {2, 4, 8}, each utterance's frames split over its 8 / B row groups;
   // a group holds up to kMaxNTW chunks of 64 frames (kernel variant by chunk count; knob persist_ntw caps it)
+  if (B != 1 && tu.persist_multi && tu.persist_pad) B = persist_batch(B);
   if (B != 1 && (!tu.persist_multi || (B != 2 && B != 4 && B != 8))) return false;
   const int ntw = pk::persist_ntw(B, T, tu.persist_opt);
   if (ntw > pk::kMaxNTW || ntw > tu.persist_ntw || ((tu.persist_opt & 1024) && ntw != 1)) return false;
@@ -2508,11 +2525,12 @@ static bool persist_eligible(Den* d, int B, int T) {
 // copy of the sticky failure word.  A failed launch NaN-poisons x and is reported by the next call / persist_info.
 static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, int T, int s0, int s1, hipStream_t st) {
   const bool cap = stream_capturing(st);
-  FL_REQUIRE(d->pmem && d->pfail_host, "persistent solve: scratch not allocated at load");
+  FL_REQUIRE(d->pmem && d->pfail_host && d->perr_host, "persistent solve: scratch not allocated at load");
   pk::Params P{};
   persist_layout(d->pmem, &P);
   d->pfail = P.sticky + pk::SY_FAILS;
-  P.T = T; P.B = B; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
+  const int Bp = tn().persist_pad ? persist_batch(B) : B;
+  P.T = T; P.B = Bp; P.Bx = Bp != B ? B : 0; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
   P.dt = (float)(1.0 / (double)nfe);
   P.mods = mods; P.MS = d->MS; P.MS0 = d->MS0;
   P.win = reinterpret_cast<const bf16*>(d->win); P.bin = d->bin;
@@ -2531,13 +2549,14 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, i
   P.xt = xt;
   P.tmo = 50000000;  // 0.5 s of s_memrealtime (100 MHz) per wait
   P.opt = tn().persist_opt;
-  P.ntw = pk::persist_ntw(B, T, P.opt);
+  P.ntw = pk::persist_ntw(Bp, T, P.opt);
   P.inject_step = tn().persist_inject;
   P.seal_skip = tn().persist_seal_skip;
   hipEvent_t* ev = nullptr;
+  const int slot = (int)(d->pring_n % Den::kPRing);
   if (!cap) {
-    ev = d->pring[d->pring_n % Den::kPRing];
-    for (int k = 0; k < 2; ++k)
+    ev = d->pring[slot];
+    for (int k = 0; k < 3; ++k)
       if (!ev[k]) FL_HIP(hipEventCreate(&ev[k]));
     FL_HIP(hipEventRecord(ev[0], st));
   }
@@ -2547,8 +2566,12 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, i
   if (lrc) return lrc;
   if (!cap) {
     FL_HIP(hipEventRecord(ev[1], st));
-    ++d->pring_n;
     FL_HIP(hipMemcpyAsync(d->pfail_host, d->pfail, sizeof(int), hipMemcpyDeviceToHost, st));
+    // this launch's own error word (set by its first failing workgroup, zeroed by the next launch's prologue, which
+    // is stream-ordered behind this copy)
+    FL_HIP(hipMemcpyAsync(d->perr_host + slot, P.ctr + pk::CT_ERR, sizeof(int), hipMemcpyDeviceToHost, st));
+    FL_HIP(hipEventRecord(ev[2], st));
+    ++d->pring_n;
   }
   ++d->pruns;
   return kOk;
@@ -2643,6 +2666,35 @@ FLAMED_API int flamed_den_persist_fails(flamed_den_t h, int* fails) {
   return kOk;
 }
 
+FLAMED_API int flamed_den_persist_last(flamed_den_t h, long long* seq) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && seq, "flamed_den_persist_last: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  *seq = d->pring_n - 1;
+  return kOk;
+}
+
+FLAMED_API int flamed_den_persist_query(flamed_den_t h, long long seq, int* state) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && state, "flamed_den_persist_query: bad args");
+  std::lock_guard<std::recursive_mutex> lk(d->mu);
+  FL_REQUIRE(seq >= 0 && seq < d->pring_n, "flamed_den_persist_query: no such launch");
+  if (seq < d->pring_n - Den::kPRing) {
+    *state = 3;  // its ring slot has been reused
+    return kOk;
+  }
+  DeviceGuard dg(d->device);
+  const int slot = (int)(seq % Den::kPRing);
+  const hipError_t e = hipEventQuery(d->pring[slot][2]);
+  if (e == hipErrorNotReady) {
+    *state = 2;
+    return kOk;
+  }
+  FL_HIP(e);
+  *state = __atomic_load_n(d->perr_host + slot, __ATOMIC_RELAXED) != 0 ? 1 : 0;
+  return kOk;
+}
+
 FLAMED_API int flamed_den_persist_times(flamed_den_t h, float* ms, int n) {
   Den* d = reinterpret_cast<Den*>(h);
   if (!d || !ms || n < 0) {
@@ -2651,7 +2703,7 @@ FLAMED_API int flamed_den_persist_times(flamed_den_t h, float* ms, int n) {
   }
   std::lock_guard<std::recursive_mutex> lk(d->mu);
   DeviceGuard dg(d->device);
-  int k = n < d->pring_n ? n : d->pring_n;
+  int k = (long long)n < d->pring_n ? n : (int)d->pring_n;
   if (k > Den::kPRing) k = Den::kPRing;
   for (int i = 0; i < k; ++i) {
     hipEvent_t* ev = d->pring[(d->pring_n - k + i) % Den::kPRing];

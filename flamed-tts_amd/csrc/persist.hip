@@ -24,7 +24,14 @@ constexpr int kStampSlots = 160;
 // the address of the next stamp slot (or null), for a stamp taken inside a helper
 #define PSTP(step) \
   (((step) == P.pst_step && P.pst && pst_k < kStampSlots) ? P.pst + blockIdx.x * kStampSlots + pst_k++ : (++pst_k, nullptr))
+// GroupNorm exchange dump (flamed_persist_gndump): lane tid < 32 of workgroup (g, s), hand-off blk of step gnd_step
+#define GND(k, v)                                                                                       \
+  do {                                                                                                  \
+    if (cur_step == P.gnd_step && P.gnd)                                                                \
+      P.gnd[(((size_t)blk * kWGs + g * kSlots + s) * 32 + (tid & 31)) * 32 + (k)] = (v);                \
+  } while (0)
 #else
+#define GND(k, v) ((void)0)
 #define PST(step) ((void)0)
 #define PSTP(step) nullptr
 #endif
@@ -588,6 +595,22 @@ __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) 
     for (int i = 0; i < 4; ++i) v[nt][i] = acc[nt][i];
 }
 
+// GroupNorm statistics of one channel from the 8 groups' (count, mean, M2), Chan-combined in group order over this
+// utterance's groups only (another utterance's entries are masked whole: a zero count alone would still add its M2),
+// and the (mean, scale) the apply uses.  One code path for both exchange forms, every operation rounded on its own
+// (chan_combine_rn), so the granule and counter forms give the same bits for any row partition.
+__device__ __forceinline__ float2 gn_finalize(const float (&nv)[kGroups], const float (&mv)[kGroups], const float (&qv)[kGroups],
+                                              int utt, int gpu, int T, float gw) {
+#pragma clang fp contract(off)
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kGroups; ++k) {
+    const bool mine = k / gpu == utt;
+    chan_combine_rn(n, mean, m2, mine ? nv[k] : 0.f, mine ? mv[k] : 0.f, mine ? qv[k] : 0.f);
+  }
+  return make_float2(mean, (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gw);
+}
+
 // KH: GEMM phases split 2 x 2 over the waves (gemm_kh, persist_opt 1024): a template parameter, so each variant
 // gets its own register allocation
 // NTW: chunks of 64 rows per group (template: registers are indexed by it), 1..kMaxNTW; KH only with NTW == 1.
@@ -618,6 +641,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   group_rows(g, T, P.B, r0, nr, P.opt);
   const int gpu = kGroups / P.B, utt = g / gpu;  // this group's utterance and its frames [ub, ue)
   const int ub = utt * T, ue = ub + T;
+  // padded batch (P.Bx): an idle utterance runs the same phases on zeros (every group still takes part in every
+  // hand-off), without touching xt; its modulation row is the last real utterance's
+  const bool idle = P.Bx > 0 && utt >= P.Bx;
+  const int MB = P.Bx > 0 ? P.Bx : P.B, mutt = idle ? P.Bx - 1 : utt;
   const int c = lane & 15, q = lane >> 4;
   const int col0 = kCols * s;
   char* stg = smem + L_HS;  // epilogue staging (aliases the dwconv window)
@@ -690,7 +717,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     xs0[i] = 0.f;
     xs1[i] = 0.f;
     const int row = kChunk * i + xr_row;
-    if (row < nr) {
+    if (row < nr && !idle) {
       xs0[i] = P.xt[(size_t)(r0 + row) * kC + xch];
       xs1[i] = P.xt[(size_t)(r0 + row) * kC + xch + 1];
     }
@@ -736,7 +763,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
       const int row = kChunk * i + xr_row;
-      if (row < nr) {
+      if (row < nr && !idle) {
         P.xt[(size_t)(r0 + row) * kC + xch] = __builtin_nanf("");
         P.xt[(size_t)(r0 + row) * kC + xch + 1] = __builtin_nanf("");
       }
@@ -821,6 +848,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         unsigned* pf = reinterpret_cast<unsigned*>(P.sticky + SY_PFAIL);
         if (__hip_atomic_exchange(pf, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != target)
           __hip_atomic_fetch_add(fails, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // and in this launch's error word (zeroed before the second arrival), which the host copies per launch
+        // (flamed_den_persist_query); the workgroups that did get through stop at their first wait
+        __hip_atomic_store(errw, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       fail_exit();
       return;
@@ -831,7 +861,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   float X[NTW][2][4];  // residual stream tiles (this wave's tiles wave + 4 i: 16 rows x 32 columns each), MFMA layout
 
   for (int step = P.s0; step < P.s1; ++step) {
-    const float* md = P.mods + (size_t)(step * P.B + utt) * P.MS;  // this utterance's modulation row
+    const float* md = P.mods + (size_t)(step * MB + mutt) * P.MS;  // this utterance's modulation row
     cur_step = step;
     if (step == P.inject_step) {  // diagnostic failure injection: every workgroup abandons here
       if (tid == 0) raise_err(errw, fails, 3);
@@ -1036,6 +1066,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           float m2t = 0.f;
 #pragma unroll
           for (int k = 0; k < 8; ++k) m2t += red[k * kCols + cc];
+          GND(26, mg);
+          GND(27, m2t);
+          GND(28, (float)nr);
           if (gran) {  // (mean, M2) as two tagged granules: the data is the flag (no drain, no counter)
             unsigned long long* gq = reinterpret_cast<unsigned long long*>(P.gnp) + ((size_t)g * H + col0 + cc) * 2;
             const unsigned long long tag = (unsigned long long)(ndg + 1) << 32;
@@ -1084,16 +1117,20 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
           }
           if (tid == 0) *flag = ok ? 1 : 0;
           if (ok && tid < kCols) {
-            float n = 0.f, mean = 0.f, m2 = 0.f;
+            float nv[kGroups];  // group k's row count from group_rows
 #pragma unroll
             for (int k = 0; k < kGroups; ++k) {
               int ka, kn;
               group_rows(k, T, P.B, ka, kn, P.opt);
-              if (k / gpu != utt) kn = 0;  // another utterance's group: not part of these statistics
-              chan_combine(n, mean, m2, (float)kn, kn > 0 ? mv[k] : 0.f, kn > 0 ? qv[k] : 0.f);
+              nv[k] = (float)kn;
+              GND(3 * k, nv[k]);
+              GND(3 * k + 1, mv[k]);
+              GND(3 * k + 2, qv[k]);
             }
-            const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
-            gnv[tid] = make_float4(mean, sc, gbv, 0.f);
+            const float2 ms = gn_finalize(nv, mv, qv, utt, gpu, T, gwv);
+            GND(24, ms.x);
+            GND(25, ms.y);
+            gnv[tid] = make_float4(ms.x, ms.y, gbv, 0.f);
           }
         }
         __syncthreads();
@@ -1106,17 +1143,21 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (tid < kCols) {  // the 8 groups' partials of this channel, Chan-combined in group order
         const __amdgpu_buffer_rsrc_t rq = rsrc(P.gnp, kGroups * kH * 16);
-        float n = 0.f, mean = 0.f, m2 = 0.f;
+        float nv[kGroups], mv[kGroups], qv[kGroups];  // the producers' (count, mean, M2)
 #pragma unroll
         for (int k = 0; k < kGroups; ++k) {
           const float4 v = as_f4(ld16(rq, (unsigned)((k * H + col0 + tid) * 16)));
-          // this utterance's groups only: another utterance's (count, mean, M2) all masked (a zero count
-          // alone would still add its M2 in chan_combine)
-          const bool mine = k / gpu == utt;
-          chan_combine(n, mean, m2, mine ? v.x : 0.f, mine ? v.y : 0.f, mine ? v.z : 0.f);
+          nv[k] = v.x;
+          mv[k] = v.y;
+          qv[k] = v.z;
+          GND(3 * k, v.x);
+          GND(3 * k + 1, v.y);
+          GND(3 * k + 2, v.z);
         }
-        const float sc = (1.0f / sqrtf(m2 * (1.0f / (float)T) + 1e-5f)) * gwv;
-        gnv[tid] = make_float4(mean, sc, gbv, 0.f);
+        const float2 ms = gn_finalize(nv, mv, qv, utt, gpu, T, gwv);
+        GND(24, ms.x);
+        GND(25, ms.y);
+        gnv[tid] = make_float4(ms.x, ms.y, gbv, 0.f);
       }
       }
       __syncthreads();
@@ -1427,7 +1468,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
   for (int ci = 0; ci < NTW; ++ci) {
     const int row = kChunk * ci + xr_row;
-    if (row < nr) {
+    if (row < nr && !idle) {
       P.xt[(size_t)(r0 + row) * kC + xch] = xs0[ci];
       P.xt[(size_t)(r0 + row) * kC + xch + 1] = xs1[ci];
     }
@@ -1437,6 +1478,13 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #ifdef FL_STAMPS
 static unsigned long long* g_pst_buf = nullptr;
 static int g_pst_step = -1;
+static float* g_gnd_buf = nullptr;
+static int g_gnd_step = -1;
+int persist_gndump(void* buf, int step) {
+  g_gnd_buf = reinterpret_cast<float*>(buf);
+  g_gnd_step = step;
+  return kOk;
+}
 int persist_stamps(void* buf, int step) {
   g_pst_buf = reinterpret_cast<unsigned long long*>(buf);
   g_pst_step = step;
@@ -1470,6 +1518,8 @@ int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
 #ifdef FL_STAMPS
   P.pst = g_pst_buf;
   P.pst_step = g_pst_step;
+  P.gnd = g_gnd_buf;
+  P.gnd_step = g_gnd_step;
 #endif
   // Cooperative: the runtime checks the grid against the kernel's occupancy and rejects it up front
   // (hipErrorCooperativeLaunchTooLarge) instead of queueing workgroups behind resident ones that wait for
@@ -1497,6 +1547,7 @@ int persist_launch(const Params& Pin, hipStream_t st, bool cooperative) {
 
 #ifdef FL_STAMPS
 extern "C" FLAMED_API int flamed_persist_stamps(void* buf, int step) { return fl::pk::persist_stamps(buf, step); }
+extern "C" FLAMED_API int flamed_persist_gndump(void* buf, int step) { return fl::pk::persist_gndump(buf, step); }
 #endif
 
 // Host-side check of the reset prologue's ticket arithmetic (include/flamed_diag.h; CPU unit test).

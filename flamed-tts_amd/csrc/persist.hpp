@@ -79,6 +79,9 @@ struct BlockW {
 struct Params {
   int T, NB, s0, s1;
   int B = 1;               // utterances (1, 2, 4 or 8), each T frames: utterance u owns row groups u 8/B .. + 8/B - 1
+  int Bx = 0;              // > 0: only utterances < Bx carry data (a batch of 3 or 5..7 run as B = 4 / 8): the others
+                           // compute on zeros, never read or write xt, and take modulation row Bx - 1 (mods hold
+                           // nfe x Bx rows)
   float dt;
   const float* mods;
   int MS, MS0;
@@ -112,6 +115,8 @@ struct Params {
   int opt = 0;                        // experiment bits (flamed_tune persist_opt)
   unsigned long long* pst = nullptr;  // FL_STAMPS builds: timeline of step pst_step (persist_timeline.py)
   int pst_step = -1;
+  float* gnd = nullptr;               // FL_STAMPS builds: GroupNorm exchange dump of step gnd_step (rowpart_probe.py)
+  int gnd_step = -1;
 };
 
 // Host side (persist.hip): whether this device runs the 256-workgroup grid fully resident, and the launch.

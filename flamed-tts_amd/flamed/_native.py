@@ -40,6 +40,8 @@ SIGNATURES = {
     "flamed_den_persist_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_float)]),
     "flamed_den_persist_times": (c_int, [P, ctypes.POINTER(c_float), c_int]),
     "flamed_den_persist_status": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "flamed_den_persist_last": (c_int, [P, ctypes.POINTER(ctypes.c_longlong)]),
+    "flamed_den_persist_query": (c_int, [P, ctypes.c_longlong, ctypes.POINTER(c_int)]),
     "flamed_den_solve_part": (c_int, [P, P, P, c_int, c_int, c_int, P, c_size_t, c_int, c_int, c_int, P]),
     "flamed_den_time_kernels_graph": (c_int, [P, P, P, c_int, c_int, P, c_size_t, c_int, ctypes.POINTER(c_float), P]),
     "flamed_tune": (c_int, [ctypes.c_char_p, c_int]),
@@ -101,6 +103,7 @@ DIAG_SIGNATURES = {
     "flamed_probe_mx_gemm": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "flamed_stamp_buffer": (c_int, [P]),
     "flamed_persist_stamps": (c_int, [P, c_int]),
+    "flamed_persist_gndump": (c_int, [P, c_int]),
     "flamed_pva_stamps": (c_int, [P, c_int]),
 }
 # include/flamed_diag.h, "libflamed_hip.so diagnostics" section: exported by the product library, used by

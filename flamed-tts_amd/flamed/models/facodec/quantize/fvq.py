@@ -1,5 +1,9 @@
 """Factorized vector quantizer (drop-in for reference flamed/models/facodec/quantize/fvq.py).
 
+Adapted from Amphion's FACodec `fvq.py` (Copyright (c) 2023 Amphion; MIT license, as the reference file
+carries it): the constructor, `vq2emb`, `get_emb`, `embed_code` and `decode_code` keep Amphion's structure
+because the state-dict schema and the code ids are fixed by released checkpoints.
+
 Per frame: z_e = in_proj(z) (weight-norm Linear dim -> codebook_dim), nearest code by the
 L2-normalised euclidean distance |e|^2 - 2 e.c + |c|^2 (reference fvq.py:102-116), z_q = raw codebook
 row, straight-through `z_e + (z_q - z_e)` kept in that order (it is not bit-identical to z_q in fp32,

@@ -126,6 +126,9 @@ class Flamed(nn.Module):
                                              temperature=temp_denoiser, mask=~tgt_mask.unsqueeze(-1))
         if latents.is_cuda:
             torch.cuda.synchronize(latents.device)  # 'time' covers the device work, as the eager reference does
+            den = self.prob_generator.denoiser
+            if den._hip is not None:  # the solves are checked here, at the sync the pipeline makes anyway
+                den._hip.settle(block=False)
         outputs = {"prior_embs": prior_emb_cond, "prior_logits": prior_logits, "tgt_mask": tgt_mask,
                    "latents": latents, "time": time.time() - start}
         if codec_decoder is not None:

@@ -375,12 +375,13 @@ class DenoiserHIP:
         self.ws = nat.Workspace()
         self.ada_ws = nat.Workspace()
         self._solve_bufs = {}
-        # after a solve that ran as a persistent launch (B = 1 .. 8, bf16), wait for it and re-run it on the
-        # graph of launches if the kernel reported a failure (NaN-poisoned x), so a failed launch never
-        # reaches the caller as a result; skipped inside a stream capture (the caller then owns the check:
-        # persist_status)
+        # a solve that ran as an uncaptured persistent launch (B = 1 .. 8, bf16) is checked WITHOUT waiting for
+        # it: its outcome (flamed_den_persist_query) is looked at by this handle's next call, or by settle() at
+        # the caller's own sync point (Flamed.sample_batch), and a failed launch (NaN-poisoned x) is then re-run
+        # on the graph of launches into the same output tensor, so a failure never survives to the caller's
+        # host copy; skipped inside a stream capture (the caller then owns the check: persist_status)
         self.check_persist = True
-        self._fails_seen = 0
+        self._pending = []  # (launch seq, output, input x, ts, spk, nfe) of solves not yet known to have succeeded
         self.oid = ops.register(self)  # torch.ops.flamed_hip.den_* carry this id
 
     def __del__(self):
@@ -497,11 +498,60 @@ class DenoiserHIP:
         return [float(buf[i]) for i in range(k)]
 
     def solve(self, xt: torch.Tensor, ts: torch.Tensor, spk: torch.Tensor, nfe: int) -> torch.Tensor:
-        """Full Euler solve; returns a new (B,T,C) fp32 tensor."""
+        """Full Euler solve; returns a new (B,T,C) fp32 tensor.  Only enqueues work: a persistent launch is
+        checked later (settle), and a failed one re-written in place before the caller's next sync point."""
         dev = xt.device
         self._ensure(dev)
         B, T, C = xt.shape
         self._check_groupnorm(B, T)
+        capturing = torch.cuda.is_current_stream_capturing()
+        if self._pending and not capturing:  # (event queries are not allowed while a stream captures)
+            self.settle(block=False)
+        runs0, _ = self.persist_status()
+        x = self._launch(xt, ts, spk, nfe, 0)
+        out = x.clone()
+        if self.check_persist and not capturing and self.persist_status()[0] > runs0:
+            seq = ctypes.c_longlong(-1)
+            nat.check(nat.lib().flamed_den_persist_last(self.handle, ctypes.byref(seq)), "flamed_den_persist_last")
+            self._pending.append((seq.value, out, xt.detach().clone(), ts.detach().clone(), spk.detach().clone(), nfe))
+            if len(self._pending) > 32:  # the launch ring holds 64: settle the oldest before their slots are reused
+                self.settle(block=True)
+        return out
+
+    def settle(self, block: bool = True) -> int:
+        """Check this handle's pending persistent solves (flamed_den_persist_query, no wait per launch); a failed
+        one is reported with a warning and re-run on the graph of launches (use_graph bit 2) into the tensor that
+        solve returned, enqueued on the current stream.  block=True first waits for the device, so every pending
+        solve is decided (the call Flamed.sample_batch makes at its own synchronisation); block=False leaves the
+        unfinished ones pending.  Returns the number of re-runs."""
+        if not self._pending or torch.cuda.is_current_stream_capturing():
+            return 0
+        L = nat.lib()
+        if block:
+            torch.cuda.synchronize(self._pending[0][1].device)
+        keep, reruns = [], 0
+        for rec in self._pending:
+            seq, out, x0, ts, spk, nfe = rec
+            st = ctypes.c_int(0)
+            nat.check(L.flamed_den_persist_query(self.handle, seq, ctypes.byref(st)), "flamed_den_persist_query")
+            state = st.value
+            if state == 2:
+                keep.append(rec)
+                continue
+            if state == 3:  # the launch's ring slot was reused: decide from the output itself
+                state = 1 if bool(torch.isnan(out).any()) else 0
+            if state == 1:
+                warnings.warn("flamed: persistent solve failed (its output was NaN-poisoned); "
+                              "re-running it on the graph of launches")
+                out.copy_(self._launch(x0, ts, spk, nfe, 2))
+                reruns += 1
+        self._pending = keep
+        return reruns
+
+    def _launch(self, xt, ts, spk, nfe, extra_graph_bits):
+        """AdaLN rows + flamed_den_solve into the handle's solve buffer (returned, not copied)."""
+        dev = xt.device
+        B, T, C = xt.shape
         L = nat.lib()
         key = (B, T, nfe)
         bufs = self._solve_bufs.get(key)
@@ -517,25 +567,11 @@ class DenoiserHIP:
         # chunk runs was measured slower: 34.8 -> 36.6 ms at B = 1, 352 -> 358 ms at B = 64)
         self.adaln(ts[:nfe], spk, bufs["tidx"], bufs["sidx"], out=bufs["mods"])
         bufs["x"].copy_(xt)
-        use_graph = int(bool(self.den.hip_graph))
-        runs0, _ = self.persist_status()
+        use_graph = int(bool(self.den.hip_graph)) | extra_graph_bits
         nat.check(L.flamed_den_solve(self.handle, nat.ptr(bufs["x"]), nat.ptr(bufs["mods"]), nfe, B, T, nat.ptr(ws),
                                      ws.numel(), use_graph, nat.stream_ptr(dev)),
-                  "flamed_den_solve")
-        if self.check_persist and not torch.cuda.is_current_stream_capturing():
-            runs1, _ = self.persist_status()
-            if runs1 > runs0:  # this solve ran as a persistent launch: make sure it did not fail
-                torch.cuda.current_stream(dev).synchronize()  # also completes the failure count's copy
-                _, fails = self.persist_status()
-                if fails > self._fails_seen:
-                    self._fails_seen = fails
-                    warnings.warn(f"flamed: persistent solve failed ({fails} so far on this handle); "
-                                  "re-running it on the graph of launches")
-                    bufs["x"].copy_(xt)
-                    nat.check(L.flamed_den_solve(self.handle, nat.ptr(bufs["x"]), nat.ptr(bufs["mods"]), nfe, B, T,
-                                                 nat.ptr(ws), ws.numel(), use_graph | 2, nat.stream_ptr(dev)),
-                              "flamed_den_solve (re-run)")
-        return bufs["x"].clone()
+                  "flamed_den_solve" if not extra_graph_bits else "flamed_den_solve (re-run)")
+        return bufs["x"]
 
     def persist_status(self):
         """(persistent launches enqueued, failed launches as of the last completed copy) of this handle; never

@@ -1,5 +1,8 @@
 """Text -> symbol ids (reference flamed/text/__init__.py): plain text goes through the cleaners and
-character symbols; text inside {curly braces} is ARPAbet mapped to "@"-prefixed phoneme symbols."""
+character symbols; text inside {curly braces} is ARPAbet mapped to "@"-prefixed phoneme symbols.
+
+Adapted from https://github.com/keithito/tacotron (MIT license), as the reference's text package notes: the
+`text_to_sequence` / `sequence_to_text` behaviour is kept so the symbol ids are bit-exact."""
 import re
 
 from flamed.text import cleaners

@@ -1,6 +1,7 @@
 """Offline text cleaners (reference flamed/text/cleaners.py).  `unidecode` and `inflect` are not
 available offline: ASCII folding uses unicodedata and numbers are spelled by a small built-in
-speller (integers and decimals), which covers the English cleaner pipeline used at inference."""
+speller (integers and decimals), which covers the English cleaner pipeline used at inference.  The cleaner pipeline follows
+https://github.com/keithito/tacotron (MIT license), as the reference notes."""
 import re
 import unicodedata
 

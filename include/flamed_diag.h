@@ -49,6 +49,11 @@ FLAMED_API int flamed_stamp_buffer(void* buf);
  * s_memrealtime at every wait / compute / signal point of Euler step `step` into buf[wg * 160 + k]
  * (device memory, 256 x 160 uint64); buf = NULL turns it off.  tools/persist_timeline.py. */
 FLAMED_API int flamed_persist_stamps(void* buf, int step);
+/* Persistent solve GroupNorm exchange dump (libflamed_hip_stamps.so only): at Euler step `step`, for every
+ * GroupNorm hand-off j (0..NB), workgroup wg and channel lane c < 32, the 8 groups' (count, mean, M2) exactly as the
+ * combining lane read them, then the combined (mean, scale): buf[((j * 256 + wg) * 32 + c) * 32 + k], k < 26 (device
+ * memory, (NB + 1) x 256 x 32 x 32 floats); buf = NULL turns it off.  tools/rowpart_probe.py --dump. */
+FLAMED_API int flamed_persist_gndump(void* buf, int step);
 /* Persistent PVA flow timeline (libflamed_hip_stamps.so only): thread 0 of every workgroup writes
  * s_memrealtime at fixed points of Euler step `step` into buf[wg * 16 + k]; tools/pva_timeline.py. */
 FLAMED_API int flamed_pva_stamps(void* buf, int step);

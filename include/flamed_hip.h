@@ -110,7 +110,8 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
                                      size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t stream);
 /* The persistent solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken by
  * flamed_den_solve / _solve_part with use_graph != 0 on a bf16 handle for one utterance of 16..2560 frames,
- * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances with B x T <= 2560;
+ * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances with B x T <= 2560 (and, knob
+ * "persist_pad", B = 3 / 5..7 as B = 4 / 8 with idle utterances);
  * decided once per solve by its step-0 part, and later parts follow it).  The launch is
  * cooperative (all workgroups co-resident or refused up front, then this device uses the graph of launches)
  * and is only ENQUEUED: no host synchronisation, so it may be captured into a hipGraph (the captured node
@@ -125,9 +126,19 @@ FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mod
 FLAMED_API int flamed_den_persist_info(flamed_den_t h, int* runs, int* broken, float* last_ms);
 /* Never waits: *runs = persistent launches enqueued on this handle, *fails = its failed launches as of the
  * last completed asynchronous copy of the device's failure count (exact once the stream of the last launch has
- * been synchronised: the copy is ordered behind the launch).  The Python wrapper checks it after each
- * persistent solve and re-runs a failed one with use_graph bit 2. */
+ * been synchronised: the copy is ordered behind the launch).  Retry-budget bookkeeping; a caller that must
+ * know whether one particular solve failed uses flamed_den_persist_last / _query. */
 FLAMED_API int flamed_den_persist_status(flamed_den_t h, int* runs, int* fails);
+/* Per-launch outcome, never waiting.  flamed_den_persist_last: *seq = sequence number of this handle's most recent
+ * uncaptured persistent launch (-1 if none; call it right after a flamed_den_solve that took the persistent path).
+ * flamed_den_persist_query: *state = 0 the launch finished and succeeded, 1 it finished and failed (its xt is
+ * NaN-poisoned: re-run the solve with use_graph | 2), 2 not finished yet (query again later, or synchronise the
+ * launch stream first), 3 unknown (more than 64 uncaptured persistent launches ago).  Each launch's own error word
+ * is copied behind it into pinned memory, so the answer concerns that launch only, not earlier captured replays.
+ * The Python wrapper (DenoiserHIP.settle) checks pending solves this way at its next call or at the caller's sync
+ * point and re-runs a failed one in place. */
+FLAMED_API int flamed_den_persist_last(flamed_den_t h, long long* seq);
+FLAMED_API int flamed_den_persist_query(flamed_den_t h, long long seq, int* state);
 /* Device times (ms, oldest first) of the up to n most recent uncaptured persistent launches (a ring of 64
  * HIP event pairs; waits for them); returns how many were written, -1 on error. */
 FLAMED_API int flamed_den_persist_times(flamed_den_t h, float* ms, int n);
@@ -193,6 +204,8 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     exercise the NaN poisoning / failure count / retry budget;
  *   "persist_multi" — 1 (default): B = 2 / 4 / 8 equal-length utterances also run as one persistent
  *                     launch (rows per group <= 64 x persist_ntw: B x T <= 2560); 0: B = 1 only;
+ *   "persist_pad"   — 1 (default): B = 3 / 5..7 run as the B = 4 / 8 persistent launch with idle zero utterances
+ *                     in the spare row groups (4 x T / 8 x T <= 2560); 0: those B take the graph of launches;
  *   "persist_ntw"   — 64-frame chunks per persistent row group, 1..5 (default 5: T <= 2560 at B = 1);
  *   "persist_capmode" — persistent launch inside a stream capture: 0 (default) cooperative node, 1 plain;
  *   "coop"          — 1 (default): the persistent denoiser solve and PVA flow are cooperative launches;

@@ -104,7 +104,7 @@ def test_diag_header_bound_and_separate(lib):
         assert hasattr(lib, n), f"{n} must be exported by the product library"
     dl = _native.diag_lib()
     for n in names:
-        if n not in ("flamed_stamp_buffer", "flamed_persist_stamps", "flamed_pva_stamps"):  # FL_STAMPS build only
+        if n not in ("flamed_stamp_buffer", "flamed_persist_stamps", "flamed_persist_gndump", "flamed_pva_stamps"):  # FL_STAMPS build only
             assert hasattr(dl, n), n
 
 
