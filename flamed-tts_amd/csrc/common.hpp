@@ -184,16 +184,19 @@ struct Tune {
   int persist_pad = 1;     // persistent solve for B = 3 / 5..7 as B = 4 / 8 with idle utterances (persist_batch)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
+  int persist_multi_ntw = 2;  // ... and for B > 1 up to this many: beyond 2 chunks the graph of launches is faster
+                           // (r06c: B = 4 T = 400, 4 chunks: 60.4 ms persistent vs 47.5 for B = 3 on the graph; B = 2
+                           // T = 400, 2 chunks: 31.4 vs 37.7); B = 1 keeps 5 (long-form T = 2400: 152.6 vs 184 ms)
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
-  int persist_opt = 361032;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
+  int persist_opt = 361034;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
                            // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms), 65536 = deferred hand-off
                            // seals (default-on verification, +2.5 %), 262144 = one gemm() per 64-frame chunk
                            // (multi-chunk solves 8 % faster than gemm_multi), 32768 = wave-local staging order (default since
                            // r05bn: B = 2 T = 400 32.1 -> 31.7 ms, long-form 156 -> 152.6 ms, B = 1 neutral);
-                           // 2 = row groups of whole 16-row tiles (A/B: B = 1 T = 400 21.1 -> 20.7 ms, B = 2 32.1 ->
-                           // 31.2 ms, but with it the counter-form GroupNorm (bit 512 off) no longer equals the granule
-                           // form bitwise at B = 4 T = 100 (r05bn) -- not default until that is understood);
+                           // 2 = row groups of whole 16-row tiles (default since r06c: B = 1 T = 400 20.93 -> 20.55 ms,
+                           // B = 2 31.97 -> 31.43 ms; the r05 counter- vs granule-form GroupNorm divergence under it was
+                           // FMA contraction in one of two inlined combines, fixed by gn_finalize);
                            // A/B bits: 1 = four-wave weight DMA (round 3
                            // default; since round 5 waves 1..3 issue, so wave 0's poll never waits behind weight loads:
                            // 21.50 -> 21.18 ms), 16384 blocking seals (+12 %),

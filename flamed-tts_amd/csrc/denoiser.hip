@@ -2516,6 +2516,7 @@ static bool persist_eligible(Den* d, int B, int T) {
   if (B != 1 && (!tu.persist_multi || (B != 2 && B != 4 && B != 8))) return false;
   const int ntw = pk::persist_ntw(B, T, tu.persist_opt);
   if (ntw > pk::kMaxNTW || ntw > tu.persist_ntw || ((tu.persist_opt & 1024) && ntw != 1)) return false;
+  if (B > 1 && ntw > tu.persist_multi_ntw) return false;  // several utterances: the graph path is faster beyond 2 chunks
   if (d->pdev_ok < 0) d->pdev_ok = pk::persist_device_ok(d->device) ? 1 : 0;
   return d->pdev_ok == 1;
 }

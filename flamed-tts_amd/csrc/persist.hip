@@ -177,7 +177,7 @@ __device__ __forceinline__ bool seals_ok(const int* sp, int n, int target, int* 
     const int lane = threadIdx.x;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
-    for (unsigned it = 0;; ++it) {
+    for (;;) {
       bool mine = true;
       for (int i = lane; i < n; i += 64)
         mine = mine && __hip_atomic_load(sp + 4 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;

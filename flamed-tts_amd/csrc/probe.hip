@@ -256,6 +256,30 @@ __global__ __launch_bounds__(256) void l2_prefetch_kernel(const char* __restrict
 
 using namespace fl;
 
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+// STREAM-style copy for the measured HBM peak (bench.py measured_peaks): each thread moves 4 float4 per grid-stride
+// iteration (mode 1: non-temporal loads and stores, 0: plain), the 4 loads in flight before the 4 stores.
+template <bool NT>
+__global__ __launch_bounds__(256) void copy_probe_kernel(const f32x4v* __restrict__ src, f32x4v* __restrict__ dst, size_t n) {
+  const size_t stride = (size_t)gridDim.x * 1024;
+  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+    f32x4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const size_t j = i + (size_t)k * 256;
+      if (j < n) v[k] = NT ? __builtin_nontemporal_load(src + j) : src[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const size_t j = i + (size_t)k * 256;
+      if (j < n) {
+        if (NT) __builtin_nontemporal_store(v[k], dst + j);
+        else dst[j] = v[k];
+      }
+    }
+  }
+}
+
 extern "C" {
 
 FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int wbufs, const void* A, const void* W,
@@ -370,6 +394,21 @@ FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream
   return time_graph(body, reps, st, us_out);
 }
 
+
+FLAMED_API int flamed_probe_copy(const void* src, void* dst, size_t bytes, int blocks, int mode, int reps, float* us_out,
+                                 hipStream_t st) {
+  FL_REQUIRE(src && dst && us_out && bytes % 16 == 0 && blocks > 0 && reps > 0, "flamed_probe_copy: bad args");
+  const size_t n = bytes / 16;
+  auto body = [&](hipStream_t s) -> int {
+    if (mode == 1)
+      hipLaunchKernelGGL(copy_probe_kernel<true>, dim3(blocks), dim3(256), 0, s, (const f32x4v*)src, (f32x4v*)dst, n);
+    else
+      hipLaunchKernelGGL(copy_probe_kernel<false>, dim3(blocks), dim3(256), 0, s, (const f32x4v*)src, (f32x4v*)dst, n);
+    FL_LAUNCH_CHECK();
+    return kOk;
+  };
+  return time_graph(body, reps, st, us_out);
+}
 
 FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const void* src, float* us_out, hipStream_t st) {
   FL_REQUIRE(src && us_out && blocks > 0 && kb > 0 && kb % 16 == 0 && reps > 0, "flamed_probe_stream: bad args");

@@ -97,6 +97,7 @@ DIAG_SIGNATURES = {
     "flamed_last_error": (ctypes.c_char_p, []),
     "flamed_probe_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_empty": (c_int, [c_int, c_int, ctypes.POINTER(c_float), P]),
+    "flamed_probe_copy": (c_int, [P, P, c_size_t, c_int, c_int, c_int, ctypes.POINTER(c_float), P]),
     "flamed_probe_gemm_pf": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_stream": (c_int, [c_int, c_int, c_int, c_int, P, ctypes.POINTER(c_float), P]),
     "flamed_probe_mx": (c_int, [P, P, P, P, P, c_int, P]),

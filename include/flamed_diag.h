@@ -26,6 +26,11 @@ FLAMED_API int flamed_probe_gemm(int variant, int M, int N, int K, int reps, int
  * (mode 1: LDS-DMA ring, mode 0: register loads).  src must hold blocks x kb KB. */
 FLAMED_API int flamed_probe_stream(int blocks, int kb, int mode, int reps, const void* src, float* us_out, hipStream_t stream);
 FLAMED_API int flamed_probe_empty(int blocks, int reps, float* us_out, hipStream_t stream);
+/* flamed_probe_copy: STREAM-style copy of `bytes` (a multiple of 16) from src to dst by `blocks` x 256 threads, 4 float4
+ * per thread per grid-stride step; mode 1 non-temporal loads / stores, 0 plain.  Average us per launch in a graph of
+ * `reps` launches (bench.py's measured HBM peak: 2 x bytes / time). */
+FLAMED_API int flamed_probe_copy(const void* src, void* dst, size_t bytes, int blocks, int mode, int reps, float* us_out,
+                                 hipStream_t stream);
 /* flamed_probe_gemm_pf: flamed_probe_gemm's chain with a concurrent L2 warm-up of the next launch's
  * weights on a second captured stream (pf_blocks workgroups, a multiple of 8; 0 = none). */
 FLAMED_API int flamed_probe_gemm_pf(int variant, int M, int N, int K, int reps, int wbufs, int pf_blocks, const void* A,

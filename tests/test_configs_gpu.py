@@ -116,8 +116,11 @@ def test_cfg1_prob_sample_128(pg_bf16):
 
 @pytest.fixture(scope="module")
 def cfg2(pg_bf16):
-    x0, spk = _inputs(2, 64, 400)
-    return x0, spk
+    return cfg2_inputs()
+
+
+def cfg2_inputs():
+    return _inputs(2, 64, 400)
 
 
 def test_cfg2_velocity_full_size(pg_bf16, cfg2):
@@ -332,13 +335,81 @@ def test_concurrent_handles_bitwise(pg_bf16):
     assert bad == 0, f"{bad} of 12 overlapped evaluations differ from the solo one"
 
 
-def test_cfg2_split_batch_bitwise(pg_bf16, cfg2):
+def test_concurrent_persistent_solve_bitwise(pg_bf16):
+    """the headline kernel overlapped with the fp32-MFMA work a pipelined caller puts on a second
+    stream.  A configs[1] persistent solve (B = 1, T = 400, nfe = 128, one cooperative launch) must give the same bits
+    as alone while another handle's AdaLN GEMMs (fp32 MFMA) or a PVA flow on its graph of exact-fp32 MFMA launches run
+    on a second stream, started at staggered offsets.  (The library is built without packed-fp32 instructions since
+    round 6 -- tests/test_isa_cpu.py -- so the round-5 trigger pattern cannot occur; this pins the behaviour.)"""
+    from flamed import _native as nat
+    from flamed.models.synthesizer.prob_generator import DenoiserHIP
+    from flamed.models.synthesizer.pva import PVA
+    import yaml
+    from _common import PKG, seeded
+    pg, _ = pg_bf16
+    hA = pg.denoiser.hip()
+    hB = DenoiserHIP(pg.denoiser, "bf16")
+    cfg = yaml.safe_load(open(os.path.join(PKG, "configs", "prior.yaml")))["variance_adaptor"]
+    pva = PVA(cfg).eval()
+    sd = seeded("pva")
+    pva.load_state_dict({k[len("prior_generator.pva."):]: v for k, v in sd.items()})
+    pva = pva.to(DEV)
+    g = torch.Generator().manual_seed(78)
+    x0 = torch.randn(1, 400, C, generator=g).to(DEV)
+    spk = torch.randn(1, C, generator=g).to(DEV)
+    ts = torch.linspace(0, 1, 129, device=DEV)
+    Bb = 64
+    cb = torch.randn(Bb, C, generator=g).to(DEV)
+    r = torch.arange(Bb, device=DEV, dtype=torch.int32)
+    tv = torch.full((Bb,), 0.3, device=DEV)
+    enc = torch.randn(2, 247, 192, generator=g).to(DEV)
+    mask = (torch.arange(247)[None, :] >= torch.tensor([247, 200])[:, None]).to(DEV)
+    L = nat.lib()
+    nat.check(L.flamed_tune(b"pva_persist", 0), "flamed_tune")  # the PVA's graph of fp32-MFMA launches
+    bad, n = 0, 0
+    try:
+        with torch.inference_mode():
+            solo = hA.solve(x0, ts, spk, 128).clone()
+            hB._ensure(torch.device(DEV))  # load the second handle's weights (adaln alone does not)
+            hB.adaln(tv, cb, r, r)
+            pva.flow(enc, mask, 16, 0.3)
+            torch.cuda.synchronize()
+            r0 = hA.persist_status()[0]
+            for mode in ("adaln", "pva"):
+                for rep in range(4):
+                    sA, sB = torch.cuda.Stream(), torch.cuda.Stream()
+                    torch.cuda.synchronize()
+                    with torch.cuda.stream(sB):
+                        if mode == "adaln":
+                            for _ in range(200):
+                                hB.adaln(tv, cb, r, r)
+                        else:
+                            for _ in range(6):
+                                pva.flow(enc, mask, 16, 0.3)
+                    with torch.cuda.stream(sA):
+                        torch.cuda._sleep(20000 * rep)
+                        got = hA.solve(x0, ts, spk, 128)
+                    torch.cuda.synchronize()
+                    bad += int(not torch.equal(got, solo))
+                    n += 1
+            assert hA.settle() == 0
+            runs = hA.persist_status()[0] - r0
+    finally:
+        nat.check(L.flamed_tune(b"pva_persist", 1), "flamed_tune")
+    assert runs == n, "the overlapped solves did not all take the persistent path"
+    assert bad == 0, f"{bad} of {n} overlapped persistent solves differ from the solo one"
+
+
+@pytest.mark.parametrize("B,T", [(64, 400), (128, 100), (50, 250), (24, 512), (33, 400)])
+def test_cfg2_split_batch_bitwise(pg_bf16, B, T):
     """With the dwgn fix, two concurrent sub-batch chains (split_batch 2: parallel graph branches) give exactly the
     single-chain solve (each utterance's arithmetic is independent of the batch split, and concurrency no longer
-    perturbs a kernel)."""
+    perturbs a kernel).  ADVICE r5: beyond configs[2]'s T = 400 (dwgn's 7-chunk instantiation) also T = 100, 250 and
+    512 (other chunk counts), and B = 33 T = 400, where the whole batch (13,200 rows >= g8p_rows) takes the 256 x 256
+    8-phase GEMM tiles while each chain (6,800 / 6,400 rows) takes the 128 x 128 LDS-DMA tiles."""
     from flamed import _native as nat
     pg, _ = pg_bf16
-    x0, spk = cfg2
+    x0, spk = (cfg2_inputs() if (B, T) == (64, 400) else _inputs(90 + B, B, T))
     L = nat.lib()
     nat.check(L.flamed_tune(b"split_batch", 1), "flamed_tune")
     one = _solve(pg, x0, spk, 32)

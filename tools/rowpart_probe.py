@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.join(REPO, "flamed-tts_amd"))
 import torch  # noqa: E402
 import yaml  # noqa: E402
 
-DEFAULT = 361032
+DEFAULT = 361032  # round-5 default (equal shares); the probe flips bit 2 itself
 
 
 def main():
