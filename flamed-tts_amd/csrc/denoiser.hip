@@ -268,7 +268,7 @@ struct EpiConvNeXtResid {
     constexpr int S = kEVecStride;  // field-major (structure of arrays): a row's lanes read consecutive columns
     if (idx < cnt) {
       vec[(slot * 3 + 0) * S + c] = w * sc1;
-      vec[(slot * 3 + 1) * S + c] = b * sc1 + shv;
+      vec[(slot * 3 + 1) * S + c] = __builtin_fmaf(b, sc1, shv);
       vec[(slot * 3 + 2) * S + c] = gv;
       if (slot == 0) vec[6 * S + c] = b3v;
       vec[(7 + slot) * S + c] = al;
@@ -278,29 +278,60 @@ struct EpiConvNeXtResid {
       const size_t mo = (size_t)(r0 + sl) * md.ms + n;
       const float s1 = 1.0f + md.sc[mo];
       vec[(sl * 3 + 0) * S + cc] = (AFF ? lnw[n] : 1.0f) * s1;
-      vec[(sl * 3 + 1) * S + cc] = (AFF ? lnb[n] : 0.0f) * s1 + md.sh[mo];
+      vec[(sl * 3 + 1) * S + cc] = __builtin_fmaf(AFF ? lnb[n] : 0.0f, s1, md.sh[mo]);
       vec[(sl * 3 + 2) * S + cc] = gate[so + mo];
       if (sl == 0) vec[6 * S + cc] = b3[n];
       vec[(7 + sl) * S + cc] = ya ? (yw ? yw[n] : 1.0f) * (1.0f + ysc[so + mo]) : 1.0f;
     }
     return ok;
   }
+  // Every rounding is explicit (no contraction left to the compiler), so the staged path (`use`: the tile spans <= 2
+  // modulation rows) and the direct path give the same bits, whichever GEMM tile family a batch split selects:
+  //   va = w sc1, vb = fma(b, sc1, sh), h = fma(xh, va, vb), out = fma(gate, h + (acc + b3), x)
+  static __device__ __forceinline__ float cnx_out(float x, float xh, float va, float vb, float g, float acc, float b3v) {
+#pragma clang fp contract(off)
+    const float h = __builtin_fmaf(xh, va, vb);
+    return __builtin_fmaf(g, h + (acc + b3v), x);
+  }
   __device__ float value_v(int m, int n, float acc, const float* st, const float* vec, bool use, int bm, int bn, float x) const {
+#pragma clang fp contract(off)
     float xh = (x - st[2 * (m - bm)]) * st[2 * (m - bm) + 1];
     if (use) {
       constexpr int S = kEVecStride;
       const int slot = m / mod.div - bm / mod.div;
       const float* v = vec + slot * 3 * S + (n - bn);
-      float h = xh * v[0] + v[S];
-      return x + v[2 * S] * (h + (acc + vec[6 * S + (n - bn)]));
+      return cnx_out(x, xh, v[0], v[S], v[2 * S], acc, vec[6 * S + (n - bn)]);
     }
     const long long so = mod.so.get();
     const ModRef md = mod.at();
     size_t mo = (size_t)(m / md.div) * md.ms + n;
     float sc1 = 1.0f + md.sc[mo];
     float w = AFF ? lnw[n] : 1.0f, b = AFF ? lnb[n] : 0.0f;
-    float h = xh * (w * sc1) + (b * sc1 + md.sh[mo]);
-    return x + gate[so + mo] * (h + (acc + b3[n]));
+    return cnx_out(x, xh, w * sc1, __builtin_fmaf(b, sc1, md.sh[mo]), gate[so + mo], acc, b3[n]);
+  }
+  // four consecutive columns (n % 4 == 0), the staged vectors read as float4 (gemm_dma.hpp value4_pre); value_v's
+  // expression per column
+  __device__ void value4_v(int m, int n, const float* acc, const float* st, const float* vec, bool use, int bm, int bn,
+                           const float* x, float* out) const {
+    if (!use) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[e] = value_v(m, n + e, acc[e], st, vec, use, bm, bn, x[e]);
+      return;
+    }
+    constexpr int S = kEVecStride;
+    const float mean = st[2 * (m - bm)], rstd = st[2 * (m - bm) + 1];
+    const int slot = m / mod.div - bm / mod.div;
+    const float* v = vec + slot * 3 * S + (n - bn);
+    const float4 va = *reinterpret_cast<const float4*>(v), vb = *reinterpret_cast<const float4*>(v + S);
+    const float4 vg = *reinterpret_cast<const float4*>(v + 2 * S), v3 = *reinterpret_cast<const float4*>(vec + 6 * S + (n - bn));
+    const float a4[4] = {va.x, va.y, va.z, va.w}, b4[4] = {vb.x, vb.y, vb.z, vb.w};
+    const float g4[4] = {vg.x, vg.y, vg.z, vg.w}, c4[4] = {v3.x, v3.y, v3.z, v3.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma clang fp contract(off)
+      const float xh = (x[e] - mean) * rstd;
+      out[e] = cnx_out(x[e], xh, a4[e], b4[e], g4[e], acc[e], c4[e]);
+    }
   }
   // alpha_next of column n for row m (staged, or from the mods table)
   __device__ float alpha_next(int m, int n, const float* vec, bool use, int bm, int bn) const {
@@ -317,8 +348,13 @@ struct EpiConvNeXtResid {
     store_val4<XT>(X + (size_t)m * ld + n, v);
     if (ya) {
       float y[4];
+      if (use && (n - bn) % 4 == 0) {  // the staged alpha row as one float4
+        const float4 a = *reinterpret_cast<const float4*>(vec + (7 + m / mod.div - bm / mod.div) * kEVecStride + (n - bn));
+        y[0] = v[0] * a.x; y[1] = v[1] * a.y; y[2] = v[2] * a.z; y[3] = v[3] * a.w;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = v[e] * alpha_next(m, n + e, vec, use, bm, bn);
+        for (int e = 0; e < 4; ++e) y[e] = v[e] * alpha_next(m, n + e, vec, use, bm, bn);
+      }
       store_val4<bf16>(ya + (size_t)m * ld + n, y);
     }
   }
@@ -361,10 +397,25 @@ struct EpiGatedResidT {  // X = X + gate * (acc + b); [gate x 2 rows, b] staged 
     return true;
   }
   __device__ float value_v(int m, int n, float acc, const float*, const float* vec, bool use, int bm, int bn, float x) const {
+    // out = fma(gate, acc + b, x) with explicit roundings: the staged and direct paths give the same bits
     if (use) {
-      return x + vec[(m / div - bm / div) * kEVecStride + (n - bn)] * (acc + vec[2 * kEVecStride + (n - bn)]);
+      return __builtin_fmaf(vec[(m / div - bm / div) * kEVecStride + (n - bn)], acc + vec[2 * kEVecStride + (n - bn)], x);
     }
-    return x + gate[so.get() + (size_t)(m / div) * ms + n] * (acc + b[n]);
+    return __builtin_fmaf(gate[so.get() + (size_t)(m / div) * ms + n], acc + b[n], x);
+  }
+  // four consecutive columns (n % 4 == 0), the staged gate and bias read as float4; value_v's expression per column
+  __device__ void value4_v(int m, int n, const float* acc, const float* st, const float* vec, bool use, int bm, int bn,
+                           const float* x, float* out) const {
+    if (!use) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[e] = value_v(m, n + e, acc[e], st, vec, use, bm, bn, x[e]);
+      return;
+    }
+    const float4 g = *reinterpret_cast<const float4*>(vec + (m / div - bm / div) * kEVecStride + (n - bn));
+    const float4 bb = *reinterpret_cast<const float4*>(vec + 2 * kEVecStride + (n - bn));
+    const float g4[4] = {g.x, g.y, g.z, g.w}, b4[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = __builtin_fmaf(g4[e], acc[e] + b4[e], x[e]);
   }
   __device__ void store(int m, int n, float v) const { store_val<XT>(X + (size_t)m * ld + n, v); }
   __device__ void store4(int m, int n, const float* v) const { store_val4<XT>(X + (size_t)m * ld + n, v); }
@@ -463,9 +514,28 @@ struct EpiLNFold {
       wa = f[0];
       wb = f[N];
     }
-    float v = rstd * (acc - mean * wa) + wb;
+    return fold_out(acc, mean, rstd, wa, wb);
+  }
+  // out = act(fma(rstd, fma(-mean, wa, acc), wb)): explicit roundings (staged and direct paths agree bitwise)
+  static __device__ __forceinline__ float fold_out(float acc, float mean, float rstd, float wa, float wb) {
+    float v = __builtin_fmaf(rstd, __builtin_fmaf(-mean, wa, acc), wb);
     if constexpr (ACT == 2) v = silu(v);
     return v;
+  }
+  // four consecutive columns (n % 4 == 0): the staged wa / wb rows read as float4
+  __device__ void value4_v(int m, int n, const float* acc, const float* st, const float* vec, bool use, int bm, int bn,
+                           const float*, float* out) const {
+    if (!use) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[e] = value_v(m, n + e, acc[e], st, vec, use, bm, bn);
+      return;
+    }
+    const float mean = st[2 * (m - bm)], rstd = st[2 * (m - bm) + 1];
+    const float* v = vec + 2 * (m / div - bm / div) * kEVecStride + (n - bn);
+    const float4 a = *reinterpret_cast<const float4*>(v), b = *reinterpret_cast<const float4*>(v + kEVecStride);
+    const float a4[4] = {a.x, a.y, a.z, a.w}, b4[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = fold_out(acc[e], mean, rstd, a4[e], b4[e]);
   }
   __device__ void store(int m, int n, float v) const { store_val<OT>(out + (size_t)m * ldo + n, v); }
   __device__ void store4(int m, int n, const float* v) const { store_val4<OT>(out + (size_t)m * ldo + n, v); }

@@ -454,7 +454,9 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
 
   // ---- epilogue, one 128-column half at a time through a 256 x 128 fp32 image
   float* ct = reinterpret_cast<float*>(smem);
-  auto cidx = [](int row, int col) __attribute__((always_inline)) { return row * 128 + (col ^ ((row & 3) << 4)); };
+  // 16-float column blocks XOR-swizzled by (row >> 2) & 3 = fq: a fragment write's four rows (4 fq + r) hit distinct
+  // banks (swizzling by row & 3, constant within one write, left it 4-way conflicted)
+  auto cidx = [](int row, int col) __attribute__((always_inline)) { return row * 128 + (col ^ (((row >> 2) & 3) << 4)); };
   constexpr bool PRE = kpre_of<EP>::value;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -489,12 +491,13 @@ __global__ __launch_bounds__(k8pThreads) void gemm8p_kernel(const void* __restri
         const float4 a4 = *reinterpret_cast<const float4*>(ct + cidx(row, c));
         const float av[4] = {a4.x, a4.y, a4.z, a4.w};
         float v[4];
+        if constexpr (PRE) {
+          value4_pre(ep, m, bnh + c, av, e_stats, e_vec, e_uv, bm, bnh, xr[u], v);
+        } else if constexpr (EV) {
+          value4_ev(ep, m, bnh + c, av, e_stats, e_vec, e_uv, bm, bnh, v);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = bnh + c + e;
-          if constexpr (PRE) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bnh, xr[u][e]);
-          else if constexpr (EV) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bnh);
-          else v[e] = ep.value(m, n, av[e], e_stats, bm);
+          for (int e = 0; e < 4; ++e) v[e] = ep.value(m, bnh + c + e, av[e], e_stats, bm);
         }
         if constexpr (kf8out_of<EP>::value) {  // MX-fp8 output: 8 lanes = one 32-column block of the row
           float am = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));

@@ -58,6 +58,33 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
+// Four consecutive columns of one row through a residual epilogue (kPre): value4_v when the epilogue has one (its
+// staged per-column vectors read as float4 -- four scalar reads at a 4-word lane stride are 2-way LDS bank conflicts),
+// else value_v per column.  value4_v evaluates each column with value_v's expression, so the results are the same.
+template <class T, class = void> struct has_value4 { static constexpr bool value = false; };
+template <class T> struct has_value4<T, std::void_t<decltype(&T::value4_v)>> { static constexpr bool value = true; };
+template <class EP>
+__device__ __forceinline__ void value4_pre(const EP& ep, int m, int n, const float* av, const float* st, const float* vec,
+                                           bool use, int bm, int bn, const float* x, float* v) {
+  if constexpr (has_value4<EP>::value) {
+    ep.value4_v(m, n, av, st, vec, use, bm, bn, x, v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = ep.value_v(m, n + e, av[e], st, vec, use, bm, bn, x[e]);
+  }
+}
+// ... and through an epilogue with staged per-column vectors but no residual (kEVec, no kPre: the LayerNorm fold)
+template <class EP>
+__device__ __forceinline__ void value4_ev(const EP& ep, int m, int n, const float* av, const float* st, const float* vec,
+                                          bool use, int bm, int bn, float* v) {
+  if constexpr (has_value4<EP>::value) {
+    ep.value4_v(m, n, av, st, vec, use, bm, bn, nullptr, v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = ep.value_v(m, n + e, av[e], st, vec, use, bm, bn);
+  }
+}
+
 // Four consecutive outputs of one row: the epilogue's own store4 when it has one, else four stores.
 template <class T, class = void> struct has_store4 { static constexpr bool value = false; };
 template <class T>
@@ -318,11 +345,12 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
 
   if constexpr (SM::VEPI) {
     // ---- row-vectorised epilogue: accumulators -> fp32 tile image in LDS (16-float column blocks
-    // XOR-swizzled by row & 3, so a fragment write's four rows hit distinct banks), then each thread
-    // handles 16 x (one row, 4 consecutive columns): 16-B residual loads / stores, row statistics over
-    // a half-wave per row.
+    // XOR-swizzled by (row >> 2) & 3: the four rows of one fragment write are 4 fq + r for a fixed r, so they
+    // differ in bits 2..3 -- the round-5 swizzle by row & 3 was constant within a write and left it 4-way
+    // bank-conflicted), then each thread handles 16 x (one row, 4 consecutive columns): 16-B residual loads /
+    // stores, row statistics over a half-wave per row.
     float* ct = reinterpret_cast<float*>(smem);
-    auto cidx = [](int row, int col) __attribute__((always_inline)) { return row * BN + (col ^ ((row & 3) << 4)); };
+    auto cidx = [](int row, int col) __attribute__((always_inline)) { return row * BN + (col ^ (((row >> 2) & 3) << 4)); };
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -351,12 +379,13 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
       const float4 a4 = *reinterpret_cast<const float4*>(ct + cidx(row, c));
       const float av[4] = {a4.x, a4.y, a4.z, a4.w};
       float v[4];
+      if constexpr (PRE) {
+        value4_pre(ep, m, bn + c, av, e_stats, e_vec, e_uv, bm, bn, xr[it], v);
+      } else if constexpr (EV) {
+        value4_ev(ep, m, bn + c, av, e_stats, e_vec, e_uv, bm, bn, v);
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = bn + c + e;
-        if constexpr (PRE) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bn, xr[it][e]);
-        else if constexpr (EV) v[e] = ep.value_v(m, n, av[e], e_stats, e_vec, e_uv, bm, bn);
-        else v[e] = ep.value(m, n, av[e], e_stats, bm);
+        for (int e = 0; e < 4; ++e) v[e] = ep.value(m, bn + c + e, av[e], e_stats, bm);
       }
       if constexpr (EP::kRowStats) {
         float sum = (v[0] + v[1]) + (v[2] + v[3]);

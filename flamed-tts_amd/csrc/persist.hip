@@ -256,7 +256,11 @@ __device__ __forceinline__ void dma_panel4(char* dst, const void* base, RowB row
 
 // ---- one GEMM phase: wave w < ntile computes rows [16 w, 16 w + 16) of the group's tile x the slot's 32
 // columns: A (bf16 rows, K) straight to registers with sc1 loads (rows >= nr read as 0: buffer range),
-// B fragments from the LDS weight panel.
+// B fragments from the LDS weight panel.  The MFMA takes the weight fragment as its A operand and the activation
+// fragment as its B operand (D = W . A^T), so lane (c, q) ends up holding TRANSPOSED output: acc[nt][r] = row c of
+// the tile, column 16 nt + 4 q + r -- one row and 4 consecutive columns per 16-column half, the consumer's fragment
+// order in 8-byte pieces (store_op_t), so no epilogue stages through LDS.  Same products, same K order: swapping
+// the operands changes only where the results land.
 // Fragment-major A image (persist_opt 64): group g's rows as [tile t < 4][K-step ks][lane][8 bf16], lane =
 // (row c, K-quarter q) exactly as a v_mfma_f32_16x16x32_bf16 A operand takes it, so a wave's 16-B/lane load
 // of one K-step is ONE contiguous 1 KB (8 full lines) instead of 16 half-lines of 16 rows; rows past the
@@ -314,8 +318,8 @@ __device__ __forceinline__ void gemm(const bf16* A, int r0, int nr, const char* 
         b0[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (ks + kBP) + q));
         b1[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (ks + kBP) + q));
       }
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, x0), acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[ks]), __builtin_bit_cast(bf16x8, x1), acc[1], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0), __builtin_bit_cast(bf16x8, a[ks]), acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1), __builtin_bit_cast(bf16x8, a[ks]), acc[1], 0, 0, 0);
     }
   }
 }
@@ -381,8 +385,8 @@ __device__ __forceinline__ void gemm_multi(const bf16* A, int r0, int nr, const 
           b1[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (k0 + ks + kBP) + q));
         }
         const u32x4 av = a[u & 1][ks];
-        ac[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, x0), ac[0], 0, 0, 0);
-        ac[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, x1), ac[1], 0, 0, 0);
+        ac[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0), __builtin_bit_cast(bf16x8, av), ac[0], 0, 0, 0);
+        ac[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1), __builtin_bit_cast(bf16x8, av), ac[1], 0, 0, 0);
       }
     }
   }
@@ -447,12 +451,12 @@ __device__ __forceinline__ void gemm_kh(const bf16* A, int r0, int nr, char* wl,
       b1[kk % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (k0 + kk + kBP) + q));
     }
     if (use0) {
-      p[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[0][kk]), __builtin_bit_cast(bf16x8, x0), p[0][0], 0, 0, 0);
-      p[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[0][kk]), __builtin_bit_cast(bf16x8, x1), p[0][1], 0, 0, 0);
+      p[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0), __builtin_bit_cast(bf16x8, a[0][kk]), p[0][0], 0, 0, 0);
+      p[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1), __builtin_bit_cast(bf16x8, a[0][kk]), p[0][1], 0, 0, 0);
     }
     if (use1) {
-      p[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[1][kk]), __builtin_bit_cast(bf16x8, x0), p[1][0], 0, 0, 0);
-      p[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[1][kk]), __builtin_bit_cast(bf16x8, x1), p[1][1], 0, 0, 0);
+      p[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0), __builtin_bit_cast(bf16x8, a[1][kk]), p[1][0], 0, 0, 0);
+      p[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1), __builtin_bit_cast(bf16x8, a[1][kk]), p[1][1], 0, 0, 0);
     }
   }
   __syncthreads();  // every wave has read the panel: its buffer now carries the partials
@@ -472,28 +476,89 @@ __device__ __forceinline__ void gemm_kh(const bf16* A, int r0, int nr, char* wl,
   }
 }
 
-// LayerNorm partials (mean, M2 over the slot's 32 columns) of the wave's 16 rows, from the MFMA layout
-// (lane c, q holds rows 4q + i, columns c and 16 + c): write-through 8-B stores.
-__device__ __forceinline__ void store_partials(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int tile, int lane_in,
-                                               bool local = false) {
+// LayerNorm partials (mean, M2 over the slot's 32 columns) of row 16 tile + c, from the transposed accumulator
+// layout (lane (c, q): columns 16 nt + 4 q + r): 8 values per lane, summed over the row's four q lanes (c, c + 16,
+// c + 32, c + 48; ((s0 + s1) + (s2 + s3)) in every lane, by commutativity), two passes; write-through 8-B store.
+__device__ __forceinline__ void store_partials_t(float2* xpart, const float (&x)[2][4], int r0, int nr, int s, int tile, int lane_in) {
   const int lane = opq(lane_in);
   const int c = lane & 15, q = lane >> 4;
+  float sm = ((x[0][0] + x[0][1]) + (x[0][2] + x[0][3])) + ((x[1][0] + x[1][1]) + (x[1][2] + x[1][3]));
+  sm += __shfl_xor(sm, 16);
+  sm += __shfl_xor(sm, 32);
+  const float mean = sm * (1.0f / kCols);
+  float m2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float sm = wave_sum16(x[0][i] + x[1][i]);
-    const float mean = sm * (1.0f / kCols);
-    const float d0 = x[0][i] - mean, d1 = x[1][i] - mean;
-    const float m2 = wave_sum16(d0 * d0 + d1 * d1);
-    const int row = 16 * tile + 4 * q + i;
-    if (c == 0 && row < nr) {
-      const float2 v = make_float2(mean, m2);
-      if (local)
-        xpart[(size_t)(r0 + row) * kSlots + s] = v;
-      else
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(xpart + (size_t)(r0 + row) * kSlots + s),
-                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = x[nt][r] - mean;
+      m2 = fmaf(d, d, m2);
     }
+  m2 += __shfl_xor(m2, 16);
+  m2 += __shfl_xor(m2, 32);
+  const int row = 16 * tile + c;
+  if (q == 0 && row < nr)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(xpart + (size_t)(r0 + row) * kSlots + s),
+                       __builtin_bit_cast(unsigned long long, make_float2(mean, m2)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+// The lane's two 4-column pieces of row 16 tile + c (transposed layout), bf16, written through straight from the
+// registers: fragment-major (frag: group g's [tile][K-step s][lane' = row + 16 (2 nt + q / 2)][8 bf16], byte 8 (q & 1)
+// of the 16-B piece; rows >= nr as zeros) or row-major (T x H, rows >= nr not stored).
+__device__ __forceinline__ void store_op_t(bf16* dst, int g, int s, int tile, const float (&v)[2][4], int r0, int nr,
+                                           int col0, int TT, int lane_in, bool frag) {
+  constexpr int KST = kH / 32;
+  const int lane = opq(lane_in);
+  const int c = lane & 15, q = lane >> 4;
+  const int row = 16 * tile + c;
+  const bool live = row < nr;
+  u32x2 piece[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const bf16x4 b = {(bf16)v[nt][0], (bf16)v[nt][1], (bf16)v[nt][2], (bf16)v[nt][3]};
+    piece[nt] = live ? __builtin_bit_cast(u32x2, b) : u32x2{0u, 0u};
   }
+  if (frag) {
+    const __amdgpu_buffer_rsrc_t rs =
+        rsrc(reinterpret_cast<char*>(dst) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST));
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const unsigned off = (unsigned)(((tile * KST + s) * 64 + c + 16 * (2 * nt + (q >> 1))) * 16 + (q & 1) * 8);
+      __builtin_amdgcn_raw_buffer_store_b64(piece[nt], rs, off, 0, 16);
+    }
+  } else if (live) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(dst, (unsigned)TT * kH * 2);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      __builtin_amdgcn_raw_buffer_store_b64(piece[nt], rs, (unsigned)(((size_t)(r0 + row) * kH + col0 + 16 * nt + 4 * q) * 2), 0, 16);
+  }
+}
+
+// The fp32 residual rows other groups read: only the kHalo rows at each end of the group (the depthwise halo of its
+// neighbours), two 16-B write-through stores per lane straight from the transposed registers; the middle rows never
+// leave the workgroup.
+__device__ __forceinline__ void store_halo_t(float* ximg, const float (&x)[2][4], int r0, int nr, int col0, int tile, int TT,
+                                             int lane_in) {
+  const int lane = opq(lane_in);
+  const int c = lane & 15, q = lane >> 4;
+  const int row = 16 * tile + c;
+  if (row < nr && (row < kHalo || row >= nr - kHalo)) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc(ximg, (unsigned)TT * kH * 4);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      st16(rs, (unsigned)(((size_t)(r0 + row) * kH + col0 + 16 * nt + 4 * q) * 4),
+           __builtin_bit_cast(u32x4, make_float4(x[nt][0], x[nt][1], x[nt][2], x[nt][3])));
+  }
+}
+
+// Column vector p[16 nt + 4 q + r] of the lane's columns (transposed layout)
+__device__ __forceinline__ void ld_cols(float (&v)[2][4], const float* p, int q) {
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[nt][r] = p[16 * nt + 4 * q + r];
 }
 
 // (mean, rstd) of rows [ra, rb) from the 32 slots' partials (sc1 loads), into st[2 (r - rbase)]; two
@@ -529,20 +594,8 @@ __device__ __forceinline__ void row_stats(const float2* xpart, int T, int ra, in
   }
 }
 
-// Stage the wave's (16 rows x 32 columns) values in LDS (row-major [64][32] of OT) ...
-template <typename OT>
-__device__ __forceinline__ void stage_tile(char* stg, const float (&v)[2][4], int wave, int lane_in) {
-  const int lane = opq(lane_in);
-  const int c = lane & 15, q = lane >> 4;
-  OT* t = reinterpret_cast<OT*>(stg);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 16 * wave + 4 * q + i;
-    t[row * kCols + c] = (OT)v[0][i];
-    t[row * kCols + 16 + c] = (OT)v[1][i];
-  }
-}
-// ... then write it through with 16-B sc1 stores (rows [ra, rb) of the tile) into dst (row stride ld).
+// A staged tile (the GroupNorm apply's bf16 rows: thread -> channel, not an MFMA layout) written through with 16-B sc1
+// stores (rows [ra, rb) of the tile) into dst (row stride ld).
 // Each wave writes the rows it staged itself ([16 w, 16 w + 16) of the chunk), so a stage -> flush pair needs no
 // workgroup barrier (persist_opt 32768: the wave's own LDS writes are ordered before its reads).
 template <typename OT>
@@ -574,18 +627,6 @@ __device__ __forceinline__ void flush_frag(const char* stg, bf16* dst, int g, in
     if (local) st16p(rs, off, v);
     else st16(rs, off, v);
   }
-}
-
-// The fp32 residual rows other groups read: only the kHalo rows at each end of a group (the depthwise
-// halo of its neighbours), written through; the middle rows never leave the workgroup's registers.  The staged
-// chunk holds the group's rows [c0, c0 + nrc) (chunk-local row = group row - c0).
-__device__ __forceinline__ void flush_halo(const char* stg, float* ximg, int r0, int nr, int col0, int T, int c0 = 0,
-                                           int nrc = -1) {
-  if (nrc < 0) nrc = nr;
-  const int a1 = min(c0 + nrc, kHalo);  // the group's first kHalo rows inside this chunk: [c0, a1)
-  if (a1 > c0) flush_tile<float>(stg, ximg, kH, r0 + c0, 0, a1 - c0, col0, T);
-  const int b0 = max(c0, max(nr - kHalo, kHalo)), b1 = c0 + nrc;  // its last kHalo rows (not written above)
-  if (b1 > b0) flush_tile<float>(stg, ximg, kH, r0 + c0, b0 - c0, b1 - c0, col0, T);
 }
 
 __device__ __forceinline__ void acc_to(float (&v)[2][4], const f32x4 (&acc)[2]) {
@@ -872,7 +913,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     pst_k = 0;
 #endif
     // ------------------------------ proj_in (:361) ------------------------------
-    const float binv[2] = {P.bin[col0 + c], P.bin[col0 + 16 + c]};
+    float binv[2][4];  // epilogue vectors of the lane's columns (transposed layout), before the wait
+    ld_cols(binv, P.bin + col0, q);
     PST(step);
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
@@ -890,12 +932,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) X[ci][nt][i] += binv[nt];
-      if (16 * tl < nr) store_partials(P.xpart[0], X[ci], r0, nr, s, tl, lane);
-      if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
-      stage_tile<float>(stg, X[ci], wave, lane);
-      stage_sync();
-      flush_halo(stg, P.ximg, r0, nr, col0, TT, kChunk * ci, crows(ci));
+        for (int i = 0; i < 4; ++i) X[ci][nt][i] += binv[nt][i];
+      if (16 * tl < nr) {
+        store_partials_t(P.xpart[0], X[ci], r0, nr, s, tl, lane);
+        store_halo_t(P.ximg, X[ci], r0, nr, col0, tl, TT, lane);
+      }
     }
     seal_put();
     if (dmafirst) {
@@ -920,7 +961,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       const int cc = tid & 31, rg = tid >> 5;
       // raw loads only before the wait (the arithmetic that consumes them after it: computed here, the compiler
       // put the loads' wait ahead of the poll instead of behind it)
-      float hsc[4], hsh[4], hlw[4], hlb[4], osc[2], osh[2], olw[2], olb[2];
+      float hsc[4], hsh[4], hlw[4], hlb[4], osc[2][4], osh[2][4], olw[2][4], olb[2][4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int col = col0 + 4 * (tid & 7) + e;
@@ -930,13 +971,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         hlb[e] = fin ? 0.0f : bw.lnb[col];
       }
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = col0 + 16 * nt + c;
-        osc[nt] = mb[H + col];
-        osh[nt] = mb[col];
-        olw[nt] = fin ? 1.0f : bw.lnw[col];
-        olb[nt] = fin ? 0.0f : bw.lnb[col];
-      }
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // the lane's own columns (transposed layout)
+          const int col = col0 + 16 * nt + 4 * q + r;
+          osc[nt][r] = mb[H + col];
+          osh[nt][r] = mb[col];
+          olw[nt][r] = fin ? 1.0f : bw.lnw[col];
+          olb[nt][r] = fin ? 0.0f : bw.lnb[col];
+        }
       float w[kTaps];
 #pragma unroll
       for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col0 + cc];
@@ -950,7 +993,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
       // va = w (1 + sc), vb = b (1 + sc) + sh (vab's arithmetic; w = 1, b = 0 without the affine)
-      float hva[4], hvb[4], ova[2], ovb[2];
+      float hva[4], hvb[4], ova[2][4], ovb[2][4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float sc1 = 1.0f + hsc[e];
@@ -958,11 +1001,13 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         hvb[e] = fin ? hsh[e] : hlb[e] * sc1 + hsh[e];
       }
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const float sc1 = 1.0f + osc[nt];
-        ova[nt] = fin ? sc1 : olw[nt] * sc1;
-        ovb[nt] = fin ? osh[nt] : olb[nt] * sc1 + osh[nt];
-      }
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sc1 = 1.0f + osc[nt][r];
+          ova[nt][r] = fin ? sc1 : olw[nt][r] * sc1;
+          ovb[nt][r] = fin ? osh[nt][r] : olb[nt][r] * sc1 + osh[nt][r];
+        }
       const int wa = max(r0 - kHalo, ub), wz = min(r0 + nr + kHalo, ue);  // the utterance's frames only
       // Everything this phase reads that does not wait on another phase goes out first, so the loads'
       // latencies overlap: the thread's halo item (its 4 columns col0 + 4 (tid & 7)), their modulation vectors,
@@ -997,23 +1042,25 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
               o.z = ((hv.z - mean) * rstd) * hva[2] + hvb[2];
               o.w = ((hv.w - mean) * rstd) * hva[3] + hvb[3];
             }
-            *reinterpret_cast<float4*>(hs + pw * kCols + 4 * (tid & 7)) = o;
+            *reinterpret_cast<float4*>(hs + pw * kHsLd + 4 * (tid & 7)) = o;
           }
         }
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
           const int tb = 16 * (wave + 4 * j);  // first row of this wave's tile j
           if (tb < nr && tb + 16 > c0 - kHalo && tb < c0 + kChunk + kHalo) {
+            const int row = tb + c, pw = row - c0 + kHalo;  // the lane's row, 4 consecutive columns per half
+            if (row < nr && pw >= 0 && pw < kWin) {
+              const int p = row + kHalo;
+              const float mean = st[2 * p], rstd = st[2 * p + 1];
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
+              for (int nt = 0; nt < 2; ++nt) {
+                float o[4];
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int row = tb + 4 * q + i, pw = row - c0 + kHalo;
-                if (row < nr && pw >= 0 && pw < kWin) {
-                  const int p = row + kHalo;
-                  hs[pw * kCols + 16 * nt + c] = ((X[j][nt][i] - st[2 * p]) * st[2 * p + 1]) * ova[nt] + ovb[nt];
-                }
+                for (int r = 0; r < 4; ++r) o[r] = ((X[j][nt][r] - mean) * rstd) * ova[nt][r] + ovb[nt][r];
+                *reinterpret_cast<float4*>(hs + pw * kHsLd + 16 * nt + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
               }
+            }
           }
         }
         __syncthreads();
@@ -1021,7 +1068,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         {
           float win[8 + kTaps - 1];
 #pragma unroll
-          for (int j = 0; j < 8 + kTaps - 1; ++j) win[j] = hs[(8 * rg + j) * kCols + cc];
+          for (int j = 0; j < 8 + kTaps - 1; ++j) win[j] = hs[(8 * rg + j) * kHsLd + cc];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             float a = dbias;
@@ -1180,7 +1227,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       ++L;
 
       // -------- conv_2 (1x1) + GELU (:90-91)
-      const float b2v[2] = {bw.b2[col0 + c], bw.b2[col0 + 16 + c]};  // epilogue vectors before the wait
+      float b2v[2][4];  // epilogue vectors before the wait
+      ld_cols(b2v, bw.b2 + col0, q);
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
@@ -1192,24 +1240,28 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
+        const int tl = wave + 4 * ci;
         const f32x4(&acc)[2] = accm_c2[ci];
         float v[2][4];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b2v[nt]);
+          for (int i = 0; i < 4; ++i) v[nt][i] = gelu_fast(acc[nt][i] + b2v[nt][i]);
         }
-        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
-        stage_tile<bf16>(stg, v, wave, lane);
-        stage_sync();
-        if (frag) flush_frag(stg, P.u, g, s, crows(ci), kH / 32, xloc, 4 * ci);
-        else flush_tile<bf16>(stg, P.u, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
+        if (16 * tl < nr) store_op_t(P.u, g, s, tl, v, r0, nr, col0, TT, lane, frag);
+        if (ci == 0) PST(step);  // (FL_STAMPS: the conv_2 epilogue broken down -- hand-off stores issued)
       }
       seal_put();
       if (dmafirst) {
         next_w(bw.w3);
         signal_dma<16>(mygrp);
       } else {
+#ifdef FL_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PST(step);  // wave 0's hand-off stores acknowledged
+        __syncthreads();
+        PST(step);  // every wave's
+#endif
         signal(mygrp);
         next_w(bw.w3);
       }
@@ -1217,15 +1269,17 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       ++L;
 
       // -------- conv_3 (1x1) + ConvNeXt residual + gated residual (:92-93, 109, 156); x * alpha for the fold
-      float g3[2], b3v[2], alv[2];  // (ova / ovb of the dwconv phase are this epilogue's LN vectors)
+      float g3[2][4], b3v[2][4], alv[2][4];  // (ova / ovb of the dwconv phase are this epilogue's LN vectors)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = col0 + 16 * nt + c;
-        g3[nt] = mb[2 * H + col];
-        b3v[nt] = bw.b3[col];
-        // alpha = w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second)
-        alv[nt] = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
-      }
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = col0 + 16 * nt + 4 * q + r;
+          g3[nt][r] = mb[2 * H + col];
+          b3v[nt][r] = bw.b3[col];
+          // alpha = w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second)
+          alv[nt][r] = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
+        }
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
@@ -1240,23 +1294,22 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         const int tl = wave + 4 * ci;
         const f32x4(&acc)[2] = accm_c3[ci];
         float v[2][4];
+        const int p = 16 * tl + c + kHalo;  // the lane's row (transposed layout)
+        const float mean = st[2 * p], rstd = st[2 * p + 1];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int p = 16 * tl + 4 * q + i + kHalo;
-            const float xh = (X[ci][nt][i] - st[2 * p]) * st[2 * p + 1];
-            const float h = xh * ova[nt] + ovb[nt];
-            X[ci][nt][i] = X[ci][nt][i] + g3[nt] * (h + (acc[nt][i] + b3v[nt]));
-            v[nt][i] = X[ci][nt][i] * alv[nt];
+            const float xh = (X[ci][nt][i] - mean) * rstd;
+            const float h = xh * ova[nt][i] + ovb[nt][i];
+            X[ci][nt][i] = X[ci][nt][i] + g3[nt][i] * (h + (acc[nt][i] + b3v[nt][i]));
+            v[nt][i] = X[ci][nt][i] * alv[nt][i];
           }
         }
-        if (16 * tl < nr) store_partials(P.xpart[1], X[ci], r0, nr, s, tl, lane, xloc);
-        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
-        stage_tile<bf16>(stg, v, wave, lane);
-        stage_sync();
-        if (frag) flush_frag(stg, P.xa, g, s, crows(ci), kH / 32, xloc, 4 * ci);
-        else flush_tile<bf16>(stg, P.xa, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
+        if (16 * tl < nr) {
+          store_partials_t(P.xpart[1], X[ci], r0, nr, s, tl, lane);
+          store_op_t(P.xa, g, s, tl, v, r0, nr, col0, TT, lane, frag);
+        }
       }
       seal_put();
       if (dmafirst) {
@@ -1274,7 +1327,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
       // -------- mlp.0 + SiLU, the LayerNorm folded into the epilogue (:157-158)
       const float* fo0 = md + P.MS0 + (size_t)blk * 2 * H;  // [W alpha, W beta + b] of this modulation row
-      const float fa0[2] = {fo0[col0 + c], fo0[col0 + 16 + c]}, fb0[2] = {fo0[H + col0 + c], fo0[H + col0 + 16 + c]};
+      float fa0[2][4], fb0[2][4];
+      ld_cols(fa0, fo0 + col0, q);
+      ld_cols(fb0, fo0 + H + col0, q);
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
@@ -1290,19 +1345,14 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         const int tl = wave + 4 * ci;
         const f32x4(&acc)[2] = accm_m0[ci];
         float v[2][4];
+        const int p = 16 * tl + c + kHalo;  // the lane's row (transposed layout)
+        const float mean = st[2 * p], rstd = st[2 * p + 1];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int p = 16 * tl + 4 * q + i + kHalo;
-            v[nt][i] = silu(st[2 * p + 1] * (acc[nt][i] - st[2 * p] * fa0[nt]) + fb0[nt]);
-          }
+          for (int i = 0; i < 4; ++i) v[nt][i] = silu(rstd * (acc[nt][i] - mean * fa0[nt][i]) + fb0[nt][i]);
         }
-        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
-        stage_tile<bf16>(stg, v, wave, lane);
-        stage_sync();
-        if (frag) flush_frag(stg, P.u, g, s, crows(ci), kH / 32, xloc, 4 * ci);
-        else flush_tile<bf16>(stg, P.u, H, r0 + kChunk * ci, 0, crows(ci), col0, TT, xloc);
+        if (16 * tl < nr) store_op_t(P.u, g, s, tl, v, r0, nr, col0, TT, lane, frag);
       }
       seal_put();
       if (dmafirst) {
@@ -1316,7 +1366,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       ++L;
 
       // -------- mlp.2 + gated residual (:159-160)
-      const float g2v[2] = {mb[5 * H + col0 + c], mb[5 * H + col0 + 16 + c]}, bm2[2] = {bw.mb2[col0 + c], bw.mb2[col0 + 16 + c]};
+      float g2v[2][4], bm2[2][4];
+      ld_cols(g2v, mb + 5 * H + col0, q);
+      ld_cols(bm2, bw.mb2 + col0, q);
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
@@ -1333,12 +1385,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) X[ci][nt][i] = X[ci][nt][i] + g2v[nt] * (acc[nt][i] + bm2[nt]);
-        if (16 * tl < nr) store_partials(P.xpart[0], X[ci], r0, nr, s, tl, lane);
-        if (ci > 0) stage_sync();  // the previous chunk's rows have left the staging tile
-        stage_tile<float>(stg, X[ci], wave, lane);
-        stage_sync();
-        flush_halo(stg, P.ximg, r0, nr, col0, TT, kChunk * ci, crows(ci));
+          for (int i = 0; i < 4; ++i) X[ci][nt][i] = X[ci][nt][i] + g2v[nt][i] * (acc[nt][i] + bm2[nt][i]);
+        if (16 * tl < nr) {
+          store_partials_t(P.xpart[0], X[ci], r0, nr, s, tl, lane);
+          store_halo_t(P.ximg, X[ci], r0, nr, col0, tl, TT, lane);
+        }
       }
       seal_put();
       if (dmafirst) {
@@ -1355,16 +1406,18 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     // -------- conv_out k3 (taps stacked; LayerNorm + modulate folded; :238-245, 264).  Panel row n < 24 is
     // tap n / 8 of latent channel 8 s + n % 8; rows 24..31 repeat rows 0..7 (ignored)
     wb ^= 1;  // conv_out's panel was issued behind the FinalLayer's conv_3
-    float fac[2], fbc[2];  // fold vectors of the lane's stacked columns, before the wait
+    float fac[2][4], fbc[2][4];  // fold vectors of the lane's stacked columns (transposed layout), before the wait
     {
       const float* fo = md + P.MS0 + (size_t)P.NB * 2 * H;  // [wa (3 C), wb (3 C)]
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int n = 16 * nt + c, m = n < 24 ? n : n - 24;
-        const int ns = (m >> 3) * kC + kCh * s + (m & 7);  // stacked output column
-        fac[nt] = fo[ns];
-        fbc[nt] = fo[3 * kC + ns];
-      }
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * nt + 4 * q + r, m = n < 24 ? n : n - 24;
+          const int ns = (m >> 3) * kC + kCh * s + (m & 7);  // stacked output column
+          fac[nt][r] = fo[ns];
+          fbc[nt][r] = fo[3 * kC + ns];
+        }
     }
     PST(step);
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
@@ -1383,14 +1436,17 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (NTW > 1) __syncthreads();  // every wave is done with the panel
 #pragma unroll
     for (int ci = 0; ci < NTW; ++ci) {
+      const int row = 16 * (wave + 4 * ci) + c, p = row + kHalo;  // the lane's row (transposed layout)
+      if (NTW == 1 || row < nr) {
+        const float mean = st[2 * p], rstd = st[2 * p + 1];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int n = 16 * nt + c;
-        if (n < 24) {
+        for (int nt = 0; nt < 2; ++nt) {
+          const int n0 = 16 * nt + 4 * q;  // the lane's 4 stacked columns (n >= 24 repeat 0..7: not stored)
+          if (n0 < 24) {
+            float y[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int row = 16 * (wave + 4 * ci) + 4 * q + i, p = row + kHalo;
-            if (NTW == 1 || row < nr) yl[row * 24 + n] = st[2 * p + 1] * (acco[ci][nt][i] - st[2 * p] * fac[nt]) + fbc[nt];
+            for (int i = 0; i < 4; ++i) y[i] = rstd * (acco[ci][nt][i] - mean * fac[nt][i]) + fbc[nt][i];
+            *reinterpret_cast<float4*>(yl + row * 24 + n0) = make_float4(y[0], y[1], y[2], y[3]);
           }
         }
       }

@@ -49,8 +49,12 @@ constexpr int kMaxNB = 8, kMaxT = kGroups * kMaxRows;
 // LDS carve (bytes): two weight panels, the dwconv window (aliased by the epilogue staging tile), row
 // statistics of the window, GroupNorm reduction scratch, poll flag
 constexpr int kWPanel = kCols * kH * 2;
+// dwconv window rows are padded to 36 floats: the transposed epilogue layout writes a lane's row as float4 pieces, and
+// with a 32-float stride the 16 rows of one write would share 2 bank groups; at 36 they hit 16 distinct ones (and the
+// depthwise conv's two rows per wave, 8 apart, fall in opposite bank halves)
+constexpr int kHsLd = kCols + 4;
 constexpr int L_HS = 2 * kWPanel;
-constexpr int L_ST = L_HS + kWin * kCols * 4;
+constexpr int L_ST = L_HS + kWin * kHsLd * 4;
 constexpr int L_RED = L_ST + (kMaxRows + 2 * kHalo) * 8;  // row statistics of the whole group window
 constexpr int L_GNV = L_RED + 8 * kCols * 4;
 constexpr int L_FLAG = L_GNV + kCols * 16;

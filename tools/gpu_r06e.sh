@@ -1,5 +1,5 @@
 bash tools/gpu_steps.sh r06e \
- configs 900 "python -u -m pytest tests/test_configs_gpu.py -x -v --timeout 300 --timeout-method thread -m gpu -k 'concurrent or split_batch'" \
+ timeline 300 "python -u tools/persist_timeline.py --frames 400 --nfe 16 --step 5 --out gpurun_out/r06e/timeline_T400.txt" \
  pmc_b1 900 "bash tools/pmc_mfma.sh r06e_b1" \
  pmc_b64 900 "bash tools/pmc_mfma.sh r06e_b64 --batch 64" \
- pmc_fp8 900 "bash tools/pmc_mfma.sh r06e_fp8 --config 4"
+ pmc_fp8 900 "bash tools/pmc_mfma.sh r06e_fp8 --config 4 --nfe 8"
