@@ -184,9 +184,11 @@ struct Tune {
   int persist_pad = 1;     // persistent solve for B = 3 / 5..7 as B = 4 / 8 with idle utterances (persist_batch)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
-  int persist_multi_ntw = 2;  // ... and for B > 1 up to this many: beyond 2 chunks the graph of launches is faster
-                           // (r06c: B = 4 T = 400, 4 chunks: 60.4 ms persistent vs 47.5 for B = 3 on the graph; B = 2
-                           // T = 400, 2 chunks: 31.4 vs 37.7); B = 1 keeps 5 (long-form T = 2400: 152.6 vs 184 ms)
+  int persist_multi_ntw = 5;  // ... and for B > 1 up to this many (A/B knob).  r06c, with the round-5 epilogues, had the
+                           // graph of launches ahead beyond 2 chunks (B = 4 T = 400: 60.4 ms persistent); with the
+                           // transposed register epilogues (r06i) the persistent launch wins at every multi-chunk shape
+                           // measured: B = 4 T = 400 47.4 vs 76.1 ms, B = 4 T = 300 38.6 vs 45.5, B = 8 T = 320 61.9 vs
+                           // 77.3, B = 2 T = 1000 51.7 vs 76.0; B = 3 T = 400 (padded to 4) 47.5 vs 46.6
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
   int persist_opt = 361034;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange

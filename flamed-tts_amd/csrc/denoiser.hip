@@ -2604,6 +2604,8 @@ static int persist_solve(Den* d, float* xt, const float* mods, int nfe, int B, i
   P.T = T; P.B = Bp; P.Bx = Bp != B ? B : 0; P.NB = d->NB; P.s0 = s0; P.s1 = s1;
   P.dt = (float)(1.0 / (double)nfe);
   P.mods = mods; P.MS = d->MS; P.MS0 = d->MS0;
+  // the kernel reads modulation rows as 16-B vectors (persist.hip ld_cols)
+  FL_REQUIRE(P.MS % 4 == 0 && P.MS0 % 4 == 0 && ((uintptr_t)mods & 15) == 0, "persistent solve: modulation rows not 16-B aligned");
   P.win = reinterpret_cast<const bf16*>(d->win); P.bin = d->bin;
   for (int i = 0; i <= d->NB; ++i) {
     const DenBlockW& b = i < d->NB ? d->blk[i] : d->fin;

@@ -553,12 +553,20 @@ __device__ __forceinline__ void store_halo_t(float* ximg, const float (&x)[2][4]
   }
 }
 
-// Column vector p[16 nt + 4 q + r] of the lane's columns (transposed layout)
+// Column vector p[16 nt + 4 q + r] of the lane's columns (transposed layout): two 16-B loads (p 16-B aligned: the
+// weight arena, and modulation rows of MS floats, MS % 4 == 0 -- persist_solve checks it)
 __device__ __forceinline__ void ld_cols(float (&v)[2][4], const float* p, int q) {
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const float4 a = *reinterpret_cast<const float4*>(p + 16 * nt + 4 * q);
+    v[nt][0] = a.x; v[nt][1] = a.y; v[nt][2] = a.z; v[nt][3] = a.w;
+  }
+}
+__device__ __forceinline__ void fill_cols(float (&v)[2][4], float x) {
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[nt][r] = p[16 * nt + 4 * q + r];
+    for (int r = 0; r < 4; ++r) v[nt][r] = x;
 }
 
 // (mean, rstd) of rows [ra, rb) from the 32 slots' partials (sc1 loads), into st[2 (r - rbase)]; two
@@ -970,16 +978,15 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         hlw[e] = fin ? 1.0f : bw.lnw[col];
         hlb[e] = fin ? 0.0f : bw.lnb[col];
       }
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {  // the lane's own columns (transposed layout)
-          const int col = col0 + 16 * nt + 4 * q + r;
-          osc[nt][r] = mb[H + col];
-          osh[nt][r] = mb[col];
-          olw[nt][r] = fin ? 1.0f : bw.lnw[col];
-          olb[nt][r] = fin ? 0.0f : bw.lnb[col];
-        }
+      ld_cols(osc, mb + H + col0, q);  // the lane's own columns (transposed layout)
+      ld_cols(osh, mb + col0, q);
+      if (fin) {
+        fill_cols(olw, 1.0f);
+        fill_cols(olb, 0.0f);
+      } else {
+        ld_cols(olw, bw.lnw + col0, q);
+        ld_cols(olb, bw.lnb + col0, q);
+      }
       float w[kTaps];
 #pragma unroll
       for (int j = 0; j < kTaps; ++j) w[j] = bw.dww[(size_t)j * H + col0 + cc];
@@ -1269,20 +1276,22 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       ++L;
 
       // -------- conv_3 (1x1) + ConvNeXt residual + gated residual (:92-93, 109, 156); x * alpha for the fold
-      float g3[2][4], b3v[2][4], alv[2][4];  // (ova / ovb of the dwconv phase are this epilogue's LN vectors)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int col = col0 + 16 * nt + 4 * q + r;
-          g3[nt][r] = mb[2 * H + col];
-          b3v[nt][r] = bw.b3[col];
-          // alpha = w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second)
-          alv[nt][r] = fin ? 1.0f + mb[4 * H + col] : bw.lnmw[col] * (1.0f + mb[4 * H + col]);
-        }
+      // (ova / ovb of the dwconv phase are this epilogue's LN vectors); raw loads only before the wait: alpha =
+      // w (1 + scale) of the LayerNorm the next GEMM consumes (mlp / FinalLayer's second) is formed after it, or the
+      // compiler waits for these loads ahead of the poll
+      float g3[2][4], b3v[2][4], alv[2][4], alw[2][4];
+      ld_cols(g3, mb + 2 * H + col0, q);
+      ld_cols(b3v, bw.b3 + col0, q);
+      ld_cols(alv, mb + 4 * H + col0, q);
+      if (fin) fill_cols(alw, 1.0f);
+      else ld_cols(alw, bw.lnmw + col0, q);
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) alv[nt][r] = fin ? 1.0f + alv[nt][r] : alw[nt][r] * (1.0f + alv[nt][r]);
       f32x4 accm_c3[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
@@ -1333,6 +1342,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       PST(step);
       if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
+      // the epilogue's row statistics of x (conv_3's partials) before the GEMM (issued between the GEMM's A loads and
+      // their wait instead, r06j measured 20.84 vs 20.63 ms per B = 1 solve: slower)
       row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
       f32x4 accm_m0[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
@@ -1410,14 +1421,13 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     {
       const float* fo = md + P.MS0 + (size_t)P.NB * 2 * H;  // [wa (3 C), wb (3 C)]
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = 16 * nt + 4 * q + r, m = n < 24 ? n : n - 24;
-          const int ns = (m >> 3) * kC + kCh * s + (m & 7);  // stacked output column
-          fac[nt][r] = fo[ns];
-          fbc[nt][r] = fo[3 * kC + ns];
-        }
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = 16 * nt + 4 * q, m = n < 24 ? n : n - 24;  // 4 consecutive stacked columns from ns
+        const int ns = (m >> 3) * kC + kCh * s + (m & 7);
+        const float4 a = *reinterpret_cast<const float4*>(fo + ns), b = *reinterpret_cast<const float4*>(fo + 3 * kC + ns);
+        fac[nt][0] = a.x; fac[nt][1] = a.y; fac[nt][2] = a.z; fac[nt][3] = a.w;
+        fbc[nt][0] = b.x; fbc[nt][1] = b.y; fbc[nt][2] = b.z; fbc[nt][3] = b.w;
+      }
     }
     PST(step);
     if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }

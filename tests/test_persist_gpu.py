@@ -389,7 +389,7 @@ def test_persist_multi_counter_groupnorm(pgb, B, T, part):
     pg, sd = pgb
     x0, spk = _inputs(40 + B, B, T)
     base = PERSIST_DEFAULT ^ part
-    with knob("persist_multi", 1, 1), knob("persist_multi_ntw", 5, 2):
+    with knob("persist_multi", 1, 1), knob("persist_multi_ntw", 5, 5):
         with knob("persist_opt", base, PERSIST_DEFAULT):
             a = _solve(pg, x0, spk, 8)
         r0 = _runs(pg)
@@ -458,7 +458,7 @@ def test_persist_multi_chunk(pgb, B, T):
     pg, sd = pgb
     x0, spk = _inputs(50 + B + T, B, T)
     r0 = _runs(pg)
-    with knob("persist_multi_ntw", 5, 2):  # B > 1 beyond 2 chunks: the graph path is the default (faster), reach the kernel
+    with knob("persist_multi_ntw", 5, 5):  # (the default since r06i; pinned here)
         a = _solve(pg, x0, spk, 8)
         b = _solve(pg, x0, spk, 8)
     assert _runs(pg) == r0 + 2, "the multi-chunk solve did not take the persistent path"
@@ -480,7 +480,7 @@ def test_persist_multi_chunk_variants_bitwise(pgb, B, T):
     deferred seals (65536)."""
     pg, _ = pgb
     x0, spk = _inputs(61 + B, B, T)
-    with knob("persist_multi_ntw", 5, 2):
+    with knob("persist_multi_ntw", 5, 5):
         a = _solve(pg, x0, spk, 8)
         for flip in (64, 512, 32768, 262144, 65536):
             with knob("persist_opt", PERSIST_DEFAULT ^ flip, PERSIST_DEFAULT):
