@@ -458,6 +458,23 @@ def long_form(pg, dev, args, C, T=2400, nfe=256):
     return out
 
 
+def latest_mfma(workload, B, T, dtype, cls):
+    """Per-class MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)), MFMA FLOPs (512 x
+    SQ_INSTS_VALU_MFMA_MOPS_*) and HBM bytes of a rocprofv3 PMC run of this workload (tools/pmc_mfma.sh ->
+    profiles/latest_mfma.json), or None when the recorded run is of another shape."""
+    path = os.path.join(REPO, "profiles", "latest_mfma.json")
+    if not os.path.exists(path):
+        return None
+    w = json.load(open(path)).get(workload)
+    if not w or (w.get("batch"), w.get("frames"), w.get("dtype")) != (B, T, dtype):
+        return None
+    c = w["classes"]
+    if cls is not None:
+        return dict(c[cls], source=w["source"]) if cls in c else None
+    return {"source": w["source"], "classes": {k: {f: v[f] for f in ("mfma_util", "mfma_TFs", "mean_us", "hbm_GBps") if f in v}
+                                                for k, v in c.items() if v.get("mfma_util") or v.get("hbm_GBps", 0) > 500}}
+
+
 def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
     """BASELINE configs[2] on the same handle: B = 64 utterances x 400 frames, nfe-step graph solve (one
     timed solve after a warm one), with the in-graph per-class costs and the roofline of the dominant
@@ -503,6 +520,8 @@ def throughput_mode(pg, dev, nfe, args, H, C, NB, B=64, T=400):
         roof = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof.update({"frac": round(roof["achieved"] / roof["peak"], 4), "kernel": dom["name"], "launch_us": dom["us"],
                  "tflops": dom["TFLOPs"], "gbps": dom["GBps"]})
+    # the MFMA side from rocprofv3 counters of this workload (tools/pmc_mfma.sh): every large-M class
+    roof["mfma_pmc"] = latest_mfma("b64", B, T, args.dtype, None)
     # the same workload on an MX-fp8 handle (conv_2/conv_3/mlp.0/mlp.2 block-scaled e4m3 at 25,600 rows)
     fp8 = None
     if args.dtype == "bf16":
@@ -839,6 +858,7 @@ def main():
                 "traffic_source": "rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, profiles/latest_traffic.json"
                 if ptraffic is not None else None,
                 "algorithmic_bytes": lbytes, "algorithmic_flops": lflops, "tflops": round(lflops / (pk_ms * 1e-3) / 1e12, 2),
+                "mfma_pmc": latest_mfma("b1", B, T, args.dtype, "den_persist_kernel"),
                 "step": {"bytes_canonical": sbytes, "step_us": round(pk_ms * 1e3 / nfe, 2),
                          "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
                          "bytes_model": "W (bf16 GEMM weights + fp32 vectors/taps) + 54,272 B per frame"},

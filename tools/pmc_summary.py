@@ -9,7 +9,9 @@ duration (kernel trace), MFMA utilisation, MFMA FLOPs per launch, HBM bytes per 
   MFMA FLOPs = 512 x SQ_INSTS_VALU_MFMA_MOPS_{BF16,F8,F32} (rocprofv3's MFMA_FLOPS_* derivation).
   HBM bytes  = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; the x2 is the guide's gfx950 streaming-read correction).
 Counters come from separate runs (one group per pass), so each is averaged over the class's dispatches of its own run.
-Writes OUT/summary.md and OUT/summary.json.   python tools/pmc_summary.py gpurun_out/<tag>"""
+Writes OUT/summary.md and OUT/summary.json.   python tools/pmc_summary.py gpurun_out/<tag>
+  [--latest profiles/latest_mfma.json --workload b1 --batch 1 --frames 400 --dtype bf16 --source profiles/<name>]
+records the per-class MFMA utilisation / FLOPs / HBM bytes of that workload where bench.py reads them."""
 import csv
 import glob
 import importlib.util
@@ -86,5 +88,27 @@ def main(out):
     print("\n".join(lines))
 
 
+def update_latest(rows, path, workload, batch, frames, dtype, source):
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    keep = ("launches", "mean_us", "mfma_util", "mfma_TFs", "hbm_bytes_per_launch", "hbm_GBps", "lds_bank_conflict_frac",
+            "wait_any", "active_inst")
+    d[workload] = {"batch": batch, "frames": frames, "dtype": dtype, "source": source,
+                   "classes": {r["class"]: {k: r[k] for k in keep if r.get(k) is not None} for r in rows[:24]}}
+    json.dump(d, open(path, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--latest")
+    ap.add_argument("--workload")
+    ap.add_argument("--batch", type=int)
+    ap.add_argument("--frames", type=int)
+    ap.add_argument("--dtype")
+    ap.add_argument("--source")
+    a = ap.parse_args()
+    if a.latest:
+        update_latest(json.load(open(f"{a.out}/summary.json")), a.latest, a.workload, a.batch, a.frames, a.dtype, a.source)
+    else:
+        main(a.out)
