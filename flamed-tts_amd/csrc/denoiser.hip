@@ -10,6 +10,7 @@
 //   FinalLayer:   K2a, G1, G2 as above (no-affine LN), then conv_out k3 GEMM with the LN+modulate
 //                 gather prologue and the Euler update xt += dt*v fused in the epilogue.
 // AdaLN (depends only on t and the speaker) is precomputed for every (step, utterance) at once.
+#include <cstring>
 #include "flamed_hip.h"
 #include "flamed_diag.h"
 #include "gemm.hpp"
@@ -1759,6 +1760,7 @@ struct Den {
   static constexpr int kMaxParked = 8;
   hipStream_t parked[kMaxParked] = {};         // streams the queue probe found serialising with a chain's (kept alive)
   int n_parked = 0, qprobe_retries = 0;
+  int qprobe_busy = 0;  // probe pairs that neither ran concurrently nor back-to-back (the device was busy): not parked
   int* qprobe = nullptr;                       // probe flag + result words
   int g_B = -1, g_T = -1, g_nfe = -1, g_epoch = -1;
   const void *g_xt = nullptr, *g_mods = nullptr, *g_ws = nullptr;
@@ -2247,6 +2249,13 @@ FLAMED_API int flamed_den_ws_offsets(flamed_den_t h, int B, int T, size_t* off) 
 }
 
 // Diagnostic (include/flamed_diag.h): the split-chain stream probe's record (den_chain_streams).
+FLAMED_API int flamed_den_chain_busy(flamed_den_t h, int* busy) {
+  Den* d = reinterpret_cast<Den*>(h);
+  FL_REQUIRE(d && busy, "flamed_den_chain_busy: bad args");
+  *busy = d->qprobe_busy;
+  return kOk;
+}
+
 FLAMED_API int flamed_den_chain_info(flamed_den_t h, int* parked, int* retries) {
   Den* d = reinterpret_cast<Den*>(h);
   FL_REQUIRE(d && parked && retries, "flamed_den_chain_info: bad args");
@@ -2795,22 +2804,33 @@ FLAMED_API int flamed_den_solve(flamed_den_t h, float* xt, const float* mods, in
 
 // Hardware-queue probe for two streams: a one-lane kernel on stream a waits (bounded: 2 ms of s_memrealtime)
 // for a flag that a kernel on stream b sets.  If b's launch sits on a's hardware queue it cannot start until
-// a's kernel has timed out, and the pair is reported as serialising.
+// a's kernel has timed out, and the pair is reported as serialising.  Both kernels stamp s_memrealtime (the wait
+// kernel its start and end, the set kernel its start), so a pair that was not concurrent is told apart: the set
+// kernel starting within 50 us after the wait kernel ended is the queue's back-to-back dispatch (serialising);
+// any other timing means the device was busy (e.g. another handle's cooperative launch holding every CU) and the
+// result is inconclusive -- ADVICE r5.
 __global__ void qprobe_wait_kernel(int* w) {
   if (threadIdx.x != 0) return;
+  unsigned long long* ts = reinterpret_cast<unsigned long long*>(w + 4);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   int ok = 0;
   while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < 200000) {
     if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = 1; break; }
     __builtin_amdgcn_s_sleep(2);
   }
+  ts[0] = t0;
+  ts[1] = __builtin_amdgcn_s_memrealtime();
   __hip_atomic_store(w + 1, ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ void qprobe_set_kernel(int* w) {
-  if (threadIdx.x == 0) __hip_atomic_store(w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    reinterpret_cast<unsigned long long*>(w + 4)[2] = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_store(w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
-static int streams_concurrent(int* w, hipStream_t a, hipStream_t b, bool* conc) {
-  int h[2] = {0, 0};
+// *state: 0 concurrent, 1 serialising (back-to-back on one queue), 2 inconclusive (device busy)
+static int streams_concurrent(int* w, hipStream_t a, hipStream_t b, int* state) {
+  int h[10] = {};
   FL_HIP(hipMemcpy(w, h, sizeof(h), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(qprobe_wait_kernel, dim3(1), dim3(64), 0, a, w);
   FL_LAUNCH_CHECK();
@@ -2819,7 +2839,10 @@ static int streams_concurrent(int* w, hipStream_t a, hipStream_t b, bool* conc) 
   FL_HIP(hipStreamSynchronize(a));
   FL_HIP(hipStreamSynchronize(b));
   FL_HIP(hipMemcpy(h, w, sizeof(h), hipMemcpyDeviceToHost));
-  *conc = h[1] == 1;
+  unsigned long long ts[3];
+  memcpy(ts, h + 4, sizeof(ts));
+  const long long gap = (long long)(ts[2] - ts[1]);  // set start - wait end, 10 ns ticks
+  *state = h[1] == 1 ? 0 : (gap >= 0 && gap < 5000) ? 1 : 2;
   return kOk;
 }
 
@@ -2849,11 +2872,12 @@ static int den_chain_streams(Den* d, int S, hipStream_t st) {
       FL_HIP(hipStreamCreateWithPriority(&sk, hipStreamNonBlocking, pr));
       bool ok = true;
       for (int j = k0; probe && ok && j < k; ++j) {
-        bool c1 = false, c2 = false;
+        int c1 = 0, c2 = 0;
         const int rc1 = streams_concurrent(d->qprobe, d->run_aux[pm][j], sk, &c1);
         const int rc2 = rc1 ? rc1 : streams_concurrent(d->qprobe, sk, d->run_aux[pm][j], &c2);
         if (rc2) { (void)hipStreamDestroy(sk); return rc2; }
-        ok = c1 && c2;
+        if (c1 == 2 || c2 == 2) ++d->qprobe_busy;  // inconclusive: keep the stream (only a measured serialisation parks)
+        ok = c1 != 1 && c2 != 1;
       }
       if (ok || tries >= Den::kMaxParked || d->n_parked >= Den::kMaxParked) {
         d->run_aux[pm][k] = sk;

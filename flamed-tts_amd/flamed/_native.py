@@ -114,6 +114,7 @@ HIP_DIAG_SIGNATURES = {
     "flamed_den_ws_offsets": (c_int, [P, c_int, c_int, ctypes.POINTER(c_size_t)]),
     "flamed_persist_ticket": (c_int, [ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(c_int)]),
     "flamed_den_chain_info": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "flamed_den_chain_busy": (c_int, [P, ctypes.POINTER(c_int)]),
 }
 
 FLAMED_F32, FLAMED_BF16, FLAMED_FP8 = 0, 1, 2

@@ -78,6 +78,9 @@ FLAMED_API int flamed_persist_ticket(unsigned ticket, unsigned cur, unsigned* ta
 /* Split-chain replay streams of this handle: how many the hardware-queue probe parked (they serialised with an
  * earlier chain's stream) and how many re-creations it took in total. */
 FLAMED_API int flamed_den_chain_info(flamed_den_t h, int* parked, int* retries);
+/* ... and how many probe pairs were inconclusive (neither concurrent nor dispatched back-to-back: the device was busy);
+ * those never park a stream. */
+FLAMED_API int flamed_den_chain_busy(flamed_den_t h, int* busy);
 
 #ifdef __cplusplus
 }
