@@ -143,39 +143,6 @@ __device__ __forceinline__ bool wait_ge(int* err, int* fails, long long tmo, int
   return ok;
 }
 
-// The same wait over the groups of a bit mask (lane k < kGroups polls group k's counter when bit k is set): the
-// depthwise phase and the Euler update read rows of their neighbouring groups only (halo rows, row statistics, conv_out
-// boundary rows), so they wait for those groups instead of all eight (persist_opt 524288: all eight, round 5).
-__device__ __forceinline__ bool wait_mask(int* err, int* fails, long long tmo, int* base, int stride, unsigned mask, int target, int* flag) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    bool ok = true;
-    for (unsigned it = 0;; ++it) {
-      bool mine = true;
-      if (lane < kGroups && ((mask >> lane) & 1u))
-        mine = __hip_atomic_load(base + lane * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target;
-      else if (lane == 63) mine = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-      if (__all(mine)) break;
-      if ((it & 31) == 31) {
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) { ok = false; break; }
-        if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > tmo) {
-          if (lane == 0) raise_err(err, fails, 1);
-          ok = false;
-          break;
-        }
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0) *flag = ok ? 1 : 0;
-  }
-  __syncthreads();
-  const bool ok = *flag != 0;
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return ok;
-}
-
 // The reset prologue's grid-wide arrival: wave 0 polls a monotonic (wrapping) ticket counter until it has
 // reached `target` (no error word yet: the counter block is being reset); a timeout leaves the launch.
 __device__ __forceinline__ bool arrive_wait(unsigned* ctr, unsigned target, long long tmo, int* flag) {
@@ -723,18 +690,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   group_rows(g, T, P.B, r0, nr, P.opt);
   const int gpu = kGroups / P.B, utt = g / gpu;  // this group's utterance and its frames [ub, ue)
   const int ub = utt * T, ue = ub + T;
-  // the groups whose rows this group's depthwise window [r0 - kHalo, r0 + nr + kHalo) and Euler update (rows r0 - 1,
-  // r0 + nr) read, within its utterance, itself included
-  unsigned nbr = 0;
-  {
-    const int wa = max(r0 - kHalo, ub), wz = min(r0 + nr + kHalo, ue);
-    for (int k = 0; k < kGroups; ++k) {
-      int a, b;
-      group_rows(k, T, P.B, a, b, P.opt);
-      if (k == g || (b > 0 && a < wz && a + b > wa)) nbr |= 1u << k;
-    }
-    if (P.opt & 524288) nbr = (1u << kGroups) - 1;
-  }
   // padded batch (P.Bx): an idle utterance runs the same phases on zeros (every group still takes part in every
   // hand-off), without touching xt; its modulation row is the last real utterance's
   const bool idle = P.Bx > 0 && utt >= P.Bx;
@@ -842,11 +797,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   auto seal_wait = [&](int g0, int ng) -> bool {
     if (dseal) {
       if (wave == 0) {
-        // one load per lane: the group's 32 seals (twice), or for the neighbour waits (depthwise halo, Euler
-        // boundary rows) the seals of the two neighbouring groups whose rows this workgroup reads -- those the wait
-        // covered (nbr; another utterance's group is not waited for, so its seals may lag), else its own
-        const int gp = (g + kGroups - 1) % kGroups, gn = (g + 1) % kGroups;
-        const int gi = ng == 1 ? g0 : (lane < 32 ? ((nbr >> gp) & 1u ? gp : g) : ((nbr >> gn) & 1u ? gn : g));
+        // one load per lane: the group's 32 seals (twice), or for the all-group waits (depthwise halo, Euler
+        // boundary rows) the seals of the two neighbouring groups whose rows this workgroup reads
+        const int gi = ng == 1 ? g0 : (lane < 32 ? (g + kGroups - 1) % kGroups : (g + 1) % kGroups);
         dseal_v = __hip_atomic_load(P.seal + 4 * (gi * kSlots + (lane & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         dseal_tgt = L;
       }
@@ -1044,7 +997,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
         gbv = bw.gnb[col0 + tid];
       }
       PST(step);
-      if (!wait_mask(errw, fails, tmo, grp, 16, nbr, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }  // the neighbours' halo rows
+      if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }  // every group: the halo rows of the neighbours
       PST(step);
       // va = w (1 + sc), vb = b (1 + sc) + sh (vab's arithmetic; w = 1, b = 0 without the affine)
       float hva[4], hvb[4], ova[2][4], ovb[2][4];
@@ -1198,17 +1151,11 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
             if (tid < kCols) {
 #pragma unroll
               for (int k = 0; k < kGroups; ++k) {
-                // this utterance's groups only (another utterance's granules are masked in gn_finalize anyway, and
-                // nothing of this group's depends on that utterance's progress)
-                mv[k] = 0.f;
-                qv[k] = 0.f;
-                if (k / gpu == utt) {
-                  const unsigned long long a = __hip_atomic_load(gq + (size_t)k * H * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  const unsigned long long b = __hip_atomic_load(gq + (size_t)k * H * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  mine = mine && (unsigned)(a >> 32) == (unsigned)ndg && (unsigned)(b >> 32) == (unsigned)ndg;
-                  mv[k] = __uint_as_float((unsigned)a);
-                  qv[k] = __uint_as_float((unsigned)b);
-                }
+                const unsigned long long a = __hip_atomic_load(gq + (size_t)k * H * 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long b = __hip_atomic_load(gq + (size_t)k * H * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                mine = mine && (unsigned)(a >> 32) == (unsigned)ndg && (unsigned)(b >> 32) == (unsigned)ndg;
+                mv[k] = __uint_as_float((unsigned)a);
+                qv[k] = __uint_as_float((unsigned)b);
               }
             }
             if (__all(mine)) break;
@@ -1535,7 +1482,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
 
     // -------- Euler update x += dt * v, v[t] = b + Y1[t] + Y0[t-1] + Y2[t+1] (:445; conv3_combine order)
     PST(step);
-    if (!wait_mask(errw, fails, tmo, grp, 16, nbr, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }
+    if (!wait_ge(errw, fails, tmo, grp, 16, kGroups, 32 * L, flag) || !seal_wait(0, kGroups)) { fail_exit(); return; }
     PST(step);
     int gp = 0, gn_ = 0;  // the groups owning frames r0 - 1 and r0 + nr (nearest non-empty neighbours)
     for (int k = 0; k < kGroups; ++k) {

@@ -148,15 +148,14 @@ PERSIST_DEFAULT = 361034  # flamed_tune persist_opt default (csrc/common.hpp Tun
 
 @pytest.mark.parametrize("part", [0, 2])
 @pytest.mark.parametrize("T", [400, 131, 16])
-@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 4096, 16384, 32768, 65536, 524288])
+@pytest.mark.parametrize("flip", [64, 512, 64 | 512 | 1, 4096, 16384, 32768, 65536])
 def test_persist_variants_bitwise(pgb, T, flip, part):
     """Hand-off variants change where and how data moves, never the arithmetic: the default equals, bitwise,
     the default with row-major instead of fragment-major A images (bit 64), counter-based instead of
     tagged-granule GroupNorm exchange (bit 512), both plus the other weight-DMA wave split (bit 1), the
     hand-off drain issued behind the next weight DMA (bit 4096), the seal verification modes (bit 16384:
     every group wait also checks the producers' hand-off seals; bit 65536: the same seals loaded with the
-    phase's operands and checked a phase later), wave-local staging order (bit 32768), the depthwise phase and Euler
-    update waiting for all eight groups instead of their neighbours only (bit 524288), for full, partial-tile
+    phase's operands and checked a phase later), wave-local staging order (bit 32768), for full, partial-tile
     and nearly-empty
     row groups (rows past a group's end are stored as zeros; empty groups add nothing to the GroupNorm) -- under
     both row partitions (part: persist_opt bit 2 flipped from the default, equal shares vs whole 16-row tiles; the
@@ -483,7 +482,7 @@ def test_persist_multi_chunk_variants_bitwise(pgb, B, T):
     x0, spk = _inputs(61 + B, B, T)
     with knob("persist_multi_ntw", 5, 5):
         a = _solve(pg, x0, spk, 8)
-        for flip in (64, 512, 32768, 262144, 65536, 524288):
+        for flip in (64, 512, 32768, 262144, 65536):
             with knob("persist_opt", PERSIST_DEFAULT ^ flip, PERSIST_DEFAULT):
                 r0 = _runs(pg)
                 b = _solve(pg, x0, spk, 8)
