@@ -190,7 +190,7 @@ struct Tune {
                            // measured: B = 4 T = 400 47.4 vs 76.1 ms, B = 4 T = 300 38.6 vs 45.5, B = 8 T = 320 61.9 vs
                            // 77.3, B = 2 T = 1000 51.7 vs 76.0; B = 3 T = 400 (padded to 4) 47.5 vs 46.6
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
-  int persist_opt = 361034;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
+  int persist_opt = 885322;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange
                            // (measured per B = 1 T = 400 solve: 26.4 -> 22.8 -> 21.7 ms), 65536 = deferred hand-off
                            // seals (default-on verification, +2.5 %), 262144 = one gemm() per 64-frame chunk
@@ -199,6 +199,9 @@ struct Tune {
                            // 2 = row groups of whole 16-row tiles (default since r06c: B = 1 T = 400 20.93 -> 20.55 ms,
                            // B = 2 31.97 -> 31.43 ms; the r05 counter- vs granule-form GroupNorm divergence under it was
                            // FMA contraction in one of two inlined combines, fixed by gn_finalize);
+                           // 524288 = K-outer multi-chunk GEMM gemm_ko (default since r06x, same box: T = 2400
+                           // 130.7 -> 126.9 ms, B = 2 T = 400 28.0 -> 26.0, B = 4 T = 400 51.7 -> 46.9, T = 800
+                           // 28.2 -> 26.2, B = 8 T = 300 32.9 -> 32.0; B = 1 T <= 512 has one chunk: unaffected);
                            // A/B bits: 1 = four-wave weight DMA (round 3
                            // default; since round 5 waves 1..3 issue, so wave 0's poll never waits behind weight loads:
                            // 21.50 -> 21.18 ms), 16384 blocking seals (+12 %),

@@ -401,6 +401,86 @@ __device__ __forceinline__ void gemm_seq(const bf16* A, int r0, int nr, const ch
   for (int ci = 0; ci < NTW; ++ci) gemm<K>(A, r0, nr, wl, acc[ci], wave, lane_in, ci == 0 ? stamp : nullptr, g, frag, wave + 4 * ci, ci == 0);
 }
 
+// Several chunks, K-outer (persist_opt 524288): K-step by K-step over every tile of the wave, so each pair of B
+// fragments read from LDS feeds all NTW tiles (the panel is read once per wave per phase, not NTW times) and the
+// A fragments stream through a ring D K-steps deep (D NTW 16-B loads in flight, <= 128 VGPRs), the loads of every
+// chunk overlapping the MFMAs of every other.  Tiles past the group's last one load from outside the buffer range
+// (zeros, no memory traffic) so every K-step issues the same NTW loads.  Per tile the K-steps accumulate in the
+// same order as gemm(): bitwise the same products.
+// Ring depth (K-steps in flight) per chunk count, measured (r06y/r06z, same box, ms per solve): NTW = 5 depth 3
+// (T = 2400: 109.4-110.2 vs 110.8 at 4, 111.5 at 2, 126.9 at 6), NTW = 4 depth 5 (B = 4 T = 400: 42.9 vs 44.6 at
+// 4, 47.1 at 8, 44.9 at 6), NTW = 3 depth 8 (r06aa: T = 1500 35.4-35.7 vs 35.9 at 6, 36.7-37.0 at 4), NTW = 2
+// depth 10 (= 16); deeper rings spill.  Overridable per chunk count for A/B builds.
+#ifndef FL_KO_D2
+#define FL_KO_D2 10
+#endif
+#ifndef FL_KO_D3
+#define FL_KO_D3 8
+#endif
+#ifndef FL_KO_D4
+#define FL_KO_D4 5
+#endif
+#ifndef FL_KO_D5
+#define FL_KO_D5 3
+#endif
+template <int K, int NTW>
+__device__ __forceinline__ void gemm_ko(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[NTW][2], int wave,
+                                        int lane_in, unsigned long long* stamp, int g, bool frag) {
+  constexpr int KST = K / 32, D0 = NTW == 2 ? FL_KO_D2 : NTW == 3 ? FL_KO_D3 : NTW == 4 ? FL_KO_D4 : FL_KO_D5;
+  constexpr int D = D0 > KST ? KST : D0;
+  const int lane = opq(lane_in);
+  const int ntile = (nr + 15) >> 4;
+  const int c = lane & 15, q = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rs = frag ? rsrc(reinterpret_cast<const char*>(A) + (size_t)g * frag_group_bytes(KST), frag_group_bytes(KST))
+                                         : rsrc(A + (size_t)r0 * K, (unsigned)nr * K * 2);
+  const unsigned oob = 0x7ff00000u;
+  unsigned base[NTW];
+#pragma unroll
+  for (int ci = 0; ci < NTW; ++ci) {
+    const int tile = wave + 4 * ci;
+    base[ci] = tile >= ntile ? oob
+               : frag        ? (unsigned)(((tile * KST) * 64 + lane) * 16)
+                             : (unsigned)(((16 * tile + c) * K + q * 8) * 2);
+  }
+  const unsigned kstride = frag ? 1024u : 64u;
+  u32x4 a[D][NTW];
+#pragma unroll
+  for (int p = 0; p < D - 1; ++p)
+#pragma unroll
+    for (int ci = 0; ci < NTW; ++ci) a[p][ci] = ld16(rs, base[ci] + p * kstride);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((D - 1) * NTW) : "memory");  // this wave's (older) weight DMA landed
+  __syncthreads();  // every wave's DMA: the whole panel is in LDS
+  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // FL_STAMPS timeline only
+#pragma unroll
+  for (int ci = 0; ci < NTW; ++ci) acc[ci][0] = acc[ci][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int kBP = 4;
+  u32x4 b0[kBP], b1[kBP];
+#pragma unroll
+  for (int p = 0; p < kBP; ++p) {
+    b0[p] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * p + q));
+    b1[p] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * p + q));
+  }
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) {
+    if (ks + D - 1 < KST)
+#pragma unroll
+      for (int ci = 0; ci < NTW; ++ci) a[(ks + D - 1) % D][ci] = ld16(rs, base[ci] + (ks + D - 1) * kstride);
+    const u32x4 x0 = b0[ks % kBP], x1 = b1[ks % kBP];
+    if (ks + kBP < KST) {
+      b0[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(c, 4 * (ks + kBP) + q));
+      b1[ks % kBP] = *reinterpret_cast<const u32x4*>(wl + woff<K>(16 + c, 4 * (ks + kBP) + q));
+    }
+#pragma unroll
+    for (int ci = 0; ci < NTW; ++ci) {
+      if (wave + 4 * ci < ntile) {
+        const u32x4 av = a[ks % D][ci];
+        acc[ci][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x0), __builtin_bit_cast(bf16x8, av), acc[ci][0], 0, 0, 0);
+        acc[ci][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1), __builtin_bit_cast(bf16x8, av), acc[ci][1], 0, 0, 0);
+      }
+    }
+  }
+}
+
 // The same product with the work split 2 x 2 (persist_opt 1024): wave w = (pair p, half h) multiplies row tiles
 // 2p and 2p + 1 by K-steps [h KST/2, (h + 1) KST/2), so each B fragment read from LDS feeds two row tiles and
 // the panel is read twice per workgroup instead of four times; the two halves of tile w are then summed
@@ -929,8 +1009,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     f32x4 accm[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
     if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
+    else if (P.opt & 524288) gemm_ko<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
     else if (P.opt & 262144) gemm_seq<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
-      else gemm_multi<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
+    else gemm_multi<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
     PST(step);
 #pragma unroll
     for (int ci = 0; ci < NTW; ++ci) {
@@ -1242,6 +1323,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_c2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
       else if (P.opt & 262144) gemm_seq<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
       PST(step);
@@ -1295,6 +1377,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_c3[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
       else if (P.opt & 262144) gemm_seq<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
       PST(step);
@@ -1348,6 +1431,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_m0[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);
       else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);  // (the first tile's barrier orders the statistics)
       PST(step);
@@ -1386,6 +1470,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_m2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
       else if (P.opt & 262144) gemm_seq<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
       PST(step);
@@ -1436,7 +1521,8 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     f32x4 acco[NTW][2];  // every tile's products first: with several chunks Y goes into this phase's panel buffer
     if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
-    else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
+    else if (P.opt & 524288) gemm_ko<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
+      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
       else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
     PST(step);
     // Y of the group: [row][24] fp32 (tap-major x 8 channels) -- in the staging tile (one chunk), or in the

@@ -195,8 +195,9 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     update inside the next step's proj_in A loader (25 launches per step, state
  *                     ping-ponged through the workspace); 0: separate combine kernel (26);
  *   "persist"       — 1 (default): B = 1 bf16 solves run as one persistent cooperative launch;
- *   "persist_opt"   — persistent kernel variant bits (default 361034 = 584 + whole-16-row-tile row groups 2 +
- *                     deferred hand-off seals 65536 + per-chunk GEMMs 262144 + wave-local staging order 32768; the
+ *   "persist_opt"   — persistent kernel variant bits (default 885322 = 584 + whole-16-row-tile row groups 2 +
+ *                     deferred hand-off seals 65536 + per-chunk GEMMs 262144 + wave-local staging order 32768 +
+ *                     K-outer multi-chunk GEMMs 524288 (over 262144 when both are set); the
  *                     others are A/B variants, csrc/common.hpp);
  *   "persist_seal_skip" — diagnostic: one workgroup skips its hand-off seals in this step (-1 default =
  *                     never): a seal mode (persist_opt 16384 / 65536) must then fail the launch;

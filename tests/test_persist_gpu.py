@@ -143,7 +143,7 @@ def test_persist_knob_off_uses_launch_path(pgb):
     assert _runs(pg) == r0
 
 
-PERSIST_DEFAULT = 361034  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
+PERSIST_DEFAULT = 885322  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
 
 
 @pytest.mark.parametrize("part", [0, 2])
@@ -476,13 +476,14 @@ def test_persist_multi_chunk_variants_bitwise(pgb, B, T):
     """The multi-chunk kernel's hand-off variants change data movement only: bitwise equal to the default at
     T = 1000 (two chunks per group) and B = 2 T = 1111 (five chunks) for fragment-major off (64), counter-form
     GroupNorm (512), and -- ADVICE r5 -- the multi-chunk defaults against their alternatives: wave-local staging
-    order (32768), the per-chunk gemm() sequence vs the streamed gemm_multi (262144: same products, same order),
+    order (32768), the default K-outer gemm_ko (every tile per K-step) against the per-chunk gemm() sequence
+    (524288 off) and the streamed gemm_multi (524288 and 262144 off) -- same products, same order per tile --,
     deferred seals (65536)."""
     pg, _ = pgb
     x0, spk = _inputs(61 + B, B, T)
     with knob("persist_multi_ntw", 5, 5):
         a = _solve(pg, x0, spk, 8)
-        for flip in (64, 512, 32768, 262144, 65536):
+        for flip in (64, 512, 32768, 524288, 524288 | 262144, 65536):
             with knob("persist_opt", PERSIST_DEFAULT ^ flip, PERSIST_DEFAULT):
                 r0 = _runs(pg)
                 b = _solve(pg, x0, spk, 8)

@@ -69,7 +69,7 @@ def chain_info(L, hip):
 
 
 DEFAULTS = {"persist": 1, "persist_ntw": 5, "persist_multi": 1, "persist_pad": 1, "split_batch": 2, "split_prio": 2, "dwgn": 1, "fuse_euler": 1,
-            "persist_opt": 361034, "persist_multi_ntw": 5}
+            "persist_opt": 885322, "persist_multi_ntw": 5}
 
 if __name__ == "__main__":
     main()
