@@ -183,12 +183,15 @@ struct Tune {
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_pad = 1;     // persistent solve for B = 3 / 5..7 as B = 4 / 8 with idle utterances (persist_batch)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
-  int persist_ntw = 5;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
-  int persist_multi_ntw = 5;  // ... and for B > 1 up to this many (A/B knob).  r06c, with the round-5 epilogues, had the
+  int persist_ntw = 8;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
+  int persist_multi_ntw = 8;  // ... and for B > 1 up to this many (A/B knob).  r06c, with the round-5 epilogues, had the
                            // graph of launches ahead beyond 2 chunks (B = 4 T = 400: 60.4 ms persistent); with the
                            // transposed register epilogues (r06i) the persistent launch wins at every multi-chunk shape
                            // measured: B = 4 T = 400 47.4 vs 76.1 ms, B = 4 T = 300 38.6 vs 45.5, B = 8 T = 320 61.9 vs
-                           // 77.3, B = 2 T = 1000 51.7 vs 76.0; B = 3 T = 400 (padded to 4) 47.5 vs 46.6
+                           // 77.3, B = 2 T = 1000 51.7 vs 76.0; B = 3 T = 400 (padded to 4) 47.5 vs 46.6.  Six to eight
+                           // chunks (r06ac, K-outer GEMM; B x T <= 4096): B = 4 T = 800 73.3 vs 86.0 ms, B = 3 T = 800
+                           // 73.2 vs 78.6, B = 4 T = 1024 85.7 vs 90.5, B = 8 T = 500 85.0 vs 86.1, B = 1 T = 3000 (nfe 256)
+                           // 128.0 vs 174.0
   int persist_capmode = 0; // persistent launch inside a stream capture: 0 cooperative node, 1 plain kernel node
   int persist_opt = 885322;  // persistent kernel variant bits (pk::Params::opt): 8 = XCD-grouped grid,
                            // 64 = fragment-major GEMM A images, 512 = tagged-granule GroupNorm exchange

@@ -361,7 +361,6 @@ __global__ __launch_bounds__(kGemmThreads) void gemm_dma_kernel(AL al, const bf1
     FL_STAMP(3);
     constexpr int C4 = BN / 4, IT = BM * C4 / kGemmThreads, RPI = kGemmThreads / C4;  // rows per iteration
     static_assert(C4 == 32, "row-vectorised epilogue: a row is one half-wave of float4 columns");
-    float v[IT][4];
     float xr[IT][4];
     if constexpr (PRE) {
 #pragma unroll

@@ -423,10 +423,13 @@ __device__ __forceinline__ void gemm_seq(const bf16* A, int r0, int nr, const ch
 #ifndef FL_KO_D5
 #define FL_KO_D5 3
 #endif
+#ifndef FL_KO_D6
+#define FL_KO_D6 2  // NTW = 6..8 (B x T up to 4096)
+#endif
 template <int K, int NTW>
 __device__ __forceinline__ void gemm_ko(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[NTW][2], int wave,
                                         int lane_in, unsigned long long* stamp, int g, bool frag) {
-  constexpr int KST = K / 32, D0 = NTW == 2 ? FL_KO_D2 : NTW == 3 ? FL_KO_D3 : NTW == 4 ? FL_KO_D4 : FL_KO_D5;
+  constexpr int KST = K / 32, D0 = NTW == 2 ? FL_KO_D2 : NTW == 3 ? FL_KO_D3 : NTW == 4 ? FL_KO_D4 : NTW == 5 ? FL_KO_D5 : FL_KO_D6;
   constexpr int D = D0 > KST ? KST : D0;
   const int lane = opq(lane_in);
   const int ntile = (nr + 15) >> 4;
@@ -478,6 +481,20 @@ __device__ __forceinline__ void gemm_ko(const bf16* A, int r0, int nr, const cha
         acc[ci][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x1), __builtin_bit_cast(bf16x8, av), acc[ci][1], 0, 0, 0);
       }
     }
+  }
+}
+
+// A multi-chunk GEMM phase (NTW > 1): the K-outer gemm_ko (persist_opt 524288, default), else the per-chunk sequence
+// (262144) or the streamed gemm_multi -- A/B variants for up to five chunks only (6..8 always take gemm_ko).
+template <int K, int NTW>
+__device__ __forceinline__ void gemm_chunks(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[NTW][2], int wave,
+                                            int lane_in, unsigned long long* stamp, int g, bool frag, int opt) {
+  if constexpr (NTW > 5) {
+    gemm_ko<K, NTW>(A, r0, nr, wl, acc, wave, lane_in, stamp, g, frag);
+  } else {
+    if (opt & 524288) gemm_ko<K, NTW>(A, r0, nr, wl, acc, wave, lane_in, stamp, g, frag);
+    else if (opt & 262144) gemm_seq<K, NTW>(A, r0, nr, wl, acc, wave, lane_in, stamp, g, frag);
+    else gemm_multi<K, NTW>(A, r0, nr, wl, acc, wave, lane_in, stamp, g, frag);
   }
 }
 
@@ -1009,9 +1026,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     f32x4 accm[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
     if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
-    else if (P.opt & 524288) gemm_ko<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
-    else if (P.opt & 262144) gemm_seq<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
-    else gemm_multi<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag);
+    else gemm_chunks<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag, P.opt);
     PST(step);
 #pragma unroll
     for (int ci = 0; ci < NTW; ++ci) {
@@ -1323,9 +1338,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_c2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
-      else gemm_multi<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag);
+      else gemm_chunks<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag, P.opt);
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1377,9 +1390,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_c3[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
-      else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag);
+      else gemm_chunks<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag, P.opt);
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1431,9 +1442,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_m0[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);
-      else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag);  // (the first tile's barrier orders the statistics)
+      else gemm_chunks<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag, P.opt);  // (the first tile's barrier orders the statistics)
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1470,9 +1479,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       f32x4 accm_m2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 524288) gemm_ko<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
-      else gemm_multi<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag);
+      else gemm_chunks<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag, P.opt);
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1521,12 +1528,10 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     f32x4 acco[NTW][2];  // every tile's products first: with several chunks Y goes into this phase's panel buffer
     if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
-    else if (P.opt & 524288) gemm_ko<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
-      else if (P.opt & 262144) gemm_seq<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
-      else gemm_multi<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag);
+    else gemm_chunks<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag, P.opt);
     PST(step);
     // Y of the group: [row][24] fp32 (tap-major x 8 channels) -- in the staging tile (one chunk), or in the
-    // panel conv_out has just finished reading (several chunks: 320 x 24 x 4 B; the next panel DMA goes to the
+    // panel conv_out has just finished reading (several chunks: <= 512 x 24 x 4 B; the next panel DMA goes to the
     // other buffer, and this one is not rewritten before the next step's proj_in)
     float* yl = reinterpret_cast<float*>(NTW == 1 ? stg : smem + wb * kWPanel);
     if (NTW > 1) __syncthreads();  // every wave is done with the panel
@@ -1649,8 +1654,10 @@ static const void* const* persist_kernels() {
   static const void* const k[kMaxNTW + 1] = {
       reinterpret_cast<const void*>(den_persist_kernel<true, 1>), reinterpret_cast<const void*>(den_persist_kernel<false, 1>),
       reinterpret_cast<const void*>(den_persist_kernel<false, 2>), reinterpret_cast<const void*>(den_persist_kernel<false, 3>),
-      reinterpret_cast<const void*>(den_persist_kernel<false, 4>), reinterpret_cast<const void*>(den_persist_kernel<false, 5>)};
-  static_assert(kMaxNTW == 5, "kernel table");
+      reinterpret_cast<const void*>(den_persist_kernel<false, 4>), reinterpret_cast<const void*>(den_persist_kernel<false, 5>),
+      reinterpret_cast<const void*>(den_persist_kernel<false, 6>), reinterpret_cast<const void*>(den_persist_kernel<false, 7>),
+      reinterpret_cast<const void*>(den_persist_kernel<false, 8>)};
+  static_assert(kMaxNTW == 8, "kernel table");
   return k;
 }
 

@@ -7,7 +7,7 @@
 // default persist_opt bit 8 the XCDs form a 2 x 4 grid: the round-robin dispatch puts b on XCD x = b % 8, which
 // holds row groups 4 (x / 4) .. + 3 and slots 8 (x % 4) .. + 7 (so each weight panel is read by 2 XCDs and each
 // group's hand-off rows by 4; without bit 8, g = b % 8 and s = b / 8: one group per XCD, every panel on all 8).
-// Group g owns a contiguous range of <= 320 frames (equal shares of the utterance), processed as chunks of 64
+// Group g owns a contiguous range of <= 512 frames (equal shares of the utterance), processed as chunks of 64
 // (four 16-row MFMA tiles, one per wave; NTW chunks: a kernel variant per chunk count); slot s owns hidden
 // columns [32 s, 32 s + 32) and latent channels [8 s, 8 s + 8).  What stays on chip across phases:
 //   * the residual stream X of the workgroup's (frames x 32 columns) tile, in registers;
@@ -43,8 +43,9 @@ namespace pk {
 constexpr int kGroups = 8, kSlots = 32, kWGs = kGroups * kSlots, kThreads = 256;
 constexpr int kH = 1024, kC = 256, kCols = kH / kSlots, kCh = kC / kSlots;
 // A row group holds up to kMaxNTW chunks of kChunk = 64 frames (chunk i = 16-row tiles 4 i .. 4 i + 3, wave w owning
-// tile 4 i + w): T <= 8 x 320 = 2560 frames for one utterance (30 s at 80 Hz is 2400).
-constexpr int kChunk = 64, kMaxNTW = 5, kMaxRows = kChunk * kMaxNTW, kHalo = 15, kTaps = 31, kWin = kChunk + 2 * kHalo;
+// tile 4 i + w): B x T <= 8 x 512 = 4096 frames (one 30 s utterance at 80 Hz is 2400; the reference's metadata
+// batch of 4 at T = 1024).
+constexpr int kChunk = 64, kMaxNTW = 8, kMaxRows = kChunk * kMaxNTW, kHalo = 15, kTaps = 31, kWin = kChunk + 2 * kHalo;
 constexpr int kMaxNB = 8, kMaxT = kGroups * kMaxRows;
 // LDS carve (bytes): two weight panels, the dwconv window (aliased by the epilogue staging tile), row
 // statistics of the window, GroupNorm reduction scratch, poll flag

@@ -109,8 +109,8 @@ FLAMED_API int flamed_den_solve_chunk(flamed_den_t h, int nfe);
 FLAMED_API int flamed_den_solve_part(flamed_den_t h, float* xt, const float* mods, int nfe, int B, int T, void* ws,
                                      size_t ws_bytes, int use_graph, int s0, int s1, hipStream_t stream);
 /* The persistent solve (one launch of 256 workgroups for every step, flamed_tune "persist"; taken by
- * flamed_den_solve / _solve_part with use_graph != 0 on a bf16 handle for one utterance of 16..2560 frames,
- * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances with B x T <= 2560 (and, knob
+ * flamed_den_solve / _solve_part with use_graph != 0 on a bf16 handle for one utterance of 16..4096 frames,
+ * or -- "persist_multi", default on -- for B = 2 / 4 / 8 equal-length utterances with B x T <= 4096 (and, knob
  * "persist_pad", B = 3 / 5..7 as B = 4 / 8 with idle utterances);
  * decided once per solve by its step-0 part, and later parts follow it).  The launch is
  * cooperative (all workgroups co-resident or refused up front, then this device uses the graph of launches)
@@ -204,11 +204,11 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *   "persist_inject"— diagnostic: every persistent launch fails at this step (-1 default = never), to
  *                     exercise the NaN poisoning / failure count / retry budget;
  *   "persist_multi" — 1 (default): B = 2 / 4 / 8 equal-length utterances also run as one persistent
- *                     launch (rows per group <= 64 x persist_multi_ntw: B x T <= 2560 by default); 0: B = 1 only;
+ *                     launch (rows per group <= 64 x persist_multi_ntw: B x T <= 4096 by default); 0: B = 1 only;
  *   "persist_pad"   — 1 (default): B = 3 / 5..7 run as the B = 4 / 8 persistent launch with idle zero utterances
- *                     in the spare row groups (4 x T / 8 x T <= 2560); 0: those B take the graph of launches;
- *   "persist_ntw"   — 64-frame chunks per persistent row group, 1..5 (default 5: T <= 2560 at B = 1);
- *   "persist_multi_ntw" — ... and for B > 1, 1..5 (default 5; an A/B knob against the graph of launches);
+ *                     in the spare row groups (4 x T / 8 x T <= 4096); 0: those B take the graph of launches;
+ *   "persist_ntw"   — 64-frame chunks per persistent row group, 1..8 (default 8: T <= 4096 at B = 1);
+ *   "persist_multi_ntw" — ... and for B > 1, 1..8 (default 8; an A/B knob against the graph of launches);
  *   "persist_capmode" — persistent launch inside a stream capture: 0 (default) cooperative node, 1 plain;
  *   "coop"          — 1 (default): the persistent denoiser solve and PVA flow are cooperative launches;
  *                     0: plain launches after the same residency check (profiling runs: rocprofv3's

@@ -144,6 +144,7 @@ def test_persist_knob_off_uses_launch_path(pgb):
 
 
 PERSIST_DEFAULT = 885322  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
+NTW_DEFAULT, MULTI_NTW_DEFAULT = 8, 8  # flamed_tune persist_ntw / persist_multi_ntw defaults
 
 
 @pytest.mark.parametrize("part", [0, 2])
@@ -389,7 +390,7 @@ def test_persist_multi_counter_groupnorm(pgb, B, T, part):
     pg, sd = pgb
     x0, spk = _inputs(40 + B, B, T)
     base = PERSIST_DEFAULT ^ part
-    with knob("persist_multi", 1, 1), knob("persist_multi_ntw", 5, 5):
+    with knob("persist_multi", 1, 1), knob("persist_multi_ntw", 5, MULTI_NTW_DEFAULT):
         with knob("persist_opt", base, PERSIST_DEFAULT):
             a = _solve(pg, x0, spk, 8)
         r0 = _runs(pg)
@@ -448,17 +449,19 @@ def test_persist_padded_batch(pgb, B, T):
     assert el < 4e-3 and max(errs) < BF16_SOLVE
 
 
-@pytest.mark.parametrize("B,T", [(1, 520), (1, 1000), (1, 2400), (2, 400), (4, 300), (2, 1111)])
+@pytest.mark.parametrize("B,T", [(1, 520), (1, 1000), (1, 2400), (2, 400), (4, 300), (2, 1111),
+                                 (1, 3000), (4, 800), (3, 800), (4, 1024), (8, 500)])
 def test_persist_multi_chunk(pgb, B, T):
-    """the persistent solve beyond 64 frames per row group -- each group's rows as up to five
-    64-frame chunks (one 16-row tile per wave per chunk; a kernel variant per chunk count), so long-form
-    utterances (configs[4]: T = 2400) and B = 2 at T = 400 take one launch.  It must take the persistent path,
+    """the persistent solve beyond 64 frames per row group -- each group's rows as up
+    to eight 64-frame chunks (one 16-row tile per wave per chunk; a kernel variant per chunk count), so long-form
+    utterances (configs[4]: T = 2400), B = 2 at T = 400 and the reference's metadata batch of 4 (3) at T = 800 / 1024
+    (six to eight chunks, B x T <= 4096) take one launch.  It must take the persistent path,
     be bitwise deterministic, match the graph of launches (same bf16 operands, other fp32 order) at 4e-3 and
     every utterance the one-utterance oracle solve at the bf16 solve bar (8 steps)."""
     pg, sd = pgb
     x0, spk = _inputs(50 + B + T, B, T)
     r0 = _runs(pg)
-    with knob("persist_multi_ntw", 5, 5):  # (the default since r06i; pinned here)
+    with knob("persist_ntw", 8, NTW_DEFAULT), knob("persist_multi_ntw", 8, MULTI_NTW_DEFAULT):
         a = _solve(pg, x0, spk, 8)
         b = _solve(pg, x0, spk, 8)
     assert _runs(pg) == r0 + 2, "the multi-chunk solve did not take the persistent path"
@@ -471,17 +474,18 @@ def test_persist_multi_chunk(pgb, B, T):
     assert el < 4e-3 and max(errs) < BF16_SOLVE
 
 
-@pytest.mark.parametrize("B,T", [(1, 1000), (2, 1111)])
+@pytest.mark.parametrize("B,T", [(1, 1000), (2, 1111), (4, 800)])
 def test_persist_multi_chunk_variants_bitwise(pgb, B, T):
     """The multi-chunk kernel's hand-off variants change data movement only: bitwise equal to the default at
-    T = 1000 (two chunks per group) and B = 2 T = 1111 (five chunks) for fragment-major off (64), counter-form
+    T = 1000 (two chunks per group), B = 2 T = 1111 (five chunks) and B = 4 T = 800 (seven chunks: gemm_ko whatever
+    524288 / 262144 say) for fragment-major off (64), counter-form
     GroupNorm (512), and -- ADVICE r5 -- the multi-chunk defaults against their alternatives: wave-local staging
     order (32768), the default K-outer gemm_ko (every tile per K-step) against the per-chunk gemm() sequence
     (524288 off) and the streamed gemm_multi (524288 and 262144 off) -- same products, same order per tile --,
     deferred seals (65536)."""
     pg, _ = pgb
     x0, spk = _inputs(61 + B, B, T)
-    with knob("persist_multi_ntw", 5, 5):
+    with knob("persist_ntw", 8, NTW_DEFAULT), knob("persist_multi_ntw", 8, MULTI_NTW_DEFAULT):
         a = _solve(pg, x0, spk, 8)
         for flip in (64, 512, 32768, 524288, 524288 | 262144, 65536):
             with knob("persist_opt", PERSIST_DEFAULT ^ flip, PERSIST_DEFAULT):

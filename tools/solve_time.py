@@ -68,8 +68,8 @@ def chain_info(L, hip):
     return f", chain streams parked {pk.value} (re-created {rt.value})"
 
 
-DEFAULTS = {"persist": 1, "persist_ntw": 5, "persist_multi": 1, "persist_pad": 1, "split_batch": 2, "split_prio": 2, "dwgn": 1, "fuse_euler": 1,
-            "persist_opt": 885322, "persist_multi_ntw": 5}
+DEFAULTS = {"persist": 1, "persist_ntw": 8, "persist_multi": 1, "persist_pad": 1, "split_batch": 2, "split_prio": 2, "dwgn": 1, "fuse_euler": 1,
+            "persist_opt": 885322, "persist_multi_ntw": 8}
 
 if __name__ == "__main__":
     main()
