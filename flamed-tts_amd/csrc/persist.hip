@@ -485,11 +485,18 @@ __device__ __forceinline__ void gemm_ko(const bf16* A, int r0, int nr, const cha
 }
 
 // A multi-chunk GEMM phase (NTW > 1): the K-outer gemm_ko (persist_opt 524288, default), else the per-chunk sequence
-// (262144) or the streamed gemm_multi -- A/B variants for up to five chunks only (6..8 always take gemm_ko).
+// (262144) or the streamed gemm_multi -- A/B variants for up to five chunks only (6..8 always take gemm_ko).  Compiling
+// the alternatives out of the 2..5-chunk kernels (-DFL_KO_ONLY) changes their register allocation, not for the better:
+// T = 2400 115.0 vs 106.6 ms, B = 4 T = 400 43.6 vs 42.8, B = 2 T = 400 25.9 vs 26.0-26.5 (r06ae, same box).
 template <int K, int NTW>
 __device__ __forceinline__ void gemm_chunks(const bf16* A, int r0, int nr, const char* wl, f32x4 (&acc)[NTW][2], int wave,
                                             int lane_in, unsigned long long* stamp, int g, bool frag, int opt) {
-  if constexpr (NTW > 5) {
+#ifdef FL_KO_ONLY
+  constexpr bool only = true;
+#else
+  constexpr bool only = NTW > 5;
+#endif
+  if constexpr (only) {
     gemm_ko<K, NTW>(A, r0, nr, wl, acc, wave, lane_in, stamp, g, frag);
   } else {
     if (opt & 524288) gemm_ko<K, NTW>(A, r0, nr, wl, acc, wave, lane_in, stamp, g, frag);
