@@ -1,7 +1,7 @@
 """Time ProbGenerator solves (the denoiser's Euler loop) for given shapes under knob settings, e.g.
     python tools/solve_time.py --shapes 1x2400x256,2x400x128 --knobs persist=1 persist=0
-prints one line per (shape, knob set): median ms per solve over --reps timed solves after a warm one, and whether
-the persistent launch ran."""
+prints one line per (shape, knob set): median ms per solve over --reps timed solves after a warm one, whether
+the persistent launch ran, and whether the output equals (bitwise) the shape's first knob set's."""
 import argparse
 import os
 import statistics
@@ -37,6 +37,7 @@ def main():
         x0 = (torch.randn(B, T, 256, generator=g) * 0.3 + torch.randn(B, T, 256, generator=g)).to(dev)
         spk = torch.randn(B, 256, generator=g).to(dev)
         ts = torch.linspace(0, 1, nfe + 1, device=dev)
+        first = None
         for kn in a.knobs:
             kv = [p.split("=") for p in kn.split(",") if p]
             for k, v in kv:
@@ -52,8 +53,11 @@ def main():
                     torch.cuda.synchronize()
                     times.append((time.perf_counter() - t0) * 1e3)
                 runs = hip.persist_status()[0] - r0
+            if first is None:
+                first = ref.clone()
             print(f"B={B} T={T} nfe={nfe} [{kn or 'defaults'}]: {statistics.median(times):.2f} ms/solve "
-                  f"(min {min(times):.2f}), persistent launches {runs}/{a.reps}, finite {bool(torch.isfinite(ref).all())}"
+                  f"(min {min(times):.2f}), persistent launches {runs}/{a.reps}, finite {bool(torch.isfinite(ref).all())}, "
+                  f"equal to the first knob set {bool(torch.equal(ref, first))}"
                   f"{chain_info(L, hip)}", flush=True)
             for k, _ in kv:  # back to the process defaults of the Tune struct
                 nat.check(L.flamed_tune(k.encode(), defaults.setdefault(k, DEFAULTS.get(k, 0))), "tune")
