@@ -633,6 +633,8 @@ __device__ __forceinline__ void store_op_t(bf16* dst, int g, int s, int tile, co
       const unsigned off = (unsigned)(((tile * KST + s) * 64 + c + 16 * (2 * nt + (q >> 1))) * 16 + (q & 1) * 8);
       __builtin_amdgcn_raw_buffer_store_b64(piece[nt], rs, off, 0, 16);
     }
+    // (r06aj: swapping halves between lanes q and q ^ 1 for one 16-B store per lane measured no faster at B = 1 and
+    // 4 % slower at T = 2400, profiles/r06aj_op16_ab.txt)
   } else if (live) {
     const __amdgpu_buffer_rsrc_t rs = rsrc(dst, (unsigned)TT * kH * 2);
 #pragma unroll
