@@ -409,14 +409,15 @@ __device__ __forceinline__ void gemm_seq(const bf16* A, int r0, int nr, const ch
 // same order as gemm(): bitwise the same products.
 // Ring depth (K-steps in flight) per chunk count, measured (r06y/r06z, same box, ms per solve): NTW = 5 depth 3
 // (T = 2400: 109.4-110.2 vs 110.8 at 4, 111.5 at 2, 126.9 at 6), NTW = 4 depth 5 (B = 4 T = 400: 42.9 vs 44.6 at
-// 4, 47.1 at 8, 44.9 at 6), NTW = 3 depth 8 (r06aa: T = 1500 35.4-35.7 vs 35.9 at 6, 36.7-37.0 at 4), NTW = 2
+// 4, 47.1 at 8, 44.9 at 6), NTW = 3 depth 7 (r06an: T = 1500 35.05-35.09 ms vs 35.6-36.0 at 8, 37.7-37.9 at 10; r06aa: 8 vs 35.9 at 6,
+// 36.7-37.0 at 4), NTW = 2
 // depth 8 (r06ag / r06ah: B = 2 T = 400 25.3-25.7 ms vs 26.2 at 10 and 7, 25.7-25.9 at 9, 26.6-26.7 at 6),
 // NTW = 6..8 depth 2 (r06ad: 3 is 4-5 % slower); deeper rings spill.  Overridable per chunk count for A/B builds.
 #ifndef FL_KO_D2
 #define FL_KO_D2 8
 #endif
 #ifndef FL_KO_D3
-#define FL_KO_D3 8
+#define FL_KO_D3 7
 #endif
 #ifndef FL_KO_D4
 #define FL_KO_D4 5
