@@ -91,7 +91,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"split_prio", &Tune::split_prio, 0, 2, nullptr},
       {"prio_all", &Tune::prio_all, 0, 1, nullptr},
       {"split_min_rows", &Tune::split_min_rows, 1024, 1 << 30, nullptr},
-      {"persist_opt", &Tune::persist_opt, 0, (1 << 21) - 1, nullptr},
+      {"persist_opt", &Tune::persist_opt, 0, 1 << 20, nullptr},
       {"persist_seal_skip", &Tune::persist_seal_skip, -1, 1 << 20, nullptr},
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
       {"persist_multi", &Tune::persist_multi, 0, 1, nullptr},

@@ -208,8 +208,9 @@ struct Tune {
                            // A/B bits: 1 = four-wave weight DMA (round 3
                            // default; since round 5 waves 1..3 issue, so wave 0's poll never waits behind weight loads:
                            // 21.50 -> 21.18 ms), 16384 blocking seals (+12 %),
-                           // 1024 2 x 2 wave split, 4096 drain behind the DMA, 1048576 the GEMM phases' deferred seal
-                           // loads issued after the GEMM and checked one phase later (r06ap: no difference)
+                           // 1024 2 x 2 wave split, 4096 drain behind the DMA.  Removed after measuring: the GEMM
+                           // phases' deferred seal loads issued after the GEMM (r06ap neutral as a bit, but its code
+                           // slowed the default kernel 2-5 %, r06ar)
   int pva_split = 0;       // PVA nets: split-K of their small-M fp32 GEMMs (fixed slice order); measured
                            // neutral (L = 60 / 247, 64 steps: 2.70 / 2.94 vs 2.61 / 2.92 ms), so off
   int pva_persist = 1;     // PVA flow: both nets, every step, one persistent launch (pvaflow.hpp; B*L <= 640)

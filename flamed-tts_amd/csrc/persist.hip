@@ -889,22 +889,9 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
   // waited for -- detection without a round trip on the hand-off chain
   const bool dseal = (P.opt & 65536) != 0;
   int dseal_v = 0x7fffffff, dseal_tgt = 0;  // wave 0: min of the seals loaded at the last wait, and its target
-  // persist_opt 1048576 (A/B, off: no difference measured, profiles/r06ap_late_seals_ab.txt): at the GEMM phases' waits
-  // the seal loads are issued after the GEMM (behind its A loads in wave 0's queue, not ahead of them) and every
-  // seal_put checks the seals loaded one phase earlier
-  const bool dseal_late = dseal && (P.opt & 1048576) != 0;
-  int dseal_g = -1;
-  // late mode: each seal_put checks the seals loaded one phase earlier (dseal_v2), so the load is never waited for
-  int dseal_v2 = 0x7fffffff, dseal_tgt2 = 0;
   auto dseal_check = [&]() {
     if (dseal && wave == 0) {
-      const bool ok = dseal_late ? __all(dseal_v2 >= dseal_tgt2) : __all(dseal_v >= dseal_tgt);
-      if (dseal_late) {
-        dseal_v2 = dseal_v;
-        dseal_tgt2 = dseal_tgt;
-        dseal_v = 0x7fffffff;
-        dseal_tgt = 0;
-      }
+      const bool ok = __all(dseal_v >= dseal_tgt);
       if (!ok && lane == 0) raise_err(errw, fails, 4);
       return ok;
     }
@@ -915,20 +902,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if ((seal || dseal) && tid == 0 && !(cur_step == P.seal_skip && blockIdx.x == 5))
       __hip_atomic_store(P.seal + 4 * (g * kSlots + s), L + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  auto seal_issue = [&]() {
-    if (dseal_late && dseal_g >= 0) {
-      if (wave == 0) {
-        dseal_v = __hip_atomic_load(P.seal + 4 * (dseal_g * kSlots + (lane & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dseal_tgt = L;
-      }
-      dseal_g = -1;
-    }
-  };
-  auto seal_wait = [&](int g0, int ng, bool gemm_next = false) -> bool {
-    if (dseal_late && gemm_next && ng == 1) {
-      dseal_g = g0;
-      return true;
-    }
+  auto seal_wait = [&](int g0, int ng) -> bool {
     if (dseal) {
       if (wave == 0) {
         // one load per lane: the group's 32 seals (twice), or for the all-group waits (depthwise halo, Euler
@@ -1058,13 +1032,12 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     float binv[2][4];  // epilogue vectors of the lane's columns (transposed layout), before the wait
     ld_cols(binv, P.bin + col0, q);
     PST(step);
-    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1, true)) { fail_exit(); return; }
+    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
     f32x4 accm[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
     if constexpr (KH) gemm_kh<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kC>(P.xs, r0, nr, (smem + wb * kWPanel), accm[0], wave, lane, PSTP(step), g, frag);
     else gemm_chunks<kC, NTW>(P.xs, r0, nr, (smem + wb * kWPanel), accm, wave, lane, PSTP(step), g, frag, P.opt);
-    seal_issue();
     PST(step);
 #pragma unroll
     for (int ci = 0; ci < NTW; ++ci) {
@@ -1371,13 +1344,12 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       float b2v[2][4];  // epilogue vectors before the wait
       ld_cols(b2v, bw.b2 + col0, q);
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1, true)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
       f32x4 accm_c2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2[0], wave, lane, PSTP(step), g, frag);
       else gemm_chunks<kH, NTW>(P.a2, r0, nr, (smem + wb * kWPanel), accm_c2, wave, lane, PSTP(step), g, frag, P.opt);
-      seal_issue();
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1420,7 +1392,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if (fin) fill_cols(alw, 1.0f);
       else ld_cols(alw, bw.lnmw + col0, q);
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1, true)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
@@ -1430,7 +1402,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3[0], wave, lane, PSTP(step), g, frag);
       else gemm_chunks<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_c3, wave, lane, PSTP(step), g, frag, P.opt);
-      seal_issue();
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1474,7 +1445,7 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       ld_cols(fa0, fo0 + col0, q);
       ld_cols(fb0, fo0 + H + col0, q);
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1, true)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
       // the epilogue's row statistics of x (conv_3's partials) before the GEMM (issued between the GEMM's A loads and
       // their wait instead, r06j measured 20.84 vs 20.63 ms per B = 1 solve: slower)
@@ -1483,7 +1454,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0[0], wave, lane, PSTP(step), g, frag);
       else gemm_chunks<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), accm_m0, wave, lane, PSTP(step), g, frag, P.opt);  // (the first tile's barrier orders the statistics)
-      seal_issue();
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1515,13 +1485,12 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       ld_cols(g2v, mb + 5 * H + col0, q);
       ld_cols(bm2, bw.mb2 + col0, q);
       PST(step);
-      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1, true)) { fail_exit(); return; }
+      if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
       PST(step);
       f32x4 accm_m2[NTW][2];  // every tile's products (several chunks: one streamed pass, epilogues after it)
       if constexpr (KH) gemm_kh<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
       else if constexpr (NTW == 1) gemm<kH>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2[0], wave, lane, PSTP(step), g, frag);
       else gemm_chunks<kH, NTW>(P.u, r0, nr, (smem + wb * kWPanel), accm_m2, wave, lane, PSTP(step), g, frag, P.opt);
-      seal_issue();
       PST(step);
 #pragma unroll
       for (int ci = 0; ci < NTW; ++ci) {
@@ -1564,14 +1533,13 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
       }
     }
     PST(step);
-    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1, true)) { fail_exit(); return; }
+    if (!wait_ge(errw, fails, tmo, mygrp, 0, 1, 32 * L, flag) || !seal_wait(g, 1)) { fail_exit(); return; }
     PST(step);
     row_stats(P.xpart[1], TT, r0, r0 + nr, r0 - kHalo, st);
     f32x4 acco[NTW][2];  // every tile's products first: with several chunks Y goes into this phase's panel buffer
     if constexpr (KH) gemm_kh<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
     else if constexpr (NTW == 1) gemm<kH>(P.xa, r0, nr, (smem + wb * kWPanel), acco[0], wave, lane, PSTP(step), g, frag);
     else gemm_chunks<kH, NTW>(P.xa, r0, nr, (smem + wb * kWPanel), acco, wave, lane, PSTP(step), g, frag, P.opt);
-    seal_issue();
     PST(step);
     // Y of the group: [row][24] fp32 (tap-major x 8 channels) -- in the staging tile (one chunk), or in the
     // panel conv_out has just finished reading (several chunks: <= 512 x 24 x 4 B; the next panel DMA goes to the
@@ -1662,7 +1630,6 @@ __global__ __launch_bounds__(kThreads, 1) void den_persist_kernel(Params P) {
     if (tid == 0) *okf = 1;
     __syncthreads();
     if (!dseal_check() && lane == 0) *okf = 0;
-    if (dseal_late && !dseal_check() && lane == 0) *okf = 0;  // late mode: the last phase's seals too
     __syncthreads();
     if (*okf == 0) { fail_exit(); return; }
   }

@@ -335,13 +335,12 @@ def test_solve_part_without_step0_rejected(pgb):
     assert rc == 1001
 
 
-@pytest.mark.parametrize("bit", [16384, 65536, 65536 | 1048576])
+@pytest.mark.parametrize("bit", [16384, 65536])
 def test_persist_seal_mode_cfg1(pgb, bit):
     """the configs[1] solve with every group hand-off sealed: each producer stores
     its hand-off number write-through ahead of the drain that precedes its counter add, and every consumer checks
     the seals of all the producers it reads -- after its counter wait, spinning on a lagging one (bit 16384), or
-    loaded with the phase's operands and checked a phase later (bit 65536, no round trip on the chain; with bit
-    1048576 a GEMM phase's seal loads go out after its GEMM and are checked one seal_put later).  No seal
+    loaded with the phase's operands and checked a phase later (bit 65536, no round trip on the chain).  No seal
     may lag its counter (a lag fails the launch with error 4 and NaN), and the result equals the unsealed solve
     bitwise."""
     pg, _ = pgb
@@ -357,7 +356,7 @@ def test_persist_seal_mode_cfg1(pgb, bit):
     assert torch.isfinite(b).all() and torch.equal(a, b)
 
 
-@pytest.mark.parametrize("bit", [16384, 65536, 65536 | 1048576])
+@pytest.mark.parametrize("bit", [16384, 65536])
 def test_persist_seal_lag_detected(pgb, bit):
     """The seal modes catch a hand-off whose producer did not seal it (diagnostic knob persist_seal_skip: one
     workgroup skips its seal stores in step 3): the launch fails (NaN-poisoned x, failure counted) instead of
