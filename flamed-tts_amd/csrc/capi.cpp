@@ -96,6 +96,7 @@ int tune_apply(Tune& t, const char* key, int value) {
       {"persist_inject", &Tune::persist_inject, -1, 1 << 20, nullptr},
       {"persist_multi", &Tune::persist_multi, 0, 1, nullptr},
       {"persist_pad", &Tune::persist_pad, 0, 1, nullptr},
+      {"persist_pad_ntw", &Tune::persist_pad_ntw, 1, 8, nullptr},
       {"persist_multi_ntw", &Tune::persist_multi_ntw, 1, 8, nullptr},
       {"persist_ntw", &Tune::persist_ntw, 1, 8, nullptr},
       {"persist_capmode", &Tune::persist_capmode, 0, 1, nullptr},

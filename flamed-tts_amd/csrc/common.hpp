@@ -182,6 +182,10 @@ struct Tune {
   int persist_seal_skip = -1;  // diagnostic: one workgroup skips its hand-off seals in this step (seal modes must fail)
   int persist_inject = -1; // diagnostic: every persistent launch fails at this step (-1 = never)
   int persist_pad = 1;     // persistent solve for B = 3 / 5..7 as B = 4 / 8 with idle utterances (persist_batch)
+  int persist_pad_ntw = 4; // ... and a batch padded to >= 1.5x its size (B = 5 as 8) only up to this many chunks per row
+                           // group: the idle utterances cost whole chunks (r06au / r06av: B = 5 T = 500, eight chunks,
+                           // 84.5 ms vs 80.8 on the graph of launches, B = 5 T = 300, five chunks, 53.5 vs 50.0; B = 6 T = 300 52.7 vs 74.3, B = 3 T = 400 42.4 vs 46.6, B = 7
+                           // T = 256 44.9 vs 72.6, B = 3 T = 800 (seven chunks) 73.2 vs 78.6 stay persistent)
   int persist_multi = 1;   // persistent solve also for B = 2 / 4 / 8 utterances (each group inside one utterance)
   int persist_ntw = 8;     // persistent solve up to this many 64-frame chunks per row group (1: T <= 512 per utterance)
   int persist_multi_ntw = 8;  // ... and for B > 1 up to this many (A/B knob).  r06c, with the round-5 epilogues, had the

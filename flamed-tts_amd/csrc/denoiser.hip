@@ -2591,9 +2591,12 @@ static bool persist_eligible(Den* d, int B, int T) {
   if (d->H != pk::kH || d->C != pk::kC || d->NB > pk::kMaxNB || d->KS != pk::kTaps || T < 16) return false;
   // one utterance, or (knob persist_multi) B in {2, 4, 8}, each utterance's frames split over its 8 / B row groups;
   // a group holds up to kMaxNTW chunks of 64 frames (kernel variant by chunk count; knob persist_ntw caps it)
+  const int B0 = B;
   if (B != 1 && tu.persist_multi && tu.persist_pad) B = persist_batch(B);
   if (B != 1 && (!tu.persist_multi || (B != 2 && B != 4 && B != 8))) return false;
   const int ntw = pk::persist_ntw(B, T, tu.persist_opt);
+  // padded to at least 1.5x the batch (B = 5 as 8): the idle utterances cost whole chunks, so only up to persist_pad_ntw
+  if (B != B0 && 2 * B >= 3 * B0 && ntw > tu.persist_pad_ntw) return false;
   if (ntw > pk::kMaxNTW || ntw > tu.persist_ntw || ((tu.persist_opt & 1024) && ntw != 1)) return false;
   if (B > 1 && ntw > tu.persist_multi_ntw) return false;  // several utterances: the graph path is faster beyond 2 chunks
   if (d->pdev_ok < 0) d->pdev_ok = pk::persist_device_ok(d->device) ? 1 : 0;

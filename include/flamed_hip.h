@@ -207,6 +207,8 @@ FLAMED_API int flamed_den_time_kernels_graph(flamed_den_t h, float* xt, const fl
  *                     launch (rows per group <= 64 x persist_multi_ntw: B x T <= 4096 by default); 0: B = 1 only;
  *   "persist_pad"   — 1 (default): B = 3 / 5..7 run as the B = 4 / 8 persistent launch with idle zero utterances
  *                     in the spare row groups (4 x T / 8 x T <= 4096); 0: those B take the graph of launches;
+ *   "persist_pad_ntw" — ... and a batch padded to >= 1.5x its size (B = 5 as 8) only while it needs at most this
+ *                     many 64-frame chunks per row group, 1..8 (default 4: B = 5 up to T = 256);
  *   "persist_ntw"   — 64-frame chunks per persistent row group, 1..8 (default 8: T <= 4096 at B = 1);
  *   "persist_multi_ntw" — ... and for B > 1, 1..8 (default 8; an A/B knob against the graph of launches);
  *   "persist_capmode" — persistent launch inside a stream capture: 0 (default) cooperative node, 1 plain;

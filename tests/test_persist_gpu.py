@@ -141,6 +141,15 @@ def test_persist_knob_off_uses_launch_path(pgb):
     x9, spk9 = _inputs(10, 9, 64)  # B = 9: beyond 8 row groups, never persistent
     _solve(pg, x9, spk9, 4)
     assert _runs(pg) == r0
+    x5, spk5 = _inputs(11, 5, 500)  # B = 5 padded to 8 would need eight chunks (> persist_pad_ntw): graph of launches
+    _solve(pg, x5, spk5, 4)
+    assert _runs(pg) == r0
+    x5, spk5 = _inputs(12, 5, 300)  # ... and five (> persist_pad_ntw 4): graph of launches too
+    _solve(pg, x5, spk5, 4)
+    assert _runs(pg) == r0
+    x5, spk5 = _inputs(13, 5, 200)  # four chunks: persistent
+    _solve(pg, x5, spk5, 4)
+    assert _runs(pg) == r0 + 1
 
 
 PERSIST_DEFAULT = 885322  # flamed_tune persist_opt default (csrc/common.hpp Tune::persist_opt)
